@@ -1,0 +1,46 @@
+// am_internal.h -- shared internals of libantidote_mat (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <vector>
+
+#include "../../include/antidote_mat.h"
+
+struct am_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int n_cu = 256;
+};
+
+struct am_store {
+  am_ctx *ctx = nullptr;
+  am_op_log dev{};               // device view
+  std::vector<void *> allocs;    // owned device allocations
+};
+
+void am_set_error(const char *fmt, ...);
+
+#define AM_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      am_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+      return AM_ERR_HIP;                                                              \
+    }                                                                                 \
+  } while (0)
+
+// ops are padded so every per-op array can be read in groups of 4 (32 B of u64)
+static constexpr uint64_t AM_OP_PAD = 256;
+static inline uint64_t am_round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+// internal launchers (am_materialize.hip, am_gst.hip, am_synth.hip)
+int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
+int am_launch_gst_local_min(am_ctx *ctx, uint32_t n_dc, uint32_t n_part, const uint64_t *part_vc,
+                            const uint32_t *part_pres, const uint8_t *part_undef, uint64_t *lanes);
+int am_launch_gst_finalize(am_ctx *ctx, uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc,
+                           uint32_t *last_pres, int gr, uint64_t *out_vc, uint32_t *out_pres,
+                           uint8_t *changed);
+int am_launch_synth(am_ctx *ctx, const am_synth_params *p, am_op_log *L /* device arrays allocated */);

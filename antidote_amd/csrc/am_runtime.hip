@@ -1,0 +1,247 @@
+// am_runtime.hip -- context, device memory, op-log stores, timers and the C ABI
+// entry points of libantidote_mat.so (declared in include/antidote_mat.h).
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "am_internal.h"
+
+static thread_local char g_err[512] = {0};
+
+void am_set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" {
+
+int am_abi_version(void) { return AM_ABI_VERSION; }
+const char *am_last_error(void) { return g_err; }
+
+int am_ctx_open(int device, am_ctx **out) {
+  if (!out) return AM_ERR_INVALID;
+  int ndev = 0;
+  AM_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) {
+    am_set_error("device %d out of range (%d devices)", device, ndev);
+    return AM_ERR_INVALID;
+  }
+  AM_HIP(hipSetDevice(device));
+  am_ctx *c = new am_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  AM_HIP(hipGetDeviceProperties(&prop, device));
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  AM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  AM_HIP(hipEventCreate(&c->ev0));
+  AM_HIP(hipEventCreate(&c->ev1));
+  *out = c;
+  return AM_OK;
+}
+
+int am_ctx_close(am_ctx *c) {
+  if (!c) return AM_OK;
+  AM_HIP(hipSetDevice(c->device));
+  AM_HIP(hipStreamSynchronize(c->stream));
+  (void)hipEventDestroy(c->ev0);
+  (void)hipEventDestroy(c->ev1);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return AM_OK;
+}
+
+void *am_ctx_stream(am_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int am_ctx_sync(am_ctx *c) {
+  if (!c) return AM_ERR_INVALID;
+  AM_HIP(hipStreamSynchronize(c->stream));
+  return AM_OK;
+}
+
+int am_timer_start(am_ctx *c) {
+  if (!c) return AM_ERR_INVALID;
+  AM_HIP(hipEventRecord(c->ev0, c->stream));
+  return AM_OK;
+}
+
+int am_timer_stop(am_ctx *c, float *ms) {
+  if (!c || !ms) return AM_ERR_INVALID;
+  AM_HIP(hipEventRecord(c->ev1, c->stream));
+  AM_HIP(hipEventSynchronize(c->ev1));
+  AM_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return AM_OK;
+}
+
+int am_dev_alloc(am_ctx *c, size_t bytes, void **out) {
+  if (!c || !out) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(c->device));
+  void *p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    am_set_error("hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return AM_ERR_NOMEM;
+  }
+  *out = p;
+  return AM_OK;
+}
+
+int am_dev_free(am_ctx *c, void *p) {
+  if (!c) return AM_ERR_INVALID;
+  if (p) AM_HIP(hipFree(p));
+  return AM_OK;
+}
+
+int am_memcpy_h2d(am_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return AM_ERR_INVALID;
+  if (!bytes) return AM_OK;
+  AM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  AM_HIP(hipStreamSynchronize(c->stream));
+  return AM_OK;
+}
+
+int am_memcpy_d2h(am_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return AM_ERR_INVALID;
+  if (!bytes) return AM_OK;
+  AM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  AM_HIP(hipStreamSynchronize(c->stream));
+  return AM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- stores
+static int store_alloc(am_store *st, size_t bytes, void **out) {
+  void *p = nullptr;
+  int rc = am_dev_alloc(st->ctx, bytes, &p);
+  if (rc) return rc;
+  st->allocs.push_back(p);
+  *out = p;
+  return AM_OK;
+}
+
+template <typename T>
+static int upload(am_store *st, const T *src, uint64_t n, uint64_t n_alloc, const T **dst) {
+  if (!src) {
+    *dst = nullptr;
+    return AM_OK;
+  }
+  void *p = nullptr;
+  int rc = store_alloc(st, n_alloc * sizeof(T), &p);
+  if (rc) return rc;
+  AM_HIP(hipMemsetAsync(p, 0, n_alloc * sizeof(T), st->ctx->stream));
+  if (n) AM_HIP(hipMemcpyAsync(p, src, n * sizeof(T), hipMemcpyHostToDevice, st->ctx->stream));
+  *dst = (const T *)p;
+  return AM_OK;
+}
+
+extern "C" {
+
+int am_store_destroy(am_store *st) {
+  if (!st) return AM_OK;
+  (void)hipSetDevice(st->ctx->device);
+  (void)hipStreamSynchronize(st->ctx->stream);
+  for (void *p : st->allocs) (void)hipFree(p);
+  delete st;
+  return AM_OK;
+}
+
+int am_store_create(am_ctx *c, const am_op_log *h, am_store **out) {
+  if (!c || !h || !out || !h->key_off || !h->key_type || !h->op_meta || !h->commit_time || !h->p0) {
+    am_set_error("am_store_create: missing required arrays");
+    return AM_ERR_INVALID;
+  }
+  if (h->n_dc == 0 || h->n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  if (h->n_dc && h->n_ops && !h->snap_vc) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(c->device));
+  am_store *st = new am_store();
+  st->ctx = c;
+  const uint64_t n_ops = h->n_ops, n_keys = h->n_keys;
+  const uint64_t na = am_round_up(n_ops, AM_OP_PAD) + AM_OP_PAD;  // padded so tiles can over-read
+  am_op_log &d = st->dev;
+  d.n_dc = h->n_dc;
+  d.n_keys = n_keys;
+  d.n_ops = n_ops;
+  d.n_var = h->n_var;
+  d.snap_stride = na;
+  int rc = AM_OK;
+#define UP(field, cnt, cnt_alloc) \
+  if (!rc) rc = upload(st, h->field, cnt, cnt_alloc, &d.field)
+  UP(key_off, n_keys + 1, n_keys + 1);
+  UP(key_id_base, n_keys, n_keys);
+  UP(key_type, n_keys, n_keys);
+  UP(key_flags, n_keys, n_keys);
+  UP(op_meta, n_ops, na);
+  UP(commit_time, n_ops, na);
+  UP(snap_pres, n_ops, na);
+  UP(op_txid, n_ops, na);
+  UP(op_id, n_ops, na);
+  UP(p0, n_ops, na);
+  UP(p1, n_ops, na);
+  UP(var_off, h->var_off ? n_ops + 1 : 0, n_ops + 1);
+  UP(var_data, h->n_var, h->n_var + 4);
+#undef UP
+  if (!rc && h->snap_vc) {
+    void *p = nullptr;
+    rc = store_alloc(st, (size_t)h->n_dc * na * sizeof(uint64_t), &p);
+    if (!rc) {
+      const uint64_t hs = h->snap_stride ? h->snap_stride : n_ops;
+      AM_HIP(hipMemsetAsync(p, 0, (size_t)h->n_dc * na * sizeof(uint64_t), c->stream));
+      if (n_ops)
+        AM_HIP(hipMemcpy2DAsync(p, na * sizeof(uint64_t), h->snap_vc, hs * sizeof(uint64_t),
+                                n_ops * sizeof(uint64_t), h->n_dc, hipMemcpyHostToDevice, c->stream));
+      d.snap_vc = (const uint64_t *)p;
+    }
+  }
+  if (!rc) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      am_set_error("store upload: %s", hipGetErrorString(e));
+      rc = AM_ERR_HIP;
+    }
+  }
+  if (rc) {
+    am_store_destroy(st);
+    return rc;
+  }
+  *out = st;
+  return AM_OK;
+}
+
+int am_store_log(const am_store *st, am_op_log *out) {
+  if (!st || !out) return AM_ERR_INVALID;
+  *out = st->dev;
+  return AM_OK;
+}
+
+// ---------------------------------------------------------------- hot path
+int am_materialize(am_ctx *c, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+  if (!c) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(c->device));
+  return am_launch_materialize(c, L, B, R);
+}
+
+uint32_t am_key_partition(int64_t key, uint32_t n_partitions) {
+  if (n_partitions == 0) return 0;
+  const uint64_t a = key < 0 ? (uint64_t)(-(key + 1)) + 1 : (uint64_t)key;  // abs without UB
+  return (uint32_t)(a % n_partitions);
+}
+
+// ---------------------------------------------------------------- GST
+int am_gst_local_min(am_ctx *c, uint32_t n_dc, uint32_t n_part, const uint64_t *part_vc, const uint32_t *part_pres,
+                     const uint8_t *part_undef, uint64_t *lanes) {
+  if (!c || !lanes || n_dc == 0 || n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(c->device));
+  return am_launch_gst_local_min(c, n_dc, n_part, part_vc, part_pres, part_undef, lanes);
+}
+
+int am_gst_finalize(am_ctx *c, uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres, int gr,
+                    uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed) {
+  if (!c || !lanes || !last_vc || !last_pres || !out_vc || !out_pres || n_dc == 0 || n_dc > AM_MAX_DC)
+    return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(c->device));
+  return am_launch_gst_finalize(c, n_dc, lanes, last_vc, last_pres, gr, out_vc, out_pres, changed);
+}
+
+}  // extern "C"

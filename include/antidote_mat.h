@@ -1,0 +1,277 @@
+/*
+ * antidote_mat.h -- C ABI of the MI355X batched CRDT snapshot materializer.
+ *
+ * Drop-in boundary for the AntidoteDB Cure/ClockSI snapshot-read hot path.
+ * Every entry point names the reference interface it replaces (paths are
+ * relative to the reference tree, SmallEndian/antidote):
+ *
+ *   am_materialize          clocksi_materializer:materialize/4
+ *                           (src/clocksi_materializer.erl:82-101), batched over keys;
+ *                           called from materializer_vnode:materialize_snapshot/7
+ *                           (src/materializer_vnode.erl:469-509, call at :478)
+ *   am_store_create         the per-partition ETS ops cache laid out in HBM
+ *                           (materializer_vnode:op_insert_gc/3 appends,
+ *                           src/materializer_vnode.erl:622-647; tuple layout
+ *                           include/antidote.hrl:81-90)
+ *   am_gst_local_min        stable_time_functions:get_min_time/1 over the local
+ *                           partitions (src/stable_time_functions.erl:51-85)
+ *   am_gst_allreduce        the node-to-node broadcast + merge of meta_data_sender
+ *                           (src/meta_data_sender.erl:232-255) as one RCCL min
+ *                           all-reduce over xGMI
+ *   am_gst_finalize         meta_data_sender:update_stable/3 with
+ *                           stable_time_functions:update_func_min/2
+ *                           (src/meta_data_sender.erl:342-356,
+ *                           src/stable_time_functions.erl:42-48) and the gr-mode
+ *                           broadcast of dc_utilities:get_stable_snapshot/0
+ *                           (src/dc_utilities.erl:246-279)
+ *   am_key_partition        log_utilities:get_key_partition/1 for integer keys
+ *                           (src/log_utilities.erl:60-79,100-118)
+ *
+ * Conventions
+ *   - Plain C, POD structure-of-arrays, no framework types.  Status codes
+ *     mirror the reference's error conventions: {error, {unexpected_operation,
+ *     Effect, Type}} (src/materializer.erl:52-58) and
+ *     erlang:error(corrupted_ops_cache) (src/clocksi_materializer.erl:190-191).
+ *   - A vectorclock (a dict DcId -> time in the reference, hex vectorclock 0.1.0)
+ *     is a dense array of n_dc u64 lanes plus a presence bitmask (bit d set =
+ *     DC d is a key of the dict).  DC ids are mapped by the caller to indices
+ *     0..n_dc-1 in ascending Erlang term order (so sorted [{Dc, T}] renderings
+ *     match).  n_dc <= AM_MAX_DC.
+ *   - "ignore" (an atom in the reference) is an explicit flag.
+ *   - Device entry points take DEVICE pointers and run asynchronously on the
+ *     context's HIP stream; the *_host variants take host memory and block.
+ */
+#ifndef ANTIDOTE_MAT_H
+#define ANTIDOTE_MAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AM_ABI_VERSION 1
+#define AM_MAX_DC 32
+
+/* CRDT types (the reference's type atoms) */
+enum am_type {
+  AM_PN = 1,        /* antidote_crdt_counter_pn   */
+  AM_LWW = 2,       /* antidote_crdt_register_lww */
+  AM_AWSET = 3,     /* antidote_crdt_set_aw       */
+  AM_MVREG = 4,     /* antidote_crdt_register_mv  */
+  AM_BCOUNTER = 5   /* antidote_crdt_counter_b    */
+};
+
+/* Per-read status.  >0: the reference's {error, _} / exception outcomes. <0: API errors. */
+enum am_status {
+  AM_OK = 0,
+  AM_ERR_CORRUPTED_OPS_CACHE = 1,   /* erlang:error(corrupted_ops_cache)            */
+  AM_ERR_UNEXPECTED_OPERATION = 2,  /* {error, {unexpected_operation, Effect, Type}}*/
+  AM_ERR_OVERFLOW = 3,              /* result outside int64 (Erlang would bignum)   */
+  AM_ERR_CAPACITY = 4,              /* set result larger than the caller's capacity */
+  AM_ERR_INVALID = -1,
+  AM_ERR_HIP = -2,
+  AM_ERR_RCCL = -3,
+  AM_ERR_NOMEM = -4,
+  AM_ERR_UNSUPPORTED = -5
+};
+
+/* per-read informational flags */
+#define AM_FLAG_MISSING_DC_LOGGED 0x1u  /* logger:error("Could not find DC in SS"), src/clocksi_materializer.erl:246 */
+
+/* op_meta byte: commit DC index, effect sub-kind, invalid-effect marker */
+#define AM_META_DC(m) ((unsigned)(m)&0x1Fu)
+#define AM_META_KIND(m) (((unsigned)(m) >> 5) & 0x3u)
+#define AM_META_BAD 0x80u /* Type:update/2 raises on this effect */
+#define AM_MAKE_META(dc, kind, bad) ((uint8_t)(((dc)&0x1F) | (((kind)&3) << 5) | ((bad) ? 0x80 : 0)))
+
+/* effect sub-kinds */
+#define AM_MV_ASSIGN 0 /* {Value, Token, Overridden}  */
+#define AM_MV_RESET 1  /* {reset, Overridden}         */
+#define AM_BC_INCREMENT 0 /* {{increment, V}, Id}      -> P[{Id,Id}] += V   */
+#define AM_BC_DECREMENT 1 /* {{decrement, V}, Id}      -> D[Id] += V        */
+#define AM_BC_TRANSFER 2  /* {{transfer, V, To}, From} -> P[{From,To}] += V */
+
+/* key_flags */
+#define AM_KEY_MIXED_TYPES 0x1u /* the key's log holds ops of more than one type */
+
+/*
+ * The per-partition ops cache as structure-of-arrays (one "log" = one
+ * materializer_vnode ops_cache table).  Ops of key k occupy
+ * [key_off[k], key_off[k+1]) oldest -> newest, exactly the ETS tuple order
+ * (slot FIRST_OP .. FIRST_OP+Length-1).  Payload encoding per type:
+ *   PN        p0 = int64 delta
+ *   LWW       p0 = timestamp, p1 = value (u64)
+ *   MVREG     p0 = value, p1 = token, var = overridden tokens (kind ASSIGN|RESET)
+ *   AWSET     var = entries [elem, n_add, n_rm, add_tok..., rm_tok...]...,
+ *             entries sorted by elem, elems unique within one effect
+ *   BCOUNTER  p0 = int64 amount, p1 = from | (to << 8), kind in op_meta
+ */
+typedef struct am_op_log {
+  uint32_t n_dc;
+  uint32_t _pad;
+  uint64_t n_keys;
+  uint64_t n_ops;
+  uint64_t n_var;
+  uint64_t snap_stride;        /* elements between the DC columns of snap_vc; 0 => n_ops */
+  const uint64_t *key_off;     /* [n_keys+1]                                        */
+  const uint64_t *key_id_base; /* [n_keys] op id of the key's oldest op; NULL => 1   */
+  const uint8_t *key_type;     /* [n_keys] am_type                                   */
+  const uint8_t *key_flags;    /* [n_keys] or NULL                                   */
+  const uint8_t *op_meta;      /* [n_ops]                                            */
+  const uint64_t *commit_time; /* [n_ops] commit_time = {DcId, CT}: the CT           */
+  const uint64_t *snap_vc;     /* [n_dc][snap_stride] snapshot_time, DC-major        */
+  const uint32_t *snap_pres;   /* [n_ops] presence of snapshot_time keys; NULL=all   */
+  const uint64_t *op_txid;     /* [n_ops] or NULL (never equal to a read's TxId)     */
+  const uint64_t *op_id;       /* [n_ops] or NULL (dense ids from key_id_base)       */
+  const uint64_t *p0;          /* [n_ops]                                            */
+  const uint64_t *p1;          /* [n_ops]                                            */
+  const uint64_t *var_off;     /* [n_ops+1] or NULL                                  */
+  const uint64_t *var_data;    /* [n_var]                                            */
+} am_op_log;
+
+/*
+ * CRDT values (base snapshots in, materialized values out), SoA over reads.
+ *   PN        v0
+ *   LWW       v0 = ts (as u64 bits), v1 = value, vflag = 1 for the initial
+ *             {0, <<>>} value (a binary sorts above every integer)
+ *   AWSET     CSR of (elem, token) pairs sorted by (elem, token) -- one pair per
+ *   MVREG     live token; MV: (value, token) pairs sorted.  set_off[n+1] gives
+ *             each read's capacity, set_len[n] the used length.
+ *   BCOUNTER  bc_p[n][n_dc*n_dc] + bc_p_pres, bc_d[n][n_dc] + bc_d_pres
+ *             (P key {From,To} at From*n_dc+To; an orddict entry is present iff
+ *             it was ever updated)
+ */
+typedef struct am_values {
+  int64_t *v0;
+  uint64_t *v1;
+  uint8_t *vflag;
+  const uint64_t *set_off;
+  uint32_t *set_len;
+  uint64_t *set_a;
+  uint64_t *set_b;
+  int64_t *bc_p;
+  uint8_t *bc_p_pres;
+  int64_t *bc_d;
+  uint8_t *bc_d_pres;
+} am_values;
+
+/* One batch of snapshot reads: the materialize/4 inputs per key. */
+typedef struct am_read_batch {
+  uint64_t n_reads;
+  uint32_t per_read_clock; /* 0: one MinSnapshotTime for the whole batch; 1: one per read */
+  uint32_t type_hint;      /* am_type when every read has that type (fast path); 0 = mixed */
+  const uint64_t *key;        /* [n] key index into the log                          */
+  const uint8_t *type;        /* [n] requested Type                                  */
+  const uint64_t *read_vc;    /* [n_dc] or [n_dc][n] MinSnapshotTime                 */
+  const uint32_t *read_pres;  /* [1] or [n]                                          */
+  const uint64_t *txid;       /* [n] TxId, or NULL => every read's TxId is ignore    */
+  const uint8_t *txid_valid;  /* [n] or NULL (all valid when txid != NULL)           */
+  /* base snapshot: #snapshot_get_response{snapshot_time, materialized_snapshot} */
+  const uint8_t *base_ignore; /* [n] 1 => snapshot_time = ignore; NULL => all ignore  */
+  const uint64_t *base_vc;    /* [n_dc][n]                                            */
+  const uint32_t *base_pres;  /* [n]                                                  */
+  const int64_t *base_last_op;/* [n] or NULL => 0                                     */
+  am_values base;             /* NULL members => the type's new() value               */
+} am_read_batch;
+
+/* materialize/4 outputs: {ok, Value, NewLastOp, LastOpCt, IsNewSS, Count} */
+typedef struct am_read_result {
+  int32_t *status;         /* [n] am_status                                */
+  int64_t *new_last_op;    /* [n] NewLastOp                                */
+  uint64_t *last_ct;       /* [n_dc][n] LastOpCt                           */
+  uint32_t *last_ct_pres;  /* [n]                                          */
+  uint8_t *last_ct_ignore; /* [n] 1 => LastOpCt = ignore                   */
+  uint8_t *is_new_ss;      /* [n]                                          */
+  uint32_t *count;         /* [n] number of effects applied                */
+  uint8_t *flags;          /* [n] AM_FLAG_*                                */
+  am_values value;
+} am_read_result;
+
+typedef struct am_ctx am_ctx;     /* device + HIP stream + scratch             */
+typedef struct am_store am_store; /* a device-resident op log (one partition)  */
+typedef struct am_comm am_comm;   /* RCCL communicator for the GST all-reduce  */
+
+/* ---- context ---- */
+int am_abi_version(void);
+int am_ctx_open(int device, am_ctx **out);
+int am_ctx_close(am_ctx *ctx);
+void *am_ctx_stream(am_ctx *ctx);           /* hipStream_t */
+int am_ctx_sync(am_ctx *ctx);
+const char *am_last_error(void);            /* thread-local message of the last failure */
+int am_timer_start(am_ctx *ctx);             /* hipEventRecord on the ctx stream         */
+int am_timer_stop(am_ctx *ctx, float *ms);   /* records, syncs, returns elapsed ms       */
+
+/* ---- device memory helpers (the NIF owns no framework allocator) ---- */
+int am_dev_alloc(am_ctx *ctx, size_t bytes, void **out);
+int am_dev_free(am_ctx *ctx, void *p);
+int am_memcpy_h2d(am_ctx *ctx, void *dst, const void *src, size_t bytes);
+int am_memcpy_d2h(am_ctx *ctx, void *dst, const void *src, size_t bytes);
+
+/* ---- ops cache in HBM ---- */
+/* Upload a host op log into device memory owned by the store. */
+int am_store_create(am_ctx *ctx, const am_op_log *host_log, am_store **out);
+/* Device view of the store (pointers are device pointers). */
+int am_store_log(const am_store *st, am_op_log *out);
+int am_store_destroy(am_store *st);
+
+/* ---- the hot path ---- */
+/* Device pointers; asynchronous on the ctx stream. */
+int am_materialize(am_ctx *ctx, const am_op_log *dev_log, const am_read_batch *dev_batch,
+                   am_read_result *dev_res);
+/* Host pointers for batch/result; the log is the store's device log.  Blocks. */
+int am_materialize_host(am_ctx *ctx, const am_store *st, const am_read_batch *host_batch,
+                        am_read_result *host_res);
+
+/* ---- GST (global stable time) ---- */
+/* lanes[0..n_dc-1] = per-DC min over the partitions that have the DC (absent = UINT64_MAX);
+ * if any partition is undefined every present lane is 0 (get_min_time's rule);
+ * lanes[n_dc] = 1 (defined).  Device pointers: part_vc [n_part][n_dc] (partition-major),
+ * part_pres [n_part], part_undef [n_part] (or NULL). */
+int am_gst_local_min(am_ctx *ctx, uint32_t n_dc, uint32_t n_part, const uint64_t *part_vc,
+                     const uint32_t *part_pres, const uint8_t *part_undef, uint64_t *lanes);
+/* RCCL communicator (one process per GPU). */
+int am_comm_unique_id(void *id_out /* 128 bytes */);
+int am_comm_init(am_ctx *ctx, int rank, int nranks, const void *id /* 128 bytes */, am_comm **out);
+int am_comm_destroy(am_comm *comm);
+/* In place element-wise min of n_dc+1 u64 lanes across ranks (ncclMin/ncclUint64). */
+int am_gst_allreduce(am_comm *comm, uint64_t *lanes, uint32_t n_dc);
+/* Turn merged lanes into the stable snapshot: undefined => present lanes 0; then the
+ * monotone update against last (last_vc/last_pres device, updated in place);
+ * gr != 0 additionally replicates the min over present DCs to every present DC
+ * (the value a reader gets from get_stable_snapshot/0).  out_vc/out_pres receive the
+ * snapshot a reader would use; changed (device u8) = update_stable's Bool. */
+int am_gst_finalize(am_ctx *ctx, uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc,
+                    uint32_t *last_pres, int gr, uint64_t *out_vc, uint32_t *out_pres,
+                    uint8_t *changed);
+
+/* ---- sharding ---- */
+/* 0-based partition position for integer keys: abs(K) rem n_partitions. */
+uint32_t am_key_partition(int64_t key, uint32_t n_partitions);
+
+/* ---- synthetic op logs (bench + parity; counter-based, regenerable per key) ---- */
+typedef struct am_synth_params {
+  uint64_t seed;
+  uint64_t n_keys;
+  uint32_t ops_per_key;  /* uniform log length (0 => use zipf)                 */
+  uint32_t n_dc;
+  uint32_t type;         /* am_type, or 0 for mixed (40/20/20/20 PN/LWW/AW/MV) */
+  uint32_t key_base;     /* global index of key 0 (for sharding)               */
+  uint32_t max_lag;      /* snapshot lag in ops (concurrency window)           */
+  uint32_t _pad;
+} am_synth_params;
+/* Device log owned by the returned store. */
+int am_synth_store(am_ctx *ctx, const am_synth_params *p, am_store **out);
+/* The read clock the generator's quantile q selects (q in [0,1]); host output [n_dc]. */
+int am_synth_read_clock(const am_synth_params *p, double q, uint64_t *out_vc);
+/* Regenerate keys [k0, k0+nk) on the host into caller buffers sized by
+ * am_synth_host_sizes (for parity checks against the oracle). */
+int am_synth_host_sizes(const am_synth_params *p, uint64_t k0, uint64_t nk, uint64_t *n_ops,
+                        uint64_t *n_var);
+int am_synth_host(const am_synth_params *p, uint64_t k0, uint64_t nk, am_op_log *out_host_bufs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ANTIDOTE_MAT_H */

@@ -1,0 +1,264 @@
+"""Parity of the HIP path (libantidote_mat.so through its C ABI) against the oracle.
+
+Bar: bit-exact -- every output column of materialize/4 (status, value, NewLastOp,
+LastOpCt key set and values, IsNewSS, Count, the missing-DC log flag)."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from antidote_amd import abi
+from antidote_amd.oplog import HostBatch, HostLog, Op, Read
+from oracle import amo
+from tests import randlog
+from tests.kat_util import load
+from tests.test_oracle_c import _dcmap, kat_ops, run_kat_cases
+
+pytestmark = pytest.mark.gpu
+
+GPU_TYPES = [abi.AM_PN, abi.AM_LWW]
+
+
+@pytest.fixture(scope="module")
+def mat():
+    from antidote_amd.materializer import Materializer
+    m = Materializer(0)
+    yield m
+    m.close()
+
+
+KAT = load("kat_materialize.json")
+
+
+@pytest.mark.parametrize("kat", KAT["materialize"], ids=lambda k: k["name"])
+def test_gpu_kat(mat, kat):
+    m = _dcmap(kat)
+    ops = kat_ops(kat, m)
+    nd = max(len(m), 1)
+
+    def run(read):
+        log = HostLog(nd, [ops], key_types=[kat["type"]])
+        st = mat.store(log)
+        hb = mat.read_batch(st, [read])
+        st.close()
+        return hb.result(0)
+
+    run_kat_cases(kat, run)
+
+
+def _batch_compare(log, reads, mat, n_dc):
+    st = mat.store(log)
+    got = mat.read_batch(st, reads)
+    st.close()
+    ref = amo.materialize(log, HostBatch(n_dc, reads))
+    for i in range(len(reads)):
+        a, b = got.result(i), ref.result(i)
+        assert a == b, (i, reads[i], a, b)
+    return got
+
+
+@pytest.mark.parametrize("t", GPU_TYPES)
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_random_batches(mat, t, seed):
+    """Many keys per batch: ragged lengths (0 .. 700 ops, unaligned CSR offsets, keys
+    spanning several 256-op tiles), partial clocks, TxIds, cached bases, bad effects."""
+    rng = random.Random(1000 + seed * 7 + t)
+    n_dc = [1, 3, 5, 16][seed]
+    partial = seed in (1, 3)
+    keys, reads = [], []
+    for k in range(60):
+        n_ops = rng.choice([0, 1, 3, 17, 64, 255, 256, 257, 700]) if k % 5 else rng.randint(0, 40)
+        ops = randlog.rand_key_ops(rng, t, n_dc, n_ops, partial=partial, txids=seed == 2,
+                                   bad_rate=0.002 if seed == 3 else 0.0, t0=rng.randint(0, 100))
+        keys.append(ops)
+        hi = ops[-1].commit_time if ops else 50
+        clock = randlog.rand_clock(rng, n_dc, 0, hi + 5, partial=partial)
+        reads.append(Read(k, t, clock, rng.choice([None, 1, 3]) if seed == 2 else None))
+    log = HostLog(n_dc, keys, key_types=[t] * len(keys), partial=partial or None)
+    first = _batch_compare(log, reads, mat, n_dc)
+    # incremental reads from the cached results (belongs_to_snapshot_op against a base clock)
+    reads2 = []
+    for i, r in enumerate(reads):
+        res = first.result(i)
+        if res[0] != "ok":
+            continue
+        clock2 = {d: v + rng.randint(0, 200) for d, v in r.clock.items()}
+        reads2.append(Read(r.key, t, clock2, None, res[3], res[2], res[1]))
+    _batch_compare(log, reads2, mat, n_dc)
+
+
+def test_gpu_corrupted_and_invalid(mat):
+    keys = [[Op(abi.AM_PN, 0, 5, {0: 1}, 3)], [], [Op(abi.AM_PN, 0, 5, {0: 1}, 3), Op(abi.AM_LWW, 0, 6, {0: 1}, (1, 2))]]
+    log = HostLog(1, keys, key_types=[abi.AM_PN, abi.AM_LWW, abi.AM_PN])
+    reads = [Read(0, abi.AM_LWW, {0: 10}), Read(1, abi.AM_LWW, {0: 10}), Read(2, abi.AM_PN, {0: 10})]
+    got = _batch_compare(log, reads, mat, 1)
+    assert got.result(0) == ("error", abi.AM_ERR_CORRUPTED_OPS_CACHE)
+    assert got.result(1) == ("ok", (0, 0, True), 0, None, False, 0, 0)
+    assert got.result(2) == ("error", abi.AM_ERR_CORRUPTED_OPS_CACHE)
+
+
+def test_gpu_pn_overflow(mat):
+    ops = [Op(abi.AM_PN, 0, 5 + i, {0: 1}, 2**62) for i in range(3)]
+    ops2 = [Op(abi.AM_PN, 0, 5 + i, {0: 1}, v) for i, v in enumerate([2**62, 2**62, -2**62, -2**62 + 7])]
+    log = HostLog(1, [ops, ops2])
+    got = _batch_compare(log, [Read(0, abi.AM_PN, {0: 100}), Read(1, abi.AM_PN, {0: 100})], mat, 1)
+    assert got.result(0) == ("error", abi.AM_ERR_OVERFLOW)
+    assert got.result(1)[1] == 7
+
+
+def _synth_params(n_keys, n_ops, n_dc, t, seed=0x5EED + 2):
+    p = abi.am_synth_params()
+    p.seed, p.n_keys, p.ops_per_key, p.n_dc, p.type, p.key_base, p.max_lag = seed, n_keys, n_ops, n_dc, t, 0, 8
+    return p
+
+
+def _host_log_from_synth(p, k0, nk):
+    import ctypes
+    n_ops = ctypes.c_uint64()
+    abi.check(abi.lib().am_synth_host_sizes(ctypes.byref(p), k0, nk, ctypes.byref(n_ops), None), "sizes")
+    n = n_ops.value
+    log = HostLog.__new__(HostLog)
+    log.n_dc, log.n_keys, log.n_ops, log.n_var, log.has_var = p.n_dc, nk, n, 0, False
+    log.key_off = np.zeros(nk + 1, np.uint64)
+    log.key_type = np.zeros(nk, np.uint8)
+    log.key_flags = None
+    log.key_id_base = None
+    log.op_meta = np.zeros(n, np.uint8)
+    log.commit_time = np.zeros(n, np.uint64)
+    log.snap_vc = np.zeros((p.n_dc, n), np.uint64)
+    log.snap_pres = None
+    log.op_txid = log.op_id = None
+    log.p0 = np.zeros(n, np.uint64)
+    log.p1 = np.zeros(n, np.uint64)
+    log.var_off = log.var_data = None
+    s = log.as_struct()
+    abi.check(abi.lib().am_synth_host(ctypes.byref(p), k0, nk, ctypes.byref(s)), "am_synth_host")
+    return log
+
+
+@pytest.mark.parametrize("t,n_dc,n_ops", [(abi.AM_LWW, 3, 256), (abi.AM_PN, 1, 64), (abi.AM_LWW, 8, 100)])
+def test_gpu_synth_device_vs_oracle(mat, t, n_dc, n_ops):
+    """Device-generated log (the bench's input) read at two snapshot quantiles, fresh
+    and from the cached q=0.5 result; sampled keys checked against the oracle on the
+    host-regenerated log."""
+    from antidote_amd.devbatch import DeviceReads, materialize
+    import ctypes
+    n_keys = 20000
+    p = _synth_params(n_keys, n_ops, n_dc, t)
+    st = mat.synth_store(p)
+    dlog = st.device_log()
+    rng = np.random.default_rng(1)
+    sample = np.sort(rng.choice(n_keys, 300, replace=False))
+    hlog_full = _host_log_from_synth(p, 0, n_keys)
+    prev = None
+    for q in (0.5, 0.75):
+        clock = (ctypes.c_uint64 * n_dc)()
+        abi.lib().am_synth_read_clock(ctypes.byref(p), q, clock)
+        clock = list(clock)
+        dr = DeviceReads(n_keys, n_dc, t, clock)
+        if prev is not None:
+            dr.set_base_from(prev)
+        torch.cuda.synchronize()
+        materialize(mat, dlog, dr)
+        mat.sync()
+        got = dr.host()
+        # oracle on the sampled keys
+        reads = []
+        for k in sample:
+            base_clock = base_last = base_val = None
+            if prev is not None:
+                ph = prev_host
+                if not ph["last_ct_ignore"][k]:
+                    base_clock = {d: int(ph["last_ct"][d, k]) for d in range(n_dc) if (int(ph["last_ct_pres"][k]) >> d) & 1}
+                base_last = int(ph["new_last_op"][k])
+                base_val = int(ph["v0"][k]) if t == abi.AM_PN else (int(np.int64(ph["v0"][k]).view(np.uint64)),
+                                                                      int(ph["v1"][k]), bool(ph["vflag"][k]))
+            reads.append(Read(int(k), t, {d: clock[d] for d in range(n_dc)}, None, base_clock, base_last or 0,
+                              base_val))
+        ref = amo.materialize(hlog_full, HostBatch(n_dc, reads))
+        for j, k in enumerate(sample):
+            r = ref.result(j)
+            assert r[0] == "ok"
+            assert got["status"][k] == 0
+            assert got["new_last_op"][k] == r[2]
+            assert got["count"][k] == r[5]
+            assert bool(got["is_new_ss"][k]) == r[4]
+            ct = None if got["last_ct_ignore"][k] else {d: int(got["last_ct"][d, k]) for d in range(n_dc)
+                                                         if (int(got["last_ct_pres"][k]) >> d) & 1}
+            assert ct == r[3]
+            if t == abi.AM_PN:
+                assert got["v0"][k] == r[1]
+            else:
+                assert (int(np.int64(got["v0"][k]).view(np.uint64)), int(got["v1"][k]), bool(got["vflag"][k])) == r[1]
+        # size-independent properties over ALL keys
+        assert (got["status"] == 0).all()
+        assert (got["count"] <= n_ops).all()
+        if q == 0.75 and prev is not None:
+            assert (got["count"] >= 0).all()
+        prev, prev_host = dr, got
+    st.close()
+
+
+def test_gpu_gst(mat):
+    """am_gst_local_min + am_gst_finalize (+ RCCL all-reduce at nranks=1) vs the oracle."""
+    import ctypes
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        nd, npart = int(rng.integers(1, 6)), int(rng.integers(1, 9))
+        vc = rng.integers(0, 1000, size=(npart, nd)).astype(np.uint64)
+        pres = rng.integers(0, 1 << nd, size=npart).astype(np.uint32)
+        undef = (rng.random(npart) < 0.1).astype(np.uint8)
+        out = np.zeros(nd, np.uint64)
+        op = np.zeros(1, np.uint32)
+        amo.lib().amo_gst_min(nd, npart, vc.ctypes.data, pres.ctypes.data, undef.ctypes.data, out.ctypes.data,
+                              op.ctypes.data)
+        d_vc = torch.from_numpy(vc.view(np.int64)).cuda()
+        d_pres = torch.from_numpy(pres.view(np.int32)).cuda()
+        d_undef = torch.from_numpy(undef).cuda()
+        lanes = torch.zeros(nd + 1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        abi.check(mat.L.am_gst_local_min(mat.ctx, nd, npart, d_vc.data_ptr(), d_pres.data_ptr(), d_undef.data_ptr(),
+                                         lanes.data_ptr()), "local_min")
+        mat.sync()
+        ln = lanes.cpu().numpy().view(np.uint64)
+        for d in range(nd):
+            if (int(op[0]) >> d) & 1:
+                assert ln[d] == out[d]
+            else:
+                assert ln[d] == np.uint64(0xFFFFFFFFFFFFFFFF)
+        # finalize against a previous stable snapshot
+        last = rng.integers(0, 800, size=nd).astype(np.uint64)
+        lastp = np.array([rng.integers(0, 1 << nd)], np.uint32)
+        h_last, h_lastp = last.copy(), lastp.copy()
+        changed_ref = amo.lib().amo_update_stable(nd, h_last.ctypes.data, h_lastp.ctypes.data, out.ctypes.data,
+                                                  int(op[0]))
+        d_last = torch.from_numpy(last.view(np.int64)).cuda()
+        d_lastp = torch.from_numpy(lastp.view(np.int32)).cuda()
+        o_vc = torch.zeros(nd, dtype=torch.int64, device="cuda")
+        o_p = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ch = torch.zeros(1, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        abi.check(mat.L.am_gst_finalize(mat.ctx, nd, lanes.data_ptr(), d_last.data_ptr(), d_lastp.data_ptr(), 0,
+                                        o_vc.data_ptr(), o_p.data_ptr(), ch.data_ptr()), "finalize")
+        mat.sync()
+        assert int(ch.item()) == changed_ref
+        assert int(d_lastp.item()) & 0xFFFFFFFF == int(h_lastp[0])
+        gv = d_last.cpu().numpy().view(np.uint64)
+        for d in range(nd):
+            if (int(h_lastp[0]) >> d) & 1:
+                assert gv[d] == h_last[d]
+
+
+def test_gpu_rccl_single_rank(mat):
+    import ctypes
+    uid = (ctypes.c_char * 128)()
+    abi.check(mat.L.am_comm_unique_id(uid), "uid")
+    comm = ctypes.c_void_p()
+    abi.check(mat.L.am_comm_init(mat.ctx, 0, 1, uid, ctypes.byref(comm)), "comm_init")
+    lanes = torch.tensor([5, 7, 1], dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    abi.check(mat.L.am_gst_allreduce(comm, lanes.data_ptr(), 2), "allreduce")
+    mat.sync()
+    assert lanes.cpu().tolist() == [5, 7, 1]
+    mat.L.am_comm_destroy(comm)
