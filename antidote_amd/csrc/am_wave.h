@@ -1,0 +1,222 @@
+// am_wave.h -- wave64 building blocks shared by the materialize kernels:
+// DPP row reductions, wave-uniform helpers, and the per-op inclusion test of
+// clocksi_materializer:is_op_in_snapshot/7.
+#pragma once
+#include "am_internal.h"
+
+namespace amk {
+
+constexpr int WAVE = 64;
+constexpr uint64_t NONE = ~0ull;
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ---- DPP: butterflies inside a 16-lane row (quad_perm 1032 / 2301, row_ror 4 / 8) ----
+// Every lane of a row ends with the row's reduction; the four rows are then
+// combined from lanes 0/16/32/48 with v_readlane (result is wave-uniform).
+// Requires all 64 lanes active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  return ((uint64_t)dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL>((uint32_t)v);
+}
+#define AMK_ROW_STEPS(STEP) STEP(0xB1) STEP(0x4E) STEP(0x124) STEP(0x128)
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#define S_(C) v += dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return lane_u32(v, 0) + lane_u32(v, 16) + lane_u32(v, 32) + lane_u32(v, 48);
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#define S_(C) v |= dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return lane_u32(v, 0) | lane_u32(v, 16) | lane_u32(v, 32) | lane_u32(v, 48);
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#define S_(C) v = umax64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return umax64(umax64(lane_u64(v, 0), lane_u64(v, 16)), umax64(lane_u64(v, 32), lane_u64(v, 48)));
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#define S_(C) v = umin64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return umin64(umin64(lane_u64(v, 0), lane_u64(v, 16)), umin64(lane_u64(v, 32), lane_u64(v, 48)));
+}
+// exact 128-bit sum of per-lane (hi, lo) pairs
+__device__ __forceinline__ void add128(int64_t &hi, uint64_t &lo, int64_t whi, uint64_t wlo) {
+  const uint64_t s = lo + wlo;
+  hi = hi + whi + (s < lo ? 1 : 0);
+  lo = s;
+}
+__device__ __forceinline__ void wave_sum_i128(int64_t &hi, uint64_t &lo) {
+#define S_(C)                                                     \
+  {                                                               \
+    const uint64_t wlo = dpp64<C>(lo);                            \
+    const int64_t whi = (int64_t)dpp64<C>((uint64_t)hi);          \
+    add128(hi, lo, whi, wlo);                                     \
+  }
+  AMK_ROW_STEPS(S_)
+#undef S_
+  int64_t h = (int64_t)lane_u64((uint64_t)hi, 0);
+  uint64_t l = lane_u64(lo, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) add128(h, l, (int64_t)lane_u64((uint64_t)hi, r), lane_u64(lo, r));
+  hi = h;
+  lo = l;
+}
+
+// ---- per-read uniform inputs and per-lane accumulators ----
+template <int DMAX>
+struct ReadU {
+  uint64_t S[DMAX];   // MinSnapshotTime (absent lanes 0)
+  uint64_t C0[DMAX];  // base snapshot_time (absent lanes 0)
+  uint32_t spres, cpres, allmask;
+  bool base_ignore, has_txid;
+  uint64_t txid;
+};
+
+template <int DMAX>
+struct Acc {
+  uint64_t mx[DMAX];
+  uint32_t pres, count, flags;
+  uint64_t min_excl;
+  __device__ void reset() {
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = 0;
+    pres = count = flags = 0;
+    min_excl = NONE;
+  }
+};
+
+constexpr uint32_t FLAG_BAD = 0x100u;
+
+// One op of is_op_in_snapshot/7 (src/clocksi_materializer.erl:216-268) + the
+// union-max of materialize_intern_perform (:173-197).  Returns "included".
+template <int DMAX, bool GENERAL>
+__device__ __forceinline__ bool eval_op(const ReadU<DMAX> &u, uint32_t meta, uint64_t ct, const uint64_t (&snap)[DMAX],
+                                        uint32_t spres_op, bool txmatch, uint64_t pos, Acc<DMAX> &a) {
+  const uint32_t dc = meta & 31u;
+  const uint32_t xpres = GENERAL ? ((spres_op | (1u << dc)) & u.allmask) : u.allmask;
+  uint64_t X[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) X[d] = ((uint32_t)d == dc) ? ct : (((xpres >> d) & 1u) ? snap[d] : 0);
+  if (GENERAL) {
+    bool cand = u.base_ignore | txmatch;
+    if (!cand) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
+      bool le = true;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) le &= X[d] <= u.C0[d];
+      cand = !le;
+    }
+    if (!cand) return false;
+  }
+  bool incl = true;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    if ((xpres >> d) & 1u) {
+      if ((u.spres >> d) & 1u) {
+        incl &= X[d] <= u.S[d];
+      } else {  // logger:error("Could not find DC in SS"); the op is excluded
+        incl = false;
+        a.flags |= AM_FLAG_MISSING_DC_LOGGED;
+      }
+    }
+  }
+  if (incl) {
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) a.mx[d] = X[d] > a.mx[d] ? X[d] : a.mx[d];
+    a.pres |= xpres;
+    a.count += 1;
+    if (meta & AM_META_BAD) a.flags |= FLAG_BAD;
+  } else {
+    a.min_excl = pos < a.min_excl ? pos : a.min_excl;
+  }
+  return incl;
+}
+
+// ---- per-type value reductions (apply_operations folds of commutative updates) ----
+struct PnVal {  // antidote_crdt_counter_pn: integer sum, exact in 128 bits
+  int64_t hi;
+  uint64_t lo;
+  __device__ void reset() { hi = 0, lo = 0; }
+  __device__ void add(uint64_t p0, uint64_t) {
+    const int64_t v = (int64_t)p0;
+    add128(hi, lo, v < 0 ? -1 : 0, (uint64_t)v);
+  }
+};
+struct LwwVal {  // antidote_crdt_register_lww: erlang:max over {Ts, Value}
+  uint64_t ts, val;
+  uint32_t has;
+  __device__ void reset() { ts = 0, val = 0, has = 0; }
+  __device__ void add(uint64_t p0, uint64_t p1) {
+    const bool gt = !has || p0 > ts || (p0 == ts && p1 > val);
+    ts = gt ? p0 : ts;
+    val = gt ? p1 : val;
+    has = 1;
+  }
+};
+
+template <int TYPE>
+struct ValOf;
+template <>
+struct ValOf<AM_PN> {
+  using T = PnVal;
+  static constexpr bool NEED_P1 = false;
+};
+template <>
+struct ValOf<AM_LWW> {
+  using T = LwwVal;
+  static constexpr bool NEED_P1 = true;
+};
+
+// wave-uniform LWW max: row butterflies on (has, ts, val), then the four rows
+__device__ __forceinline__ void wave_max_lww(LwwVal &v) {
+#define S_(C)                                                                            \
+  {                                                                                      \
+    const uint64_t wts = dpp64<C>(v.ts), wval = dpp64<C>(v.val);                         \
+    const uint32_t whas = dpp32<C>(v.has);                                               \
+    const bool gt = whas && (!v.has || wts > v.ts || (wts == v.ts && wval > v.val));     \
+    v.ts = gt ? wts : v.ts;                                                              \
+    v.val = gt ? wval : v.val;                                                           \
+    v.has |= whas;                                                                       \
+  }
+  AMK_ROW_STEPS(S_)
+#undef S_
+  LwwVal r;
+  r.ts = lane_u64(v.ts, 0), r.val = lane_u64(v.val, 0), r.has = lane_u32(v.has, 0);
+#pragma unroll
+  for (int l = 16; l < 64; l += 16) {
+    const uint64_t wts = lane_u64(v.ts, l), wval = lane_u64(v.val, l);
+    const uint32_t whas = lane_u32(v.has, l);
+    const bool gt = whas && (!r.has || wts > r.ts || (wts == r.ts && wval > r.val));
+    r.ts = gt ? wts : r.ts;
+    r.val = gt ? wval : r.val;
+    r.has |= whas;
+  }
+  v = r;
+}
+
+}  // namespace amk

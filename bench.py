@@ -167,7 +167,16 @@ def main():
         pg.broadcast_object_list(obj, src=0)
         ctypes.memmove(uid, obj[0], 128)
     comm = ctypes.c_void_p()
-    abi.check(mat.L.am_comm_init(mat.ctx, rank, world, uid, ctypes.byref(comm)), "am_comm_init")
+    # RCCL prints its version banner on stdout; keep stdout for the one JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        rc = mat.L.am_comm_init(mat.ctx, rank, world, uid, ctypes.byref(comm))
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    abi.check(rc, "am_comm_init")
 
     # ---- this GPU's op log, generated in HBM ----
     p = synth_params(type_, n_dc, n_keys, n_ops, key_base=rank * n_keys)
