@@ -417,6 +417,8 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   const char *variant = getenv("AM_KERNEL");  // "scalar" = the one-read-per-wave kernel (A/B only)
   if (!(variant && strcmp(variant, "scalar") == 0) && (B->type_hint == AM_PN || B->type_hint == AM_LWW))
     return am_launch_stream(ctx, L, B, R);
+  if (B->type_hint == AM_AWSET || B->type_hint == AM_MVREG || B->type_hint == AM_BCOUNTER)
+    return am_launch_sets(ctx, L, B, R);
   switch (B->type_hint) {
     case AM_PN: return launch_hint<AM_PN>(ctx, L, B, R);
     case AM_LWW: return launch_hint<AM_LWW>(ctx, L, B, R);

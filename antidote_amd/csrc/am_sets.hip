@@ -1,0 +1,489 @@
+// am_sets.hip -- materialize/4 for the order-sensitive CRDTs (add-wins set,
+// MV register) and the bounded counter.  One 256-thread workgroup per read.
+//
+// antidote_crdt_set_aw / antidote_crdt_register_mv apply their effects
+// sequentially (oldest -> newest), but the final state has a closed form that
+// needs no sequential fold.  Call every token an effect inserts a BIRTH at the
+// op's position p (AW: {Elem, Tok} for each Add token; MV: {Value, Tok}) and
+// every token it drops a KILL at p (AW: {Elem, Tok} for each Remove token; MV:
+// each Overridden token).  Within one effect the AW update is
+// ToAdd ++ (Current -- ToRemove) and the MV update removes Overridden before
+// inserting, so a kill only affects births at earlier positions:
+//     a birth at p survives  <=>  no kill of the same token (and AW: elem) at q > p
+// Base-snapshot pairs are births at p = -1.  The workgroup therefore
+//   1. streams the key's log in 1024-op tiles (4 ops per lane, 16-byte loads),
+//      evaluates inclusion per op (am_wave.h eval_op), and appends the included
+//      effects' births / kills to LDS lists (LDS atomics for the slots);
+//   2. bitonic-sorts the kills by (token, elem, pos) in LDS;
+//   3. keeps each birth whose upper-bound lookup finds no later kill;
+//   4. bitonic-sorts the survivors by (a, b), drops duplicates (the reference
+//      state is compared as a canonical sorted rendering) and writes the CSR.
+// The bounded counter (orddict:update_counter on P[{From,To}] and D[Id]) is a
+// keyed sum: exact 128-bit LDS accumulators (64-bit atomics + carry).
+// Capacity: KCAP kills / BCAP births per read live in LDS (78 KB per group);
+// a read that exceeds them returns AM_ERR_CAPACITY (global-scratch path: next).
+#include "am_wave.h"
+
+using namespace amk;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int NW = BLOCK / WAVE;
+constexpr int OPL = 4;
+constexpr uint64_t TILE = (uint64_t)BLOCK * OPL;
+constexpr uint32_t KCAP = 2048;
+constexpr uint32_t BCAP = 1024;
+constexpr int32_t POS_MAX = 0x7FFFFFFF;
+
+struct Smem {
+  uint64_t *ka, *kb;  // kills: token, elem (MV: 0)
+  int32_t *kp;        // kill position
+  uint64_t *ba, *bb;  // births: AW (elem, tok), MV (value, tok)
+  int32_t *bp;        // birth position (-1: base snapshot)
+  uint64_t *oa, *ob;  // survivors
+  uint32_t *ctr;      // [0] kills [1] births [2] survivors [3] overflow [4..7] wave sums
+  uint64_t *red;      // block reduction scratch [NW][8]
+  // bounded counter slots (aliases the kill arrays)
+  uint64_t *slo;
+  int64_t *shi;
+  uint32_t *spres;
+};
+
+__device__ Smem carve(unsigned char *p) {
+  Smem s;
+  s.ka = (uint64_t *)p;
+  s.kb = s.ka + KCAP;
+  s.kp = (int32_t *)(s.kb + KCAP);
+  s.ba = (uint64_t *)(s.kp + KCAP);
+  s.bb = s.ba + BCAP;
+  s.bp = (int32_t *)(s.bb + BCAP);
+  s.oa = (uint64_t *)(s.bp + BCAP);
+  s.ob = s.oa + BCAP;
+  s.ctr = (uint32_t *)(s.ob + BCAP);
+  s.red = (uint64_t *)(s.ctr + 16);
+  s.slo = s.ka;
+  s.shi = (int64_t *)s.kb;
+  s.spres = (uint32_t *)s.kp;
+  return s;
+}
+constexpr size_t SMEM_BYTES = (size_t)KCAP * 20 + (size_t)BCAP * 20 + (size_t)BCAP * 16 + 16 * 4 + NW * 8 * 8;
+
+__device__ __forceinline__ bool less3(uint64_t a0, uint64_t b0, int32_t p0, uint64_t a1, uint64_t b1, int32_t p1) {
+  return a0 != a1 ? a0 < a1 : (b0 != b1 ? b0 < b1 : p0 < p1);
+}
+
+// block bitonic sort of (a, b, p) in LDS, n <= cap (power-of-two padded with +inf)
+__device__ void block_sort(uint64_t *a, uint64_t *b, int32_t *p, uint32_t n, uint32_t cap) {
+  uint32_t N = 1;
+  while (N < n) N <<= 1;
+  if (N > cap) N = cap;
+  for (uint32_t i = n + threadIdx.x; i < N; i += BLOCK) {
+    a[i] = ~0ull;
+    b[i] = ~0ull;
+    if (p) p[i] = POS_MAX;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= N; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < N; i += BLOCK) {
+        const uint32_t x = i ^ j;
+        if (x > i) {
+          const bool up = (i & k) == 0;
+          const int32_t pi = p ? p[i] : 0, px = p ? p[x] : 0;
+          const bool gt = less3(a[x], b[x], px, a[i], b[i], pi);
+          if (gt == up) {
+            uint64_t t = a[i]; a[i] = a[x]; a[x] = t;
+            t = b[i]; b[i] = b[x]; b[x] = t;
+            if (p) { const int32_t q = p[i]; p[i] = p[x]; p[x] = q; }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// block-wide reductions through the DPP wave reductions + LDS
+__device__ __forceinline__ uint64_t block_red_u64(Smem &s, uint64_t wave_val, int op /*0 sum,1 or,2 max,3 min*/) {
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) s.red[w] = wave_val;
+  __syncthreads();
+  uint64_t r = s.red[0];
+  for (int i = 1; i < NW; ++i) {
+    const uint64_t x = s.red[i];
+    r = op == 0 ? r + x : op == 1 ? (r | x) : op == 2 ? (r > x ? r : x) : (r < x ? r : x);
+  }
+  __syncthreads();
+  return r;
+}
+
+template <int DMAX, int TYPE>
+__global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am_read_result R) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  Smem s = carve(smem_raw);
+  const uint32_t tid = threadIdx.x;
+  const uint64_t n = B.n_reads;
+  const uint32_t nd = L.n_dc;
+  const uint32_t np = nd * nd;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+
+  for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint64_t key = uniform_u64(B.key[r]);
+    const uint32_t rtype = uniform_u32(B.type[r]);
+    int32_t status = AM_OK;
+    uint64_t off0 = 0, off1 = 0;
+    if (key >= L.n_keys) {
+      status = AM_ERR_INVALID;
+    } else {
+      off0 = uniform_u64(L.key_off[key]);
+      off1 = uniform_u64(L.key_off[key + 1]);
+      const uint32_t ktype = uniform_u32(L.key_type[key]);
+      const uint32_t kfl = L.key_flags ? uniform_u32(L.key_flags[key]) : 0u;
+      if (off1 > off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES))) status = AM_ERR_CORRUPTED_OPS_CACHE;
+      else if (rtype != (uint32_t)TYPE) status = AM_ERR_INVALID;
+    }
+    if (status != AM_OK) {
+      if (tid == 0) R.status[r] = status;
+      continue;
+    }
+
+    // ---- per-read uniform inputs ----
+    ReadU<DMAX> u;
+    u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+    const uint64_t rstride = B.per_read_clock ? n : 1, ridx = B.per_read_clock ? r : 0;
+    u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
+    u.base_ignore = !B.base_ignore || B.base_ignore[r];
+    u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+      u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+    }
+    u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+    u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+
+    if (tid < 16) s.ctr[tid] = 0;
+    if (TYPE == AM_BCOUNTER) {
+      for (uint32_t i = tid; i < np + nd; i += BLOCK) {
+        int64_t bv = 0;
+        uint32_t bpres = 0;
+        if (i < np) {
+          if (B.base.bc_p) bv = B.base.bc_p[r * np + i];
+          if (B.base.bc_p_pres) bpres = B.base.bc_p_pres[r * np + i];
+        } else {
+          if (B.base.bc_d) bv = B.base.bc_d[r * nd + (i - np)];
+          if (B.base.bc_d_pres) bpres = B.base.bc_d_pres[r * nd + (i - np)];
+        }
+        s.slo[i] = (uint64_t)bv;
+        s.shi[i] = bv < 0 ? -1 : 0;
+        s.spres[i] = bpres;
+      }
+    }
+    __syncthreads();
+    if (TYPE != AM_BCOUNTER && B.base.set_off) {  // base snapshot pairs: births at -1
+      const uint64_t bo = B.base.set_off[r];
+      const uint32_t bl = B.base.set_len[r];
+      if (bl > BCAP) {
+        if (tid == 0) s.ctr[3] = 1;
+      } else {
+        for (uint32_t i = tid; i < bl; i += BLOCK) {
+          s.ba[i] = B.base.set_a[bo + i];
+          s.bb[i] = B.base.set_b[bo + i];
+          s.bp[i] = -1;
+        }
+        if (tid == 0) s.ctr[1] = bl;
+      }
+    }
+    __syncthreads();
+
+    Acc<DMAX> a;
+    a.reset();
+    // ---- stream the log, 1024 ops per tile ----
+    for (uint64_t t0 = off0 & ~(uint64_t)(OPL - 1); t0 < off1; t0 += TILE) {
+      const uint64_t g = t0 + (uint64_t)tid * OPL;
+      if (g < off1) {
+        const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
+        const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
+        const uint64_t ct[OPL] = {c01.x, c01.y, c23.x, c23.y};
+        uint64_t sv[OPL][DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          if (d < (int)nd) {
+            const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
+            const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
+            sv[0][d] = s01.x, sv[1][d] = s01.y, sv[2][d] = s23.x, sv[3][d] = s23.y;
+          } else {
+            sv[0][d] = sv[1][d] = sv[2][d] = sv[3][d] = 0;
+          }
+        }
+        uint32_t sp[OPL] = {u.allmask, u.allmask, u.allmask, u.allmask};
+        if (L.snap_pres) {
+          const u32x4 q = *(const u32x4 *)(L.snap_pres + g);
+          sp[0] = q.x, sp[1] = q.y, sp[2] = q.z, sp[3] = q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < OPL; ++k) {
+          const uint64_t p = g + k;
+          if (p < off0 || p >= off1) continue;
+          const bool txm = u.has_txid && L.op_txid[p] == u.txid;
+          const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
+          if (!eval_op<DMAX, true>(u, meta, ct[k], sv[k], sp[k], txm, p, a)) continue;
+          if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
+          const int32_t pos = (int32_t)(p - off0);
+          if (TYPE == AM_BCOUNTER) {
+            const uint32_t kind = AM_META_KIND(meta);
+            const uint32_t from = (uint32_t)(L.p1[p] & 0xFF), to = (uint32_t)((L.p1[p] >> 8) & 0xFF);
+            if (kind > AM_BC_TRANSFER || from >= nd || to >= nd) {
+              a.flags |= FLAG_BAD;
+              continue;
+            }
+            const uint32_t slot = kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
+            const int64_t v = (int64_t)L.p0[p];
+            const uint64_t old = atomicAdd((unsigned long long *)&s.slo[slot], (unsigned long long)v);
+            const int64_t carry = (old + (uint64_t)v < old) ? 1 : 0;
+            atomicAdd((unsigned long long *)&s.shi[slot], (unsigned long long)((v < 0 ? -1 : 0) + carry));
+            atomicOr(&s.spres[slot], 1u);
+          } else if (TYPE == AM_MVREG) {
+            const uint64_t vo = L.var_off ? L.var_off[p] : 0, ve = L.var_off ? L.var_off[p + 1] : 0;
+            const uint32_t nk = (uint32_t)(ve - vo);
+            if (nk) {
+              const uint32_t i0 = atomicAdd(&s.ctr[0], nk);
+              if (i0 + nk > KCAP) {
+                s.ctr[3] = 1;
+              } else {
+                for (uint32_t i = 0; i < nk; ++i) {
+                  s.ka[i0 + i] = L.var_data[vo + i];
+                  s.kb[i0 + i] = 0;
+                  s.kp[i0 + i] = pos;
+                }
+              }
+            }
+            if (AM_META_KIND(meta) != AM_MV_RESET) {
+              const uint32_t bi = atomicAdd(&s.ctr[1], 1u);
+              if (bi >= BCAP) {
+                s.ctr[3] = 1;
+              } else {
+                s.ba[bi] = L.p0[p];
+                s.bb[bi] = L.p1[p];
+                s.bp[bi] = pos;
+              }
+            }
+          } else {  // AW-set effect entries [elem, n_add, n_rm, add..., rm...]
+            uint64_t q = L.var_off ? L.var_off[p] : 0;
+            const uint64_t qe = L.var_off ? L.var_off[p + 1] : 0;
+            while (q < qe) {
+              if (q + 3 > qe) {
+                a.flags |= FLAG_BAD;
+                break;
+              }
+              const uint64_t e = L.var_data[q], na = L.var_data[q + 1], nr = L.var_data[q + 2];
+              if (na > qe - q || nr > qe - q || q + 3 + na + nr > qe) {
+                a.flags |= FLAG_BAD;
+                break;
+              }
+              if (na) {
+                const uint32_t bi = atomicAdd(&s.ctr[1], (uint32_t)na);
+                if (bi + na > BCAP) {
+                  s.ctr[3] = 1;
+                } else {
+                  for (uint32_t i = 0; i < na; ++i) {
+                    s.ba[bi + i] = e;
+                    s.bb[bi + i] = L.var_data[q + 3 + i];
+                    s.bp[bi + i] = pos;
+                  }
+                }
+              }
+              if (nr) {
+                const uint32_t ki = atomicAdd(&s.ctr[0], (uint32_t)nr);
+                if (ki + nr > KCAP) {
+                  s.ctr[3] = 1;
+                } else {
+                  for (uint32_t i = 0; i < nr; ++i) {
+                    s.ka[ki + i] = L.var_data[q + 3 + na + i];  // token
+                    s.kb[ki + i] = e;
+                    s.kp[ki + i] = pos;
+                  }
+                }
+              }
+              q += 3 + na + nr;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- scalar outputs (block reductions) ----
+    const uint32_t count = (uint32_t)block_red_u64(s, wave_sum_u32(a.count), 0);
+    const uint32_t flags = (uint32_t)block_red_u64(s, wave_or_u32(a.flags), 1);
+    const uint32_t pres = (uint32_t)block_red_u64(s, wave_or_u32(a.pres), 1);
+    const uint64_t min_excl = block_red_u64(s, wave_min_u64(a.min_excl), 3);
+    uint64_t mx[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? block_red_u64(s, wave_max_u64(a.mx[d]), 2) : 0;
+    status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+    if (status == AM_OK && s.ctr[3]) status = AM_ERR_CAPACITY;
+
+    if (status == AM_OK && TYPE == AM_BCOUNTER) {
+      uint32_t *ovf = &s.ctr[8];  // no static __shared__: keeps the dynamic LDS base 16-byte aligned
+      if (tid == 0) *ovf = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < np + nd; i += BLOCK) {
+        const uint64_t lo = s.slo[i];
+        const int64_t hi = s.shi[i];
+        if (hi != ((int64_t)lo < 0 ? -1 : 0)) atomicOr(ovf, 1u);
+      }
+      __syncthreads();
+      if (*ovf) status = AM_ERR_OVERFLOW;
+      else
+        for (uint32_t i = tid; i < np + nd; i += BLOCK) {
+          if (i < np) {
+            R.value.bc_p[r * np + i] = (int64_t)s.slo[i];
+            R.value.bc_p_pres[r * np + i] = s.spres[i] ? 1 : 0;
+          } else {
+            R.value.bc_d[r * nd + (i - np)] = (int64_t)s.slo[i];
+            R.value.bc_d_pres[r * nd + (i - np)] = s.spres[i] ? 1 : 0;
+          }
+        }
+    }
+    if (status == AM_OK && TYPE != AM_BCOUNTER) {
+      const uint32_t nk = s.ctr[0], nb = s.ctr[1];
+      block_sort(s.ka, s.kb, s.kp, nk, KCAP);  // by (token, elem, pos)
+      if (tid == 0) s.ctr[2] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < nb; i += BLOCK) {
+        // kill key of this birth: AW (tok, elem), MV (tok, 0)
+        const uint64_t qa = s.bb[i], qb = TYPE == AM_AWSET ? s.ba[i] : 0;
+        // upper bound of (qa, qb, +inf)
+        uint32_t lo = 0, hi = nk;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          const bool le = s.ka[mid] < qa || (s.ka[mid] == qa && s.kb[mid] <= qb);
+          if (le) lo = mid + 1;
+          else hi = mid;
+        }
+        bool alive = true;
+        if (lo > 0 && s.ka[lo - 1] == qa && s.kb[lo - 1] == qb) alive = s.kp[lo - 1] <= s.bp[i];
+        if (alive) {
+          const uint32_t o = atomicAdd(&s.ctr[2], 1u);
+          s.oa[o] = s.ba[i];
+          s.ob[o] = s.bb[i];
+        }
+      }
+      __syncthreads();
+      const uint32_t no = s.ctr[2];
+      block_sort(s.oa, s.ob, nullptr, no, BCAP);
+      // drop duplicates and write the CSR (compaction by wave ballots)
+      const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
+      uint32_t base = 0;
+      for (uint32_t c = 0; c < no; c += BLOCK) {
+        const uint32_t i = c + tid;
+        const bool keep = i < no && (i == 0 || s.oa[i] != s.oa[i - 1] || s.ob[i] != s.ob[i - 1]);
+        const uint64_t m = __ballot(keep);
+        const uint32_t w = tid >> 6, l = tid & 63;
+        const uint32_t before = __popcll(m & ((1ull << l) - 1));
+        if (l == 0) s.ctr[4 + w] = __popcll(m);
+        __syncthreads();
+        uint32_t woff = 0;
+        for (uint32_t k = 0; k < w; ++k) woff += s.ctr[4 + k];
+        const uint32_t total = s.ctr[4] + s.ctr[5] + s.ctr[6] + s.ctr[7];
+        if (keep) {
+          const uint32_t o = base + woff + before;
+          if (o < ocap) {
+            R.value.set_a[ooff + o] = s.oa[i];
+            R.value.set_b[ooff + o] = s.ob[i];
+          }
+        }
+        base += total;
+        __syncthreads();
+      }
+      if (base > ocap) status = AM_ERR_CAPACITY;
+      else if (tid == 0) R.value.set_len[r] = base;
+    }
+
+    if (tid == 0) {
+      R.status[r] = status;
+      R.flags[r] = (uint8_t)(flags & 0xFFu);
+      if (status == AM_OK) {
+        const uint64_t idb = L.key_id_base ? L.key_id_base[key] : 1;
+        const uint64_t nops = off1 - off0;
+        int64_t nlo;
+        if (min_excl != NONE)
+          nlo = (L.op_id ? (int64_t)L.op_id[min_excl] : (int64_t)(idb + (min_excl - off0))) - 1;
+        else
+          nlo = nops == 0 ? 0 : (L.op_id ? (int64_t)L.op_id[off1 - 1] : (int64_t)(idb + nops - 1));
+        R.new_last_op[r] = nlo;
+        const bool ign = u.base_ignore && count == 0;
+        const uint32_t opres = ign ? 0u : (pres | u.cpres);
+        R.last_ct_ignore[r] = ign ? 1 : 0;
+        R.last_ct_pres[r] = opres;
+        for (int d = 0; d < DMAX; ++d) {
+          if (d < (int)nd) {
+            const uint64_t m = mx[d] > u.C0[d] ? mx[d] : u.C0[d];
+            R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? m : 0;
+          }
+        }
+        R.is_new_ss[r] = count > 0;
+        R.count[r] = count;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int TYPE>
+int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+  if (TYPE != AM_BCOUNTER && (!R->value.set_off || !R->value.set_len || !R->value.set_a || !R->value.set_b)) {
+    am_set_error("set results need value.set_off/set_len/set_a/set_b");
+    return AM_ERR_INVALID;
+  }
+  if (TYPE == AM_BCOUNTER && (!R->value.bc_p || !R->value.bc_p_pres || !R->value.bc_d || !R->value.bc_d_pres)) {
+    am_set_error("bcounter results need value.bc_p/bc_p_pres/bc_d/bc_d_pres");
+    return AM_ERR_INVALID;
+  }
+  if (TYPE == AM_BCOUNTER && (size_t)L->n_dc * L->n_dc + L->n_dc > KCAP) {
+    am_set_error("bcounter: n_dc too large for the LDS slots");
+    return AM_ERR_UNSUPPORTED;
+  }
+  uint64_t blocks = B->n_reads;
+  const uint64_t cap = (uint64_t)ctx->n_cu * 2;  // 2 groups per CU (78 KB LDS each)
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return AM_OK;
+  const uint32_t nd = L->n_dc;
+#define AM_S(D)                                                                                        \
+  {                                                                                                    \
+    static bool attr = false;                                                                          \
+    if (!attr) {                                                                                       \
+      AM_HIP(hipFuncSetAttribute((const void *)k_sets<D, TYPE>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                 (int)SMEM_BYTES));                                                    \
+      attr = true;                                                                                     \
+    }                                                                                                  \
+    hipLaunchKernelGGL((k_sets<D, TYPE>), dim3((unsigned)blocks), dim3(BLOCK), SMEM_BYTES, ctx->stream, \
+                       *L, *B, *R);                                                                    \
+  }                                                                                                    \
+  break;
+  switch (nd <= 1 ? 1 : nd <= 2 ? 2 : nd <= 3 ? 3 : nd <= 4 ? 4 : nd <= 8 ? 8 : nd <= 16 ? 16 : 32) {
+    case 1: AM_S(1)
+    case 2: AM_S(2)
+    case 3: AM_S(3)
+    case 4: AM_S(4)
+    case 8: AM_S(8)
+    case 16: AM_S(16)
+    default: AM_S(32)
+  }
+#undef AM_S
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
+}  // namespace
+
+int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+  switch (B->type_hint) {
+    case AM_AWSET: return launch_sets<AM_AWSET>(ctx, L, B, R);
+    case AM_MVREG: return launch_sets<AM_MVREG>(ctx, L, B, R);
+    case AM_BCOUNTER: return launch_sets<AM_BCOUNTER>(ctx, L, B, R);
+    default: return AM_ERR_UNSUPPORTED;
+  }
+}

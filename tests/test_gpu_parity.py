@@ -17,7 +17,8 @@ from tests.test_oracle_c import _dcmap, kat_ops, run_kat_cases
 
 pytestmark = pytest.mark.gpu
 
-GPU_TYPES = [abi.AM_PN, abi.AM_LWW]
+GPU_TYPES = [abi.AM_PN, abi.AM_LWW, abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER]
+SET_TYPES = (abi.AM_AWSET, abi.AM_MVREG)
 
 
 @pytest.fixture(scope="module")
@@ -47,11 +48,12 @@ def test_gpu_kat(mat, kat):
     run_kat_cases(kat, run)
 
 
-def _batch_compare(log, reads, mat, n_dc):
+def _batch_compare(log, reads, mat, n_dc, cap=256):
     st = mat.store(log)
-    got = mat.read_batch(st, reads)
+    caps = [cap] * len(reads)
+    got = mat.read_batch(st, reads, caps)
     st.close()
-    ref = amo.materialize(log, HostBatch(n_dc, reads))
+    ref = amo.materialize(log, HostBatch(n_dc, reads, caps))
     for i in range(len(reads)):
         a, b = got.result(i), ref.result(i)
         assert a == b, (i, reads[i], a, b)
@@ -67,8 +69,11 @@ def test_gpu_random_batches(mat, t, seed):
     n_dc = [1, 3, 5, 16][seed]
     partial = seed in (1, 3)
     keys, reads = [], []
+    lens = [0, 1, 3, 17, 64, 255, 256, 257, 400] if t in SET_TYPES else [0, 1, 3, 17, 64, 255, 256, 257, 700]
+    if t == abi.AM_BCOUNTER:
+        n_dc = min(n_dc, 8)
     for k in range(60):
-        n_ops = rng.choice([0, 1, 3, 17, 64, 255, 256, 257, 700]) if k % 5 else rng.randint(0, 40)
+        n_ops = rng.choice(lens) if k % 5 else rng.randint(0, 40)
         ops = randlog.rand_key_ops(rng, t, n_dc, n_ops, partial=partial, txids=seed == 2,
                                    bad_rate=0.002 if seed == 3 else 0.0, t0=rng.randint(0, 100))
         keys.append(ops)
@@ -262,3 +267,29 @@ def test_gpu_rccl_single_rank(mat):
     mat.sync()
     assert lanes.cpu().tolist() == [5, 7, 1]
     mat.L.am_comm_destroy(comm)
+
+
+def test_gpu_set_capacity_status(mat):
+    """A read whose births exceed the LDS capacity reports AM_ERR_CAPACITY (documented gap)."""
+    ops = [Op(abi.AM_MVREG, 0, 10 + i, {0: 1}, ("assign", i, 1000 + i, [])) for i in range(1100)]
+    log = HostLog(1, [ops])
+    st = mat.store(log)
+    got = mat.read_batch(st, [Read(0, abi.AM_MVREG, {0: 10**6})], [4096])
+    st.close()
+    assert got.result(0) == ("error", abi.AM_ERR_CAPACITY)
+
+
+def test_gpu_reference_system_shapes(mat):
+    """Value shapes the reference's system tests assert (test/singledc/clocksi_SUITE.erl:160-205):
+    AW-set add a, add b, remove a -> [b]; MV register a -> b -> c -> [c]."""
+    a, b = 97, 98
+    aw = [Op(abi.AM_AWSET, 0, 11, {0: 10}, [(a, [1], [])]),
+          Op(abi.AM_AWSET, 0, 12, {0: 11}, [(b, [2], [])]),
+          Op(abi.AM_AWSET, 0, 13, {0: 12}, [(a, [], [1])])]
+    mv = [Op(abi.AM_MVREG, 0, 11, {0: 10}, ("assign", 1, 7, [])),
+          Op(abi.AM_MVREG, 0, 12, {0: 11}, ("assign", 2, 8, [7])),
+          Op(abi.AM_MVREG, 0, 13, {0: 12}, ("assign", 3, 9, [8]))]
+    for t, ops, exp in ((abi.AM_AWSET, aw, [(b, 2)]), (abi.AM_MVREG, mv, [(3, 9)])):
+        log = HostLog(1, [ops])
+        got = _batch_compare(log, [Read(0, t, {0: 20})], mat, 1)
+        assert got.result(0)[1] == exp
