@@ -271,7 +271,8 @@ def main():
                    "step": "GST min all-reduce (RCCL) + materialize all keys"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(workload),
-                     "kernel": "k_materialize_scalar", "kernel_ms": kern_ms,
+                     "kernel": "k_stream" if type_ in (abi.AM_PN, abi.AM_LWW) else "k_sets",
+                     "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,
     }
