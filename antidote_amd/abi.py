@@ -85,8 +85,12 @@ class am_read_result(ctypes.Structure):
 class am_synth_params(ctypes.Structure):
     _fields_ = [
         ("seed", c_uint64), ("n_keys", c_uint64), ("ops_per_key", c_uint32), ("n_dc", c_uint32),
-        ("type", c_uint32), ("key_base", c_uint32), ("max_lag", c_uint32), ("_pad", c_uint32),
+        ("type", c_uint32), ("key_base", c_uint32), ("max_lag", c_uint32), ("zipf_milli", c_uint32),
+        ("total_ops", c_uint64), ("hot_cap", c_uint32), ("universe", c_uint32),
     ]
+
+
+AM_SYNTH_MV_BC = 6
 
 
 # (name, restype, argtypes) of every exported symbol declared in include/antidote_mat.h

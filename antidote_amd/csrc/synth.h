@@ -77,3 +77,44 @@ AM_HD uint64_t am_syn_lww_ts(uint64_t seed, uint64_t key, uint64_t i, uint32_t n
 AM_HD uint64_t am_syn_lww_val(uint64_t seed, uint64_t key, uint64_t i) {
   return am_syn_h(seed, key, i, 20);
 }
+
+// ---- mixed workloads: the key's CRDT type ----
+//   C4 mixed (type 0): 40% PN, 20% LWW, 20% AW-set, 20% MV register
+//   C5 (type 6):       50% MV register, 50% bounded counter
+AM_HD uint32_t am_syn_key_type(uint64_t seed, uint64_t key, uint32_t type) {
+  const uint64_t h = am_syn_h(seed, key, 0, 40) % 10;
+  if (type == 0) return h < 4 ? 1u : h < 6 ? 2u : h < 8 ? 3u : 4u;
+  if (type == 6) return h < 5 ? 4u : 5u;
+  return type;
+}
+
+// ---- add-wins set: causal history, every op observes every earlier op ----
+// Op i touches element elem(i) = (i*A + B) mod U (U a power of two, A odd: a
+// bijection on each period of U ops, so the previous op on the same element is
+// op i-U).  70% adds {e, [tok(i)], Observed}, 30% removes {e, [], Observed},
+// where Observed = [tok(i-U)] if op i-U was an add (the element's only live token
+// in a sequential history), else [].
+AM_HD uint64_t am_syn_aw_elem(uint64_t seed, uint64_t key, uint64_t i, uint32_t U) {
+  const uint64_t hk = am_syn_h(seed, key, 0, 41);
+  return (i * (hk | 1ull) + (hk >> 20)) & (uint64_t)(U - 1);
+}
+AM_HD bool am_syn_aw_is_add(uint64_t seed, uint64_t key, uint64_t i) { return am_syn_h(seed, key, i, 42) % 10 < 7; }
+AM_HD uint64_t am_syn_tok(uint64_t seed, uint64_t key, uint64_t i) { return am_syn_h(seed, key, i, 43); }
+AM_HD uint32_t am_syn_aw_words(uint64_t seed, uint64_t key, uint64_t i, uint32_t U) {
+  const bool rm = i >= U && am_syn_aw_is_add(seed, key, i - U);
+  return 3u + (am_syn_aw_is_add(seed, key, i) ? 1u : 0u) + (rm ? 1u : 0u);
+}
+
+// ---- MV register: assign {val(i), tok(i), [tok(i-1)]} (sequential overrides) ----
+AM_HD uint64_t am_syn_mv_val(uint64_t seed, uint64_t key, uint64_t i) { return am_syn_h(seed, key, i, 44) % 1000; }
+AM_HD uint32_t am_syn_mv_words(uint64_t i) { return i >= 1 ? 1u : 0u; }
+
+// ---- bounded counter: {{increment,V},Id} | {{decrement,V},Id} | {{transfer,V,To},From} ----
+AM_HD uint32_t am_syn_bc_kind(uint64_t seed, uint64_t key, uint64_t i) { return (uint32_t)(am_syn_h(seed, key, i, 45) % 3); }
+AM_HD uint32_t am_syn_bc_from(uint64_t seed, uint64_t key, uint64_t i, uint32_t D) {
+  return (uint32_t)(am_syn_h(seed, key, i, 46) % D);
+}
+AM_HD uint32_t am_syn_bc_to(uint64_t seed, uint64_t key, uint64_t i, uint32_t D) {
+  return (uint32_t)(am_syn_h(seed, key, i, 47) % D);
+}
+AM_HD uint64_t am_syn_bc_amount(uint64_t seed, uint64_t key, uint64_t i) { return 1 + am_syn_h(seed, key, i, 48) % 100; }

@@ -23,7 +23,7 @@ class DeviceReads:
     base snapshot = ignore (fresh) unless set_base() is used."""
 
     def __init__(self, n_reads: int, n_dc: int, type_: int, clock: Sequence[int], pres: Optional[int] = None,
-                 device: str = "cuda", keys: Optional[torch.Tensor] = None):
+                 device: str = "cuda", keys: Optional[torch.Tensor] = None, set_cap: int = 96):
         self.n, self.n_dc, self.type = n_reads, n_dc, type_
         dev = torch.device(device)
         self.dev = dev
@@ -47,6 +47,19 @@ class DeviceReads:
         self.v0 = z(torch.int64, n_reads)
         self.v1 = z(torch.int64, n_reads)
         self.vflag = z(torch.uint8, n_reads)
+        self.set_off = self.set_len = self.set_a = self.set_b = None
+        self.bc_p = self.bc_pp = self.bc_d = self.bc_dp = None
+        if type_ in (abi.AM_AWSET, abi.AM_MVREG):
+            self.set_cap = set_cap
+            self.set_off = torch.arange(0, (n_reads + 1) * set_cap, set_cap, dtype=torch.int64, device=dev)
+            self.set_len = z(torch.int32, n_reads)
+            self.set_a = z(torch.int64, n_reads * set_cap)
+            self.set_b = z(torch.int64, n_reads * set_cap)
+        elif type_ == abi.AM_BCOUNTER:
+            self.bc_p = z(torch.int64, n_reads, n_dc * n_dc)
+            self.bc_pp = z(torch.uint8, n_reads, n_dc * n_dc)
+            self.bc_d = z(torch.int64, n_reads, n_dc)
+            self.bc_dp = z(torch.uint8, n_reads, n_dc)
 
     def set_base_from(self, other: "DeviceReads"):
         """Use another batch's results as the cached base snapshots (incremental reads)."""
@@ -72,8 +85,41 @@ class DeviceReads:
         r.last_ct_ignore, r.is_new_ss, r.count, r.flags = (p(self.last_ct_ignore), p(self.is_new_ss), p(self.count),
                                                            p(self.flags))
         r.value.v0, r.value.v1, r.value.vflag = p(self.v0), p(self.v1), p(self.vflag)
+        r.value.set_off, r.value.set_len, r.value.set_a, r.value.set_b = (p(self.set_off), p(self.set_len),
+                                                                          p(self.set_a), p(self.set_b))
+        r.value.bc_p, r.value.bc_p_pres, r.value.bc_d, r.value.bc_d_pres = (p(self.bc_p), p(self.bc_pp),
+                                                                            p(self.bc_d), p(self.bc_dp))
         self._keep = (b, r)
         return b, r
+
+    def values(self, idx):
+        """Decoded values of reads idx (host), in the oracle's rendering."""
+        out = []
+        nd = self.n_dc
+        if self.type in (abi.AM_AWSET, abi.AM_MVREG):
+            sl = self.set_len.cpu().numpy()
+            sa = self.set_a.cpu().numpy().view(np.uint64)
+            sb = self.set_b.cpu().numpy().view(np.uint64)
+            for i in idx:
+                o = int(i) * self.set_cap
+                out.append([(int(sa[o + j]), int(sb[o + j])) for j in range(int(sl[i]))])
+        elif self.type == abi.AM_BCOUNTER:
+            bp, bpp = self.bc_p.cpu().numpy(), self.bc_pp.cpu().numpy()
+            bd, bdp = self.bc_d.cpu().numpy(), self.bc_dp.cpu().numpy()
+            for i in idx:
+                pd = {(j // nd, j % nd): int(bp[i, j]) for j in range(nd * nd) if bpp[i, j]}
+                dd = {j: int(bd[i, j]) for j in range(nd) if bdp[i, j]}
+                out.append((pd, dd))
+        else:
+            v0 = self.v0.cpu().numpy()
+            v1 = self.v1.cpu().numpy().view(np.uint64)
+            vf = self.vflag.cpu().numpy()
+            for i in idx:
+                if self.type == abi.AM_PN:
+                    out.append(int(v0[i]))
+                else:
+                    out.append((int(v0[i:i + 1].view(np.uint64)[0]), int(v1[i]), bool(vf[i])))
+        return out
 
     def host(self, lo: int = 0, hi: Optional[int] = None):
         """Result columns of reads [lo, hi) as numpy (u64 views where the ABI is unsigned)."""

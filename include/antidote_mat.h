@@ -254,13 +254,18 @@ uint32_t am_key_partition(int64_t key, uint32_t n_partitions);
 typedef struct am_synth_params {
   uint64_t seed;
   uint64_t n_keys;
-  uint32_t ops_per_key;  /* uniform log length (0 => use zipf)                 */
+  uint32_t ops_per_key;  /* uniform log length (ignored when zipf_milli != 0)  */
   uint32_t n_dc;
-  uint32_t type;         /* am_type, or 0 for mixed (40/20/20/20 PN/LWW/AW/MV) */
+  uint32_t type;         /* am_type, or 0 for mixed (40/20/20/20 PN/LWW/AW/MV),
+                            or 6 for MV register + bounded counter (50/50)    */
   uint32_t key_base;     /* global index of key 0 (for sharding)               */
   uint32_t max_lag;      /* snapshot lag in ops (concurrency window)           */
-  uint32_t _pad;
+  uint32_t zipf_milli;   /* Zipf exponent x1000 for key popularity; 0 = uniform */
+  uint64_t total_ops;    /* Zipf: target total ops over all keys               */
+  uint32_t hot_cap;      /* Zipf: cap on one key's log length                  */
+  uint32_t universe;     /* AW-set element universe per key (power of two)     */
 } am_synth_params;
+#define AM_SYNTH_MV_BC 6
 /* Device log owned by the returned store. */
 int am_synth_store(am_ctx *ctx, const am_synth_params *p, am_store **out);
 /* The read clock the generator's quantile q selects (q in [0,1]); host output [n_dc]. */
