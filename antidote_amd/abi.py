@@ -18,7 +18,7 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint8
 import torch  # noqa: F401  (must precede the HIP library, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libantidote_mat.so")
+LIB_PATH = os.environ.get("AM_LIB") or os.path.join(HERE, "libantidote_mat.so")  # AM_LIB: A/B of builds only
 
 AM_PN, AM_LWW, AM_AWSET, AM_MVREG, AM_BCOUNTER = 1, 2, 3, 4, 5
 TYPE_BY_NAME = {
@@ -53,6 +53,7 @@ class am_op_log(ctypes.Structure):
         ("op_meta", c_void_p), ("commit_time", c_void_p), ("snap_vc", c_void_p), ("snap_pres", c_void_p),
         ("op_txid", c_void_p), ("op_id", c_void_p), ("p0", c_void_p), ("p1", c_void_p),
         ("var_off", c_void_p), ("var_data", c_void_p),
+        ("ct_meta", c_void_p), ("snap_delta", c_void_p),
     ]
 
 

@@ -48,3 +48,4 @@ int am_launch_gst_finalize(am_ctx *ctx, uint32_t n_dc, const uint64_t *lanes, ui
 int am_launch_synth(am_ctx *ctx, const am_synth_params *p, am_op_log *L /* device arrays allocated */);
 int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
 int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
+int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)

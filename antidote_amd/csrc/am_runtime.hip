@@ -201,6 +201,7 @@ int am_store_create(am_ctx *c, const am_op_log *h, am_store **out) {
       rc = AM_ERR_HIP;
     }
   }
+  if (!rc) rc = am_store_pack(st);
   if (rc) {
     am_store_destroy(st);
     return rc;

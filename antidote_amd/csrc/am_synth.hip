@@ -224,6 +224,11 @@ int am_synth_store(am_ctx *c, const am_synth_params *p, am_store **out) {
   d.var_off = (const uint64_t *)var_off;
   d.var_data = (const uint64_t *)var_data;
   d.n_var = n_var;
+  rc = am_store_pack(st);
+  if (rc) {
+    am_store_destroy(st);
+    return rc;
+  }
   *out = st;
   return AM_OK;
 }

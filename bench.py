@@ -45,10 +45,12 @@ CONFIGS = {
 }
 
 
-def bytes_per_op(type_: int, n_dc: int) -> int:
-    """Algorithmic HBM bytes read per op by the materialize kernel:
-    op_meta 1 + commit_time 8 + snapshot_time 8*D + payload (PN 8, LWW 16)."""
-    return 1 + 8 + 8 * n_dc + (16 if type_ == abi.AM_LWW else 8)
+def bytes_per_op(type_: int, n_dc: int, packed: bool = True) -> int:
+    """Algorithmic HBM bytes read per op by the materialize kernel.
+    Packed view (am_pack.hip): ct_meta 8 + snapshot deltas 4*D + payload (PN 8, LWW 16);
+    full view: op_meta 1 + commit_time 8 + snapshot_time 8*D + payload."""
+    payload = 16 if type_ == abi.AM_LWW else 8
+    return (8 + 4 * n_dc + payload) if packed else (1 + 8 + 8 * n_dc + payload)
 
 
 def bytes_per_key(type_: int, n_dc: int) -> int:
@@ -246,7 +248,8 @@ def main():
     ms = ctypes.c_float()
     abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
     kern_ms = ms.value / kern_iters
-    alg_bytes = n_keys * (n_ops * bytes_per_op(type_, n_dc) + bytes_per_key(type_, n_dc))
+    packed = bool(dlog.ct_meta) and os.environ.get("AM_PACKED", "1") != "0"
+    alg_bytes = n_keys * (n_ops * bytes_per_op(type_, n_dc, packed) + bytes_per_key(type_, n_dc))
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
     total_ops = world * n_keys * n_ops * args.steps
@@ -273,7 +276,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(workload),
                      "kernel": "k_stream" if type_ in (abi.AM_PN, abi.AM_LWW) else "k_sets",
                      "kernel_ms": kern_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     "layout": "packed (ct_meta + int32 snapshot deltas)" if packed else "full"},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -129,7 +129,15 @@ typedef struct am_op_log {
   const uint64_t *p1;          /* [n_ops]                                            */
   const uint64_t *var_off;     /* [n_ops+1] or NULL                                  */
   const uint64_t *var_data;    /* [n_var]                                            */
+  /* Packed streaming view, built on the device by am_store_create / am_synth_store
+   * (NULL in host logs).  ct_meta[p] = commit_time | esc << 55 | op_meta << 56 and
+   * snap_delta[d][p] = commit_time - snap_vc[d][p] as int32; esc = 1 when the op
+   * does not fit (commit_time >= 2^55 or a delta outside int32), and the kernels then
+   * read that op from the full columns above.  Cuts C2 from 49 to 36 B/op. */
+  const uint64_t *ct_meta;     /* [n_ops]                                            */
+  const int32_t *snap_delta;   /* [n_dc][snap_stride]                                */
 } am_op_log;
+#define AM_CT_ESC (1ull << 55)
 
 /*
  * CRDT values (base snapshots in, materialized values out), SoA over reads.

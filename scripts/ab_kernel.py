@@ -25,16 +25,19 @@ clock = (ctypes.c_uint64 * n_dc)()
 abi.lib().am_synth_read_clock(ctypes.byref(p), q, clock)
 reads = DeviceReads(n_keys, n_dc, type_, list(clock))
 torch.cuda.synchronize()
-alg = n_keys * (n_ops * bench.bytes_per_op(type_, n_dc) + bench.bytes_per_key(type_, n_dc))
+alg = n_keys * (n_ops * bench.bytes_per_op(type_, n_dc, False) + bench.bytes_per_key(type_, n_dc))  # full-view bytes
 times = {v: [] for v in variants}
 ref = None
 for rd in range(rounds):
     for v in variants:
-        kv, _, rest = v.partition(":")
-        iv, _, ev = rest.partition(":")
-        os.environ["AM_KERNEL"] = kv
-        os.environ["AM_INTERLEAVE"] = iv or "1"
-        os.environ["AM_EXP"] = ev or "0"
+        # variant = "label" or "label:ENV=VAL;ENV=VAL"
+        label, _, envs = v.partition(":")
+        for k in ("AM_KERNEL", "AM_PACKED"):
+            os.environ.pop(k, None)
+        os.environ["AM_KERNEL"] = label
+        for kv in filter(None, envs.split(";")):
+            k, _, val = kv.partition("=")
+            os.environ[k] = val
         materialize(mat, dlog, reads)  # warm
         abi.lib().am_timer_start(mat.ctx)
         for _ in range(5):
@@ -45,9 +48,7 @@ for rd in range(rounds):
         if rd == 0:
             h = reads.host()
             sig = [h[k].tobytes() for k in ("status", "new_last_op", "last_ct", "count", "v0", "v1", "vflag")]
-            if ":" in v and v.count(":") >= 2 and not v.endswith(":0"):
-                pass
-            elif ref is None:
+            if ref is None:
                 ref = sig
             else:
                 assert sig == ref, f"variant {v} differs"

@@ -22,6 +22,43 @@ __global__ void flat(const u64x2 *a, size_t n2, u64 *out) {
   if (acc == 0x1234567) out[0] = acc;
 }
 
+__global__ void cols6(const u64 *c0, const u64 *c1, const u64 *c2, const u64 *c3, const u64 *c4, const u64 *c5,
+                      size_t n_ops, u64 *out) {
+  u64 acc = 0;
+  const size_t n4 = n_ops / 4;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
+    const size_t g = q * 4;
+    const u64 *cs[6] = {c0, c1, c2, c3, c4, c5};
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      u64x2 a = *(const u64x2 *)(cs[c] + g), b = *(const u64x2 *)(cs[c] + g + 2);
+      acc ^= a.x + a.y + b.x + b.y;
+    }
+  }
+  if (acc == 0x1234567) out[0] = acc;
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// 3 u64 columns + 3 u32 columns (compressed snapshot deltas)
+__global__ void cols33(const u64 *c0, const u64 *c1, const u64 *c2, const unsigned *d0, const unsigned *d1,
+                       const unsigned *d2, size_t n_ops, u64 *out) {
+  u64 acc = 0;
+  const size_t n4 = n_ops / 4;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
+    const size_t g = q * 4;
+    const u64 *cs[3] = {c0, c1, c2};
+    const unsigned *ds[3] = {d0, d1, d2};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      u64x2 a = *(const u64x2 *)(cs[c] + g), b = *(const u64x2 *)(cs[c] + g + 2);
+      acc ^= a.x + a.y + b.x + b.y;
+      u32x4 v = *(const u32x4 *)(ds[c] + g);
+      acc ^= v.x + v.y + v.z + v.w;
+    }
+  }
+  if (acc == 0x1234567) out[0] = acc;
+}
+
 template <bool NT>
 __global__ void cols(const unsigned *meta, const u64 *c0, const u64 *c1, const u64 *c2, const u64 *c3, const u64 *c4,
                      const u64 *c5, size_t n_ops, u64 *out) {
@@ -66,7 +103,7 @@ int main(int argc, char **argv) {
   const size_t total = n_ops * (1 + 6 * 8);
   for (int blocks_per_cu : {4, 8, 16}) {
     const int grid = 256 * blocks_per_cu;
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 5; ++mode) {
       float best = 1e9;
       for (int it = 0; it < 6; ++it) {
         hipEventRecord(e0);
@@ -75,6 +112,12 @@ int main(int argc, char **argv) {
         else if (mode == 1)
           hipLaunchKernelGGL(cols<false>, dim3(grid), dim3(256), 0, 0, meta, cols_d[0], cols_d[1], cols_d[2], cols_d[3],
                              cols_d[4], cols_d[5], n_ops, out);
+        else if (mode == 3)
+          hipLaunchKernelGGL(cols6, dim3(grid), dim3(256), 0, 0, cols_d[0], cols_d[1], cols_d[2], cols_d[3], cols_d[4],
+                             cols_d[5], n_ops, out);
+        else if (mode == 4)
+          hipLaunchKernelGGL(cols33, dim3(grid), dim3(256), 0, 0, cols_d[0], cols_d[1], cols_d[2], (const unsigned *)cols_d[3],
+                             (const unsigned *)cols_d[4], (const unsigned *)cols_d[5], n_ops, out);
         else
           hipLaunchKernelGGL(cols<true>, dim3(grid), dim3(256), 0, 0, meta, cols_d[0], cols_d[1], cols_d[2], cols_d[3],
                              cols_d[4], cols_d[5], n_ops, out);
@@ -84,7 +127,7 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         if (it > 0 && ms < best) best = ms;
       }
-      const double b = mode == 0 ? (double)bytes_col : (double)total;
+      const double b = mode == 0 ? (double)bytes_col : mode == 3 ? (double)n_ops * 48 : mode == 4 ? (double)n_ops * 36 : (double)total;
       printf("blocks/CU %2d mode %d: %.3f ms  %.0f GB/s\n", blocks_per_cu, mode, best, b / (best * 1e-3) / 1e9);
     }
   }

@@ -293,3 +293,36 @@ def test_gpu_reference_system_shapes(mat):
         log = HostLog(1, [ops])
         got = _batch_compare(log, [Read(0, t, {0: 20})], mat, 1)
         assert got.result(0)[1] == exp
+
+
+@pytest.mark.parametrize("t", [abi.AM_PN, abi.AM_LWW])
+def test_gpu_packed_view_escapes(mat, t):
+    """Ops whose snapshot entries lie > 2^31 us from the commit time, or whose commit time
+    is >= 2^55, do not fit the packed streaming view: they are flagged and read from the
+    full columns.  Mix fitting and escaping ops in one log, read at several clocks."""
+    rng = random.Random(77 + t)
+    big = 2**40
+    keys, reads = [], []
+    for k in range(40):
+        ops = []
+        ct = 10**6
+        for i in range(rng.choice([5, 100, 300])):
+            ct += rng.randint(1, 3)
+            mode = rng.random()
+            if mode < 0.1:
+                c, snap = ct + big, {0: ct - 5, 1: ct + big - 7, 2: 3}             # far behind
+            elif mode < 0.15:
+                c, snap = 2**55 + ct, {0: 2**55 + ct - 1, 1: 2**55, 2: 2**55 + 1}  # >= 2^55
+            elif mode < 0.2:
+                c, snap = ct, {0: ct + 2**33, 1: ct - 1, 2: ct - 2}                  # skewed ahead
+            else:
+                c, snap = ct, {d: ct - rng.randint(1, 50) for d in range(3)}
+            dc = rng.randrange(3)
+            eff = rng.randint(-9, 9) if t == abi.AM_PN else (rng.randint(1, 10**6), rng.randint(0, 9))
+            ops.append(Op(t, dc, c, snap, eff))
+        keys.append(ops)
+        top = max(op.commit_time for op in ops)
+        clock = {d: rng.choice([ct, ct + big, top, 2**55 + ct + 10, 2**62]) for d in range(3)}
+        reads.append(Read(k, t, clock))
+    log = HostLog(3, keys, key_types=[t] * len(keys))
+    _batch_compare(log, reads, mat, 3)
