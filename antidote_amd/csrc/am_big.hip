@@ -1,0 +1,606 @@
+// am_big.hip -- materialize/4 for add-wins-set / MV-register reads beyond the LDS
+// tier: Zipf-hot keys with up to 2^20+ ops, whose births/kills cannot be held by one
+// workgroup (am_sets.hip hands them over through its retry list).
+//
+// The closed form of am_sets.hip still holds -- a birth (a, b) at position p survives
+// iff no kill with the same kill key (AW: (tok, elem); MV: tok) sits at q > p -- but it
+// is evaluated across many workgroups:
+//   k_big_prep      one thread per big read: its op range, record capacity, chunk count
+//   k_big_offsets   one workgroup: exclusive scans -> chunk / record / hash offsets
+//   k_big_chunk     one workgroup per 1024-op chunk of any big read (flattened, so a hot
+//                   key spreads over the whole GPU): inclusion test + scalar partials
+//                   (global atomics), births/kills in LDS, LOCAL resolution (a birth
+//                   killed later in the same chunk is dead for good), then exports the
+//                   chunk's surviving births and its kills (one per kill key: the
+//                   latest) to global records.  A kill only matters for births at
+//                   earlier positions, so nothing else crosses chunks.
+//   k_big_hash      exported births -> per-read open-addressing hash on the kill key
+//   k_big_kill      each exported kill probes the hash: same key, earlier birth -> dead
+//   k_big_finish    one workgroup per big read: survivors sorted (LDS, or global scratch
+//                   when they do not fit), de-duplicated, CSR + scalar outputs
+// Chunk-local resolution makes the global traffic proportional to what escapes a chunk:
+// for the MV register's override chain that is about one birth per chunk.
+// Bounded counters (keyed sums) use the same chunking: per-chunk LDS slot sums, flushed
+// into per-read global 128-bit slots (64-bit atomics + carry), checked and written by
+// k_big_finish -- a hot key no longer serializes on one workgroup.
+#include "am_block.h"
+
+using namespace amk;
+
+namespace {
+
+constexpr int BLOCK = SBLOCK;
+constexpr int OPL = 4;
+constexpr uint64_t CHUNK = (uint64_t)BLOCK * OPL;
+constexpr uint32_t LB = 1024;   // LDS births per chunk
+constexpr uint32_t LK = 2048;   // LDS kills per chunk
+constexpr uint32_t SCAP = 2048; // survivors sorted in LDS by k_big_finish
+constexpr uint32_t HEMPTY = 0xFFFFFFFFu;
+
+struct BigRead {
+  uint64_t r, off0, off1;
+  uint64_t chunk0;  // first flattened chunk
+  uint64_t rec0;    // first record slot (births and kills each have cap slots)
+  uint64_t cap;     // record capacity (power of two: the global sort pads to it)
+  uint64_t h0;      // first hash slot
+  uint64_t hmask;   // hash slots - 1
+};
+
+struct BigAcc {
+  uint32_t count, flags, pres, nbirth, nkill, pad0;
+  unsigned long long min_excl;
+  unsigned long long mx[AM_MAX_DC];
+};
+
+struct BigSlots {  // bounded counter: ns slots per big read (P: D*D, D: D)
+  uint64_t *lo;
+  int64_t *hi;
+  uint32_t *pres;
+  uint32_t ns;
+};
+
+struct BigRec {
+  uint64_t *ba, *bb;  // births: output pair
+  int32_t *bp;        // birth position (-1 = base snapshot)
+  uint8_t *dead;
+  uint64_t *ka, *kb;  // exported kills: kill key
+  int32_t *kp;
+  uint32_t *H;        // hash slots: birth record index (relative to rec0)
+};
+
+__device__ __forceinline__ uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+__device__ __forceinline__ uint64_t key_hash(uint64_t a, uint64_t b) {
+  uint64_t h = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 32);
+}
+
+// last index i with v[i].field <= x (v sorted ascending, v[0].field == 0)
+template <typename F>
+__device__ __forceinline__ uint32_t find_read(const BigRead *br, uint32_t nbig, uint64_t x, F field) {
+  uint32_t lo = 0, hi = nbig;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (field(br[mid]) <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---- prep: per big read sizes (sz[0..2][b] = chunks, record cap, hash slots) ----
+template <int TYPE>
+__global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, const uint32_t *nbig_p, BigRead *br,
+                           BigAcc *acc, uint64_t *sz, BigSlots SL) {
+  const uint32_t nbig = *nbig_p;
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbig; b += gridDim.x * blockDim.x) {
+    const uint64_t r = list[b];
+    const uint64_t key = B.key[r];
+    const uint64_t off0 = L.key_off[key], off1 = L.key_off[key + 1];
+    const uint64_t W = L.var_off ? L.var_off[off1] - L.var_off[off0] : 0;
+    const uint64_t nbase = B.base.set_off ? B.base.set_len[r] : 0;
+    const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
+    const uint64_t nch = off1 > t0 ? (off1 - t0 + CHUNK - 1) / CHUNK : 1;
+    // births: AW <= add tokens <= W, MV <= ops; kills <= W; + base pairs
+    const uint64_t cap = TYPE == AM_BCOUNTER ? 1 : next_pow2((W > off1 - off0 ? W : off1 - off0) + nbase + 1);
+    if (TYPE == AM_BCOUNTER) {  // slots start from the base snapshot's orddicts
+      const uint32_t nd = L.n_dc, np = nd * nd;
+      for (uint32_t i = 0; i < SL.ns; ++i) {
+        int64_t bv = 0;
+        uint32_t bp = 0;
+        if (i < np) {
+          if (B.base.bc_p) bv = B.base.bc_p[r * np + i];
+          if (B.base.bc_p_pres) bp = B.base.bc_p_pres[r * np + i];
+        } else {
+          if (B.base.bc_d) bv = B.base.bc_d[r * nd + (i - np)];
+          if (B.base.bc_d_pres) bp = B.base.bc_d_pres[r * nd + (i - np)];
+        }
+        const uint64_t q = (uint64_t)b * SL.ns + i;
+        SL.lo[q] = (uint64_t)bv;
+        SL.hi[q] = bv < 0 ? -1 : 0;
+        SL.pres[q] = bp;
+      }
+    }
+    BigRead x;
+    x.r = r, x.off0 = off0, x.off1 = off1, x.chunk0 = 0, x.rec0 = 0, x.cap = cap, x.h0 = 0, x.hmask = 2 * cap - 1;
+    br[b] = x;
+    sz[b] = nch;
+    sz[(uint64_t)nbig + b] = cap;
+    BigAcc a;
+    a.count = a.flags = a.pres = a.nbirth = a.nkill = a.pad0 = 0;
+    a.min_excl = NONE;
+    for (int d = 0; d < AM_MAX_DC; ++d) a.mx[d] = 0;
+    acc[b] = a;
+  }
+}
+
+// one workgroup of 1024: exclusive scans of chunks and caps; totals[0..1]
+__global__ void __launch_bounds__(1024) k_big_offsets(const uint32_t *nbig_p, BigRead *br, const uint64_t *sz,
+                                                      uint64_t *totals) {
+  __shared__ uint64_t part[1024];
+  const uint32_t nbig = *nbig_p, tid = threadIdx.x;
+  const uint32_t per = (nbig + 1023) / 1024;
+  const uint32_t b0 = tid * per < nbig ? tid * per : nbig, b1 = b0 + per < nbig ? b0 + per : nbig;
+  for (int f = 0; f < 2; ++f) {
+    const uint64_t *v = sz + (uint64_t)f * nbig;
+    uint64_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += v[b];
+    part[tid] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+      const uint64_t w = tid >= o ? part[tid - o] : 0;
+      __syncthreads();
+      part[tid] += w;
+      __syncthreads();
+    }
+    uint64_t run = part[tid] - s;
+    for (uint32_t b = b0; b < b1; ++b) {
+      if (f == 0) br[b].chunk0 = run;
+      else br[b].rec0 = run, br[b].h0 = 2 * run;
+      run += v[b];
+    }
+    if (tid == 1023) totals[f] = part[1023];
+    __syncthreads();
+  }
+}
+
+// ---- chunk: inclusion + local resolution + export ----
+struct ChunkSmem {
+  uint64_t lb_a[LB], lb_b[LB];
+  int32_t lb_p[LB];
+  uint64_t lk_a[LK], lk_b[LK];
+  int32_t lk_p[LK];
+  uint32_t ctr[8];  // [0] kills [1] births
+  uint64_t red[4];
+};
+
+struct ChunkSink {
+  ChunkSmem *s;
+  BigRec G;
+  BigAcc *acc;
+  uint64_t rec0;
+  __device__ void gbirth(uint64_t a, uint64_t b, int32_t pos) {
+    const uint64_t i = rec0 + atomicAdd(&acc->nbirth, 1u);
+    G.ba[i] = a, G.bb[i] = b, G.bp[i] = pos;
+  }
+  template <int TYPE>
+  __device__ void gkill(uint64_t tok, uint64_t e, int32_t pos) {
+    const uint64_t i = rec0 + atomicAdd(&acc->nkill, 1u);
+    G.ka[i] = tok, G.kb[i] = TYPE == AM_AWSET ? e : 0ull, G.kp[i] = pos;
+  }
+  __device__ void births(uint64_t e, const uint64_t *tok, uint32_t n, int32_t pos) {
+    for (uint32_t i = 0; i < n; ++i) birth(e, tok[i], pos);
+  }
+  __device__ void birth(uint64_t a, uint64_t b, int32_t pos) {
+    const uint32_t bi = atomicAdd(&s->ctr[1], 1u);
+    if (bi < LB) s->lb_a[bi] = a, s->lb_b[bi] = b, s->lb_p[bi] = pos;
+    else gbirth(a, b, pos);  // LDS full: unresolved, straight to the global records
+  }
+  __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t ki = atomicAdd(&s->ctr[0], 1u);
+      if (ki < LK) s->lk_a[ki] = tok[i], s->lk_b[ki] = e, s->lk_p[ki] = pos;
+      else gkill<AM_AWSET>(tok[i], e, pos);  // e is 0 for MV kills already
+    }
+  }
+};
+
+template <int DMAX, int TYPE>
+__global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
+                                                     const BigRead *br, BigAcc *accs, BigRec G, BigSlots SL,
+                                                     uint64_t n_chunks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  ChunkSmem &s = *(ChunkSmem *)smem_raw;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nbig = uniform_u32(*nbig_p);
+  const uint64_t n = B.n_reads;
+  const uint32_t nd = L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+
+  for (uint64_t x = blockIdx.x; x < n_chunks; x += gridDim.x) {
+    const uint32_t b = find_read(br, nbig, x, [](const BigRead &v) { return v.chunk0; });
+    const BigRead R0 = br[b];
+    const uint64_t r = R0.r;
+    BigAcc *acc = accs + b;
+    const uint64_t t0 = R0.off0 & ~(uint64_t)(OPL - 1);
+    const uint64_t c = x - R0.chunk0;
+    const uint64_t lo = t0 + c * CHUNK, hi = lo + CHUNK < R0.off1 ? lo + CHUNK : R0.off1;
+
+    ReadU<DMAX> u;
+    u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+    const uint64_t rstride = B.per_read_clock ? n : 1, ridx = B.per_read_clock ? r : 0;
+    u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
+    u.base_ignore = !B.base_ignore || B.base_ignore[r];
+    u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+      u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+    }
+    u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+    u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+
+    if (tid < 8) s.ctr[tid] = 0;
+    ChunkSink sink{&s, G, acc, R0.rec0};
+    uint64_t *slo = s.lk_a;  // bounded counter: LDS slot sums of this chunk
+    int64_t *shi = (int64_t *)s.lk_b;
+    uint32_t *spres = (uint32_t *)s.lk_p;
+    if (TYPE == AM_BCOUNTER)
+      for (uint32_t i = tid; i < SL.ns; i += BLOCK) slo[i] = 0, shi[i] = 0, spres[i] = 0;
+    __syncthreads();
+    if (TYPE != AM_BCOUNTER && c == 0 && B.base.set_off) {  // base snapshot pairs: births at -1 (no later kill in
+      const uint64_t bo = B.base.set_off[r];  // this chunk can be ruled out, so global)
+      const uint32_t bl = B.base.set_len[r];
+      for (uint32_t i = tid; i < bl; i += BLOCK) sink.gbirth(B.base.set_a[bo + i], B.base.set_b[bo + i], -1);
+    }
+
+    Acc<DMAX> a;
+    a.reset();
+    const uint64_t g = lo + (uint64_t)tid * OPL;
+    if (g < hi) {
+      const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
+      const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
+      const uint64_t ct[OPL] = {c01.x, c01.y, c23.x, c23.y};
+      uint64_t sv[OPL][DMAX];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d < (int)nd) {
+          const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
+          const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
+          sv[0][d] = s01.x, sv[1][d] = s01.y, sv[2][d] = s23.x, sv[3][d] = s23.y;
+        } else {
+          sv[0][d] = sv[1][d] = sv[2][d] = sv[3][d] = 0;
+        }
+      }
+      uint32_t sp[OPL] = {u.allmask, u.allmask, u.allmask, u.allmask};
+      if (L.snap_pres) {
+        const u32x4 q = *(const u32x4 *)(L.snap_pres + g);
+        sp[0] = q.x, sp[1] = q.y, sp[2] = q.z, sp[3] = q.w;
+      }
+#pragma unroll
+      for (int k = 0; k < OPL; ++k) {
+        const uint64_t p = g + k;
+        if (p < R0.off0 || p >= hi) continue;
+        const bool txm = u.has_txid && L.op_txid[p] == u.txid;
+        const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
+        if (!eval_op<DMAX, true>(u, meta, ct[k], sv[k], sp[k], txm, p, a)) continue;
+        if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
+        if (TYPE == AM_BCOUNTER) {
+          uint32_t slot;
+          int64_t v;
+          if (!bc_slot(L, p, meta, nd, slot, v)) {
+            a.flags |= FLAG_BAD;
+            continue;
+          }
+          acc128_atomic(&slo[slot], &shi[slot], v < 0 ? -1 : 0, (uint64_t)v);
+          atomicOr(&spres[slot], 1u);
+        } else if (!set_effects<TYPE>(L, p, meta, (int32_t)(p - R0.off0), sink)) {
+          a.flags |= FLAG_BAD;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- scalar partials -> the read's accumulators ----
+    const uint32_t count = (uint32_t)block_red_u64(s.red, wave_sum_u32(a.count), 0);
+    const uint32_t flags = (uint32_t)block_red_u64(s.red, wave_or_u32(a.flags), 1);
+    const uint32_t pres = (uint32_t)block_red_u64(s.red, wave_or_u32(a.pres), 1);
+    const uint64_t min_excl = block_red_u64(s.red, wave_min_u64(a.min_excl), 3);
+    uint64_t mx[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? block_red_u64(s.red, wave_max_u64(a.mx[d]), 2) : 0;
+    if (tid == 0) {
+      if (count) atomicAdd(&acc->count, count);
+      if (flags) atomicOr(&acc->flags, flags);
+      if (pres) atomicOr(&acc->pres, pres);
+      if (min_excl != NONE) atomicMin(&acc->min_excl, (unsigned long long)min_excl);
+      for (int d = 0; d < DMAX; ++d)
+        if (d < (int)nd && mx[d]) atomicMax(&acc->mx[d], (unsigned long long)mx[d]);
+    }
+
+    if (TYPE == AM_BCOUNTER) {  // flush the chunk's slot sums into the read's global slots
+      for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
+        const uint64_t q = (uint64_t)b * SL.ns + i;
+        if (slo[i] || shi[i]) acc128_atomic(&SL.lo[q], &SL.hi[q], shi[i], slo[i]);
+        if (spres[i]) atomicOr(&SL.pres[q], 1u);
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- local resolution, then export ----
+    const uint32_t nk = s.ctr[0] < LK ? s.ctr[0] : LK;
+    const uint32_t nb = s.ctr[1] < LB ? s.ctr[1] : LB;
+    block_sort(s.lk_a, s.lk_b, s.lk_p, nk, LK);  // by (kill key, pos)
+    for (uint32_t i = tid; i < nb; i += BLOCK) {
+      uint64_t qa, qb;
+      birth_kill_key<TYPE>(s.lb_a[i], s.lb_b[i], qa, qb);
+      uint32_t l = 0, h = nk;  // upper bound of (qa, qb, +inf)
+      while (l < h) {
+        const uint32_t mid = (l + h) >> 1;
+        const bool le = s.lk_a[mid] < qa || (s.lk_a[mid] == qa && s.lk_b[mid] <= qb);
+        if (le) l = mid + 1;
+        else h = mid;
+      }
+      const bool dead = l > 0 && s.lk_a[l - 1] == qa && s.lk_b[l - 1] == qb && s.lk_p[l - 1] > s.lb_p[i];
+      if (!dead) sink.gbirth(s.lb_a[i], s.lb_b[i], s.lb_p[i]);
+    }
+    for (uint32_t i = tid; i < nk; i += BLOCK) {  // the latest kill of each key
+      if (i + 1 == nk || s.lk_a[i + 1] != s.lk_a[i] || s.lk_b[i + 1] != s.lk_b[i])
+        sink.gkill<AM_AWSET>(s.lk_a[i], s.lk_b[i], s.lk_p[i]);
+    }
+    __syncthreads();
+  }
+}
+
+// ---- births -> hash on the kill key ----
+template <int TYPE>
+__global__ void k_big_hash(const uint32_t *nbig_p, const BigRead *br, const BigAcc *accs, BigRec G, uint64_t total) {
+  const uint32_t nbig = *nbig_p;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = find_read(br, nbig, x, [](const BigRead &v) { return v.rec0; });
+    const BigRead R0 = br[b];
+    const uint64_t i = x - R0.rec0;
+    if (i >= accs[b].nbirth) continue;
+    uint64_t qa, qb;
+    birth_kill_key<TYPE>(G.ba[x], G.bb[x], qa, qb);
+    uint64_t h = key_hash(qa, qb) & R0.hmask;
+    while (atomicCAS(&G.H[R0.h0 + h], HEMPTY, (uint32_t)i) != HEMPTY) h = (h + 1) & R0.hmask;
+  }
+}
+
+// ---- kills probe the hash: same key and an earlier birth -> dead ----
+template <int TYPE>
+__global__ void k_big_kill(const uint32_t *nbig_p, const BigRead *br, const BigAcc *accs, BigRec G, uint64_t total) {
+  const uint32_t nbig = *nbig_p;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = find_read(br, nbig, x, [](const BigRead &v) { return v.rec0; });
+    const BigRead R0 = br[b];
+    if (x - R0.rec0 >= accs[b].nkill) continue;
+    const uint64_t qa = G.ka[x], qb = G.kb[x];
+    const int32_t kp = G.kp[x];
+    uint64_t h = key_hash(qa, qb) & R0.hmask;
+    while (true) {
+      const uint32_t i = G.H[R0.h0 + h];
+      if (i == HEMPTY) break;
+      const uint64_t y = R0.rec0 + i;
+      uint64_t ba, bb;
+      birth_kill_key<TYPE>(G.ba[y], G.bb[y], ba, bb);
+      if (ba == qa && bb == qb && G.bp[y] < kp) G.dead[y] = 1;
+      h = (h + 1) & R0.hmask;
+    }
+  }
+}
+
+// ---- finish: survivors sorted + CSR, scalar outputs ----
+struct FinSmem {
+  uint64_t oa[SCAP], ob[SCAP];
+  uint32_t ctr[8];
+  uint64_t red[4];
+};
+
+template <int DMAX, int TYPE>
+__global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch B, am_read_result R,
+                                                      const uint32_t *nbig_p, const BigRead *br, const BigAcc *accs,
+                                                      BigRec G, BigSlots SL) {
+  __shared__ FinSmem s;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nbig = uniform_u32(*nbig_p);
+  const uint64_t n = B.n_reads;
+  const uint32_t nd = L.n_dc;
+  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    const BigRead R0 = br[b];
+    const BigAcc A = accs[b];
+    const uint64_t r = R0.r;
+    int32_t status = (A.flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+    if (TYPE == AM_BCOUNTER && status == AM_OK) {
+      const uint32_t np = nd * nd;
+      uint32_t ovf = 0;
+      for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
+        const uint64_t q = (uint64_t)b * SL.ns + i;
+        if (SL.hi[q] != ((int64_t)SL.lo[q] < 0 ? -1 : 0)) ovf = 1;
+      }
+      ovf = (uint32_t)block_red_u64(s.red, wave_or_u32(ovf), 1);
+      if (ovf) status = AM_ERR_OVERFLOW;  // Erlang: a bignum
+      else
+        for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
+          const uint64_t q = (uint64_t)b * SL.ns + i;
+          if (i < np) {
+            R.value.bc_p[r * np + i] = (int64_t)SL.lo[q];
+            R.value.bc_p_pres[r * np + i] = SL.pres[q] ? 1 : 0;
+          } else {
+            R.value.bc_d[r * nd + (i - np)] = (int64_t)SL.lo[q];
+            R.value.bc_d_pres[r * nd + (i - np)] = SL.pres[q] ? 1 : 0;
+          }
+        }
+    } else if (status == AM_OK) {
+      // count survivors, then gather them (LDS, or the read's kill records as scratch)
+      uint32_t alive = 0;
+      for (uint32_t i = tid; i < A.nbirth; i += BLOCK) alive += G.dead[R0.rec0 + i] ? 0u : 1u;
+      alive = (uint32_t)block_red_u64(s.red, wave_sum_u32(alive), 0);
+      const bool in_lds = alive <= SCAP;
+      uint64_t *oa = in_lds ? s.oa : G.ka + R0.rec0;
+      uint64_t *ob = in_lds ? s.ob : G.kb + R0.rec0;
+      if (tid == 0) s.ctr[0] = 0;
+      __syncthreads();
+      for (uint32_t i0 = 0; i0 < A.nbirth; i0 += BLOCK) {  // stable-order compaction is not
+        const uint32_t i = i0 + tid;                         // needed: the sort follows
+        if (i < A.nbirth && !G.dead[R0.rec0 + i]) {
+          const uint32_t o = atomicAdd(&s.ctr[0], 1u);
+          oa[o] = G.ba[R0.rec0 + i];
+          ob[o] = G.bb[R0.rec0 + i];
+        }
+      }
+      __syncthreads();
+      block_sort(oa, ob, nullptr, alive, in_lds ? SCAP : (uint32_t)R0.cap);
+      const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
+      const uint32_t distinct =
+          block_write_unique(oa, ob, alive, R.value.set_a + ooff, R.value.set_b + ooff, ocap, &s.ctr[4]);
+      if (distinct > ocap) status = AM_ERR_CAPACITY;
+      else if (tid == 0) R.value.set_len[r] = distinct;
+    }
+    if (tid == 0) {
+      R.status[r] = status;
+      R.flags[r] = (uint8_t)(A.flags & 0xFFu);
+      if (status == AM_OK) {
+        const uint64_t key = B.key[r];
+        const uint64_t idb = L.key_id_base ? L.key_id_base[key] : 1;
+        const uint64_t nops = R0.off1 - R0.off0;
+        int64_t nlo;
+        if (A.min_excl != NONE)
+          nlo = (L.op_id ? (int64_t)L.op_id[A.min_excl] : (int64_t)(idb + (A.min_excl - R0.off0))) - 1;
+        else
+          nlo = nops == 0 ? 0 : (L.op_id ? (int64_t)L.op_id[R0.off1 - 1] : (int64_t)(idb + nops - 1));
+        R.new_last_op[r] = nlo;
+        const uint32_t allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+        const bool base_ignore = !B.base_ignore || B.base_ignore[r];
+        const uint32_t cpres = base_ignore ? 0u : (B.base_pres[r] & allmask);
+        const bool ign = base_ignore && A.count == 0;
+        const uint32_t opres = ign ? 0u : (A.pres | cpres);
+        R.last_ct_ignore[r] = ign ? 1 : 0;
+        R.last_ct_pres[r] = opres;
+        for (uint32_t d = 0; d < nd; ++d) {
+          const uint64_t c0 = ((cpres >> d) & 1u) ? B.base_vc[(uint64_t)d * n + r] : 0;
+          const uint64_t m = A.mx[d] > c0 ? A.mx[d] : c0;
+          R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? m : 0;
+        }
+        R.is_new_ss[r] = A.count > 0;
+        R.count[r] = A.count;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int DMAX, int TYPE>
+int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, const uint32_t *list,
+            const uint32_t *nbig_d, uint32_t nbig, BigRead *br, BigAcc *acc, BigRec G, BigSlots SL,
+            uint64_t n_chunks, uint64_t n_rec) {
+  const uint32_t cap = (uint32_t)ctx->n_cu * 2;
+  static bool attr = false;
+  if (!attr) {
+    AM_HIP(hipFuncSetAttribute((const void *)k_big_chunk<DMAX, TYPE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(ChunkSmem)));
+    attr = true;
+  }
+  const unsigned g1 = (unsigned)(n_chunks < cap ? n_chunks : cap);
+  hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L, *B, nbig_d,
+                     br, acc, G, SL, n_chunks);
+  AM_HIP(hipGetLastError());
+  if (TYPE != AM_BCOUNTER) {
+    const uint64_t eg = (n_rec + 255) / 256;
+    const unsigned g2 = (unsigned)(eg < (uint64_t)ctx->n_cu * 16 ? eg : (uint64_t)ctx->n_cu * 16);
+    hipLaunchKernelGGL((k_big_hash<TYPE>), dim3(g2), dim3(256), 0, ctx->stream, nbig_d, br, acc, G, n_rec);
+    AM_HIP(hipGetLastError());
+    hipLaunchKernelGGL((k_big_kill<TYPE>), dim3(g2), dim3(256), 0, ctx->stream, nbig_d, br, acc, G, n_rec);
+    AM_HIP(hipGetLastError());
+  }
+  const unsigned g3 = (unsigned)(nbig < cap ? nbig : cap);
+  hipLaunchKernelGGL((k_big_finish<DMAX, TYPE>), dim3(g3), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, nbig_d, br, acc,
+                     G, SL);
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
+template <int TYPE>
+int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_retry retry) {
+  uint64_t h[2];
+  int rc = am_ctx_fetch(ctx, retry.count, 1, h);  // one synchronization: the tier is data-dependent
+  if (rc) return rc;
+  const uint32_t nbig = (uint32_t)(h[0] & 0xFFFFFFFFu);
+  if (nbig == 0) return AM_OK;
+  // metadata: BigRead[nbig], BigAcc[nbig], sizes[2][nbig], totals[2], bcounter slots
+  BigSlots SL;
+  SL.ns = TYPE == AM_BCOUNTER ? L->n_dc * L->n_dc + L->n_dc : 0;
+  const size_t o_acc = am_round_up((size_t)nbig * sizeof(BigRead), 256);
+  const size_t o_sz = o_acc + am_round_up((size_t)nbig * sizeof(BigAcc), 256);
+  const size_t o_tot = o_sz + am_round_up((size_t)nbig * 16, 256);
+  const size_t o_slo = o_tot + 256, nsl = (size_t)nbig * SL.ns;
+  const size_t o_shi = o_slo + am_round_up(nsl * 8, 256), o_spr = o_shi + am_round_up(nsl * 8, 256);
+  void *meta = nullptr;
+  rc = am_ctx_scratch(ctx, AM_SCR_BIGMETA, o_spr + am_round_up(nsl * 4, 256) + 256, &meta);
+  if (rc) return rc;
+  BigRead *br = (BigRead *)meta;
+  BigAcc *acc = (BigAcc *)((char *)meta + o_acc);
+  uint64_t *sz = (uint64_t *)((char *)meta + o_sz);
+  uint64_t *tot = (uint64_t *)((char *)meta + o_tot);
+  SL.lo = (uint64_t *)((char *)meta + o_slo);
+  SL.hi = (int64_t *)((char *)meta + o_shi);
+  SL.pres = (uint32_t *)((char *)meta + o_spr);
+  const unsigned gp = (nbig + 255) / 256;
+  hipLaunchKernelGGL(k_big_prep<TYPE>, dim3(gp), dim3(256), 0, ctx->stream, *L, *B, retry.list, retry.count, br, acc,
+                     sz, SL);
+  AM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_big_offsets, dim3(1), dim3(1024), 0, ctx->stream, retry.count, br, sz, tot);
+  AM_HIP(hipGetLastError());
+  rc = am_ctx_fetch(ctx, tot, 2, h);
+  if (rc) return rc;
+  const uint64_t n_chunks = h[0], n_rec = h[1];
+  // records: births (a, b, p, dead), kills (a, b, p) -- n_rec each; hash 2*n_rec slots
+  const size_t rb = am_round_up(n_rec * 8, 256), r4 = am_round_up(n_rec * 4, 256), r1 = am_round_up(n_rec, 256);
+  const size_t hb = am_round_up(2 * n_rec * 4, 256);
+  void *recs = nullptr;
+  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 4 * rb + 2 * r4 + r1 + hb, &recs);
+  if (rc) return rc;
+  char *q = (char *)recs;
+  BigRec G;
+  G.ba = (uint64_t *)q, q += rb;
+  G.bb = (uint64_t *)q, q += rb;
+  G.ka = (uint64_t *)q, q += rb;
+  G.kb = (uint64_t *)q, q += rb;
+  G.bp = (int32_t *)q, q += r4;
+  G.kp = (int32_t *)q, q += r4;
+  G.dead = (uint8_t *)q, q += r1;
+  G.H = (uint32_t *)q;
+  AM_HIP(hipMemsetAsync(G.dead, 0, n_rec, ctx->stream));
+  AM_HIP(hipMemsetAsync(G.H, 0xFF, 2 * n_rec * 4, ctx->stream));
+  const uint32_t nd = L->n_dc;
+#define AM_B(D) return run_big<D, TYPE>(ctx, L, B, R, retry.list, retry.count, nbig, br, acc, G, SL, n_chunks, n_rec);
+  if (nd <= 1) AM_B(1)
+  if (nd <= 2) AM_B(2)
+  if (nd <= 3) AM_B(3)
+  if (nd <= 4) AM_B(4)
+  if (nd <= 8) AM_B(8)
+  if (nd <= 16) AM_B(16)
+  AM_B(32)
+#undef AM_B
+}
+
+}  // namespace
+
+int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, uint32_t type,
+                  am_retry retry) {
+  if (!retry.count) return AM_OK;
+  switch (type) {
+    case AM_AWSET: return launch_big<AM_AWSET>(ctx, L, B, R, retry);
+    case AM_MVREG: return launch_big<AM_MVREG>(ctx, L, B, R, retry);
+    case AM_BCOUNTER: return launch_big<AM_BCOUNTER>(ctx, L, B, R, retry);
+    default: return AM_OK;
+  }
+}

@@ -15,7 +15,32 @@ struct am_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int n_cu = 256;
+  void *scratch[4] = {};         // grow-only device scratch slots (planner, big-read path)
+  size_t scratch_bytes[4] = {};
+  uint64_t *pinned = nullptr;    // small pinned host buffer for device -> host counters
 };
+
+// A selection of a batch's reads: the planner's per-kernel sub-batches.  idx == nullptr
+// means the identity over [0, n_reads); otherwise the reads idx[range[0] .. range[1])
+// (range lives in device memory, so sub-batch sizes never round-trip to the host).
+struct am_sel {
+  const uint32_t *idx = nullptr;
+  const uint32_t *range = nullptr;
+};
+// Reads a set kernel could not finish in LDS (appended by the kernel; count on device).
+struct am_retry {
+  uint32_t *list = nullptr;
+  uint32_t *count = nullptr;
+};
+
+// scratch slot `slot` (0 planner, 1 big-read metadata, 2 big-read records): at least
+// `bytes` of device memory, valid until the next call for the same slot (stream-ordered
+// reuse; growing synchronizes the stream before freeing the old block)
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2 };
+int am_ctx_scratch(am_ctx *ctx, int slot, size_t bytes, void **out);
+// copy `n` u64 counters device -> host through the pinned buffer (synchronizes the stream)
+int am_ctx_fetch(am_ctx *ctx, const void *dev, uint32_t n_u64, uint64_t *host);
+int am_launch_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
 
 struct am_store {
   am_ctx *ctx = nullptr;
@@ -46,6 +71,10 @@ int am_launch_gst_finalize(am_ctx *ctx, uint32_t n_dc, const uint64_t *lanes, ui
                            uint32_t *last_pres, int gr, uint64_t *out_vc, uint32_t *out_pres,
                            uint8_t *changed);
 int am_launch_synth(am_ctx *ctx, const am_synth_params *p, am_op_log *L /* device arrays allocated */);
-int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
-int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
+int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                     uint32_t type);
+int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                   uint32_t type, am_retry retry);
+int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, uint32_t type,
+                  am_retry retry);  // am_big.hip: reads beyond the LDS tier
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)

@@ -400,31 +400,14 @@ int launch_hint(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read
 
 }  // namespace
 
-int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
-  if (!ctx || !L || !B || !R) return AM_ERR_INVALID;
-  if (L->n_dc == 0 || L->n_dc > AM_MAX_DC) {
-    am_set_error("n_dc=%u out of range", L->n_dc);
-    return AM_ERR_INVALID;
-  }
-  const uint64_t stride = L->snap_stride ? L->snap_stride : L->n_ops;
-  if ((stride & 3) || (reinterpret_cast<uintptr_t>(L->commit_time) & 15) ||
-      (reinterpret_cast<uintptr_t>(L->snap_vc) & 15) || (reinterpret_cast<uintptr_t>(L->p0) & 15) ||
-      (reinterpret_cast<uintptr_t>(L->op_meta) & 3)) {
-    am_set_error("device log must be 16-byte aligned with snap_stride %% 4 == 0 (use am_store_create)");
-    return AM_ERR_INVALID;
-  }
-  if (B->n_reads == 0) return AM_OK;
-  const char *variant = getenv("AM_KERNEL");  // "scalar" = the one-read-per-wave kernel (A/B only)
-  if (!(variant && strcmp(variant, "scalar") == 0) && (B->type_hint == AM_PN || B->type_hint == AM_LWW))
-    return am_launch_stream(ctx, L, B, R);
-  if (B->type_hint == AM_AWSET || B->type_hint == AM_MVREG || B->type_hint == AM_BCOUNTER)
-    return am_launch_sets(ctx, L, B, R);
+// The one-read-per-wave kernel (PN, LWW): kept for A/B comparisons (AM_KERNEL=scalar).
+int am_launch_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
   switch (B->type_hint) {
     case AM_PN: return launch_hint<AM_PN>(ctx, L, B, R);
     case AM_LWW: return launch_hint<AM_LWW>(ctx, L, B, R);
     case 0: return launch_hint<0>(ctx, L, B, R);
     default:
-      am_set_error("type_hint %u not supported by this build", B->type_hint);
+      am_set_error("the scalar kernel handles PN and LWW only");
       return AM_ERR_UNSUPPORTED;
   }
 }

@@ -1,0 +1,201 @@
+// am_plan.hip -- the batch planner behind am_materialize.
+//
+// A read batch from a partition's read servers mixes CRDT types (each
+// materializer_vnode:read/6 call names its Type, src/materializer_vnode.erl:97-102).
+// Every type has its own kernel (k_stream: PN counter, LWW register; k_sets: add-wins
+// set, MV register, bounded counter; am_big.hip: set reads beyond the LDS tier), so a
+// mixed batch is split on the device, never on the host:
+//   k_plan_count    per 1024-read block: class histogram (class = kernel the read needs;
+//                   reads with an unknown type or key get their status here)
+//   k_plan_scan     one workgroup: per-class block offsets and the [begin, end) range of
+//                   every class in the index array
+//   k_plan_scatter  stable partition of the read indices by class (wave ballots)
+// and each type kernel then runs over its class range (am_sel).  The ranges stay in
+// device memory: kernels are launched with a resident-capacity grid and read their
+// count at start, so the planner adds no host round trip.
+//
+// Single-type batches (type_hint != 0) skip the planner.  Set types may need the
+// big-read path, which sizes its scratch on the host (one synchronization).
+#include "am_wave.h"
+
+using namespace amk;
+
+namespace {
+
+constexpr int PB = 256;              // planner block
+constexpr int PER = 4;               // reads per thread
+constexpr uint32_t PCHUNK = PB * PER;
+constexpr int NCLS = 8;              // classes: 0..4 = type-1, 5 = done (status written)
+constexpr uint32_t CLS_DONE = 5;
+
+__device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read_batch &B, am_read_result &R,
+                                               uint64_t r, bool write_status) {
+  const uint32_t t = B.type[r];
+  const uint64_t key = B.key[r];
+  if (t < AM_PN || t > AM_BCOUNTER || key >= L.n_keys) {
+    if (write_status) R.status[r] = AM_ERR_INVALID;
+    return CLS_DONE;
+  }
+  return t - 1;
+}
+
+__global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, uint32_t *cnt) {
+  __shared__ uint32_t c[NCLS];
+  if (threadIdx.x < NCLS) c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t r = base + (uint64_t)j * PB + threadIdx.x;
+    if (r < B.n_reads) atomicAdd(&c[read_class(L, B, R, r, true)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = c[threadIdx.x];
+}
+
+// one workgroup of 1024: cnt[blk][cls] -> exclusive offsets (class-major), range[2*cls]
+__global__ void __launch_bounds__(1024) k_plan_scan(uint32_t *cnt, uint32_t n_blk, uint32_t *range) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t total[NCLS];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (n_blk + 1023) / 1024;
+  const uint32_t b0 = tid * per, b1 = b0 + per < n_blk ? b0 + per : n_blk;
+  uint32_t start = 0;
+  for (int c = 0; c < NCLS; ++c) {
+    uint32_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += cnt[(uint64_t)b * NCLS + c];
+    part[tid] = s;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 partials
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+      const uint32_t v = tid >= o ? part[tid - o] : 0u;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    uint32_t run = start + part[tid] - s;  // exclusive prefix of this thread's segment
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t x = cnt[(uint64_t)b * NCLS + c];
+      cnt[(uint64_t)b * NCLS + c] = run;
+      run += x;
+    }
+    if (tid == 1023) total[c] = part[1023];
+    __syncthreads();
+    if (tid == 0) {
+      range[2 * c] = start;
+      range[2 * c + 1] = start + total[c];
+    }
+    start += total[c];
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch B, am_read_result R,
+                                                     const uint32_t *off, uint32_t *idx) {
+  __shared__ uint32_t run[NCLS];
+  __shared__ uint32_t wcnt[PB / WAVE][NCLS];
+  const uint32_t tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
+  if (tid < NCLS) run[tid] = off[(uint64_t)blockIdx.x * NCLS + tid];
+  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
+  for (int j = 0; j < PER; ++j) {
+    const uint64_t r = base + (uint64_t)j * PB + tid;
+    const uint32_t c = r < B.n_reads ? read_class(L, B, R, r, false) : NCLS;
+    uint32_t rank = 0;
+    for (uint32_t k = 0; k < NCLS; ++k) {
+      const uint64_t m = __ballot(c == k);
+      if (c == k) rank = __popcll(m & ((1ull << lane) - 1));
+      if (lane == 0) wcnt[w][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (c < NCLS) {
+      uint32_t before = run[c];
+      for (uint32_t v = 0; v < w; ++v) before += wcnt[v][c];
+      idx[before + rank] = (uint32_t)r;
+    }
+    __syncthreads();
+    if (tid < NCLS) {
+      uint32_t t = 0;
+      for (int v = 0; v < PB / WAVE; ++v) t += wcnt[v][tid];
+      run[tid] += t;
+    }
+    __syncthreads();
+  }
+}
+
+// Set kernels + the big-read tier for one type over selection S.
+int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
+             uint32_t *retry_buf) {
+  am_retry retry;
+  retry.count = retry_buf;
+  retry.list = retry_buf + 1;
+  AM_HIP(hipMemsetAsync(retry.count, 0, sizeof(uint32_t), ctx->stream));
+  int rc = am_launch_sets(ctx, L, B, R, S, type, retry);
+  if (rc) return rc;
+  return am_launch_big(ctx, L, B, R, type, retry);
+}
+
+}  // namespace
+
+int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+  if (!ctx || !L || !B || !R) return AM_ERR_INVALID;
+  if (L->n_dc == 0 || L->n_dc > AM_MAX_DC) {
+    am_set_error("n_dc=%u out of range", L->n_dc);
+    return AM_ERR_INVALID;
+  }
+  const uint64_t stride = L->snap_stride ? L->snap_stride : L->n_ops;
+  if ((stride & 3) || (reinterpret_cast<uintptr_t>(L->commit_time) & 15) ||
+      (reinterpret_cast<uintptr_t>(L->snap_vc) & 15) || (reinterpret_cast<uintptr_t>(L->p0) & 15) ||
+      (reinterpret_cast<uintptr_t>(L->op_meta) & 3)) {
+    am_set_error("device log must be 16-byte aligned with snap_stride %% 4 == 0 (use am_store_create)");
+    return AM_ERR_INVALID;
+  }
+  const uint64_t n = B->n_reads;
+  if (n == 0) return AM_OK;
+  if (n > 0xFFFFFFF0ull) {
+    am_set_error("n_reads %llu exceeds the 32-bit read index of one batch", (unsigned long long)n);
+    return AM_ERR_INVALID;
+  }
+  const char *variant = getenv("AM_KERNEL");  // "scalar" = the one-read-per-wave kernel (A/B only)
+  if (variant && strcmp(variant, "scalar") == 0 && B->type_hint <= AM_LWW) return am_launch_scalar(ctx, L, B, R);
+
+  const am_sel all{};
+  if (B->type_hint == AM_PN || B->type_hint == AM_LWW) return am_launch_stream(ctx, L, B, R, all, B->type_hint);
+  if (B->type_hint == AM_AWSET || B->type_hint == AM_MVREG || B->type_hint == AM_BCOUNTER) {
+    void *scr = nullptr;
+    int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &scr);
+    if (rc) return rc;
+    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr);
+  }
+  if (B->type_hint != 0) {
+    am_set_error("type_hint %u not supported", B->type_hint);
+    return AM_ERR_UNSUPPORTED;
+  }
+
+  // ---- mixed batch: partition by class on the device ----
+  const uint64_t n_blk = (n + PCHUNK - 1) / PCHUNK;
+  // scratch: [retry count + list: n+1][range: 2*NCLS][cnt: n_blk*NCLS][idx: n]
+  const size_t words = (n + 64) + 2 * NCLS + n_blk * NCLS + n + 64;
+  void *scr = nullptr;
+  int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, words * sizeof(uint32_t), &scr);
+  if (rc) return rc;
+  uint32_t *retry_buf = (uint32_t *)scr;
+  uint32_t *range = retry_buf + n + 64;
+  uint32_t *cnt = range + 2 * NCLS;
+  uint32_t *idx = cnt + n_blk * NCLS;
+  hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, cnt);
+  AM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, (uint32_t)n_blk, range);
+  AM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, cnt, idx);
+  AM_HIP(hipGetLastError());
+  for (uint32_t t = AM_PN; t <= AM_BCOUNTER; ++t) {
+    am_sel S;
+    S.idx = idx;
+    S.range = range + 2 * (t - 1);
+    if (t == AM_PN || t == AM_LWW)
+      rc = am_launch_stream(ctx, L, B, R, S, t);
+    else
+      rc = run_sets(ctx, L, B, R, S, t, retry_buf);
+    if (rc) return rc;
+  }
+  return AM_OK;
+}

@@ -45,6 +45,9 @@ int am_ctx_close(am_ctx *c) {
   if (!c) return AM_OK;
   AM_HIP(hipSetDevice(c->device));
   AM_HIP(hipStreamSynchronize(c->stream));
+  for (void *&p : c->scratch)
+    if (p) (void)hipFree(p), p = nullptr;
+  if (c->pinned) (void)hipHostFree(c->pinned), c->pinned = nullptr;
   (void)hipEventDestroy(c->ev0);
   (void)hipEventDestroy(c->ev1);
   (void)hipStreamDestroy(c->stream);
@@ -74,6 +77,42 @@ int am_timer_stop(am_ctx *c, float *ms) {
   return AM_OK;
 }
 
+}  // extern "C"
+
+int am_ctx_scratch(am_ctx *c, int slot, size_t bytes, void **out) {
+  if (!c || slot < 0 || slot >= 4 || !out) return AM_ERR_INVALID;
+  if (bytes == 0) bytes = 256;
+  if (c->scratch_bytes[slot] < bytes) {
+    if (c->scratch[slot]) {
+      AM_HIP(hipStreamSynchronize(c->stream));
+      AM_HIP(hipFree(c->scratch[slot]));
+      c->scratch[slot] = nullptr;
+      c->scratch_bytes[slot] = 0;
+    }
+    const size_t want = bytes + bytes / 4;  // headroom against regrowth
+    void *p = nullptr;
+    const hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      am_set_error("scratch hipMalloc(%zu): %s", want, hipGetErrorString(e));
+      return AM_ERR_NOMEM;
+    }
+    c->scratch[slot] = p;
+    c->scratch_bytes[slot] = want;
+  }
+  *out = c->scratch[slot];
+  return AM_OK;
+}
+
+int am_ctx_fetch(am_ctx *c, const void *dev, uint32_t n, uint64_t *host) {
+  if (n > 64) return AM_ERR_INVALID;
+  if (!c->pinned) AM_HIP(hipHostMalloc((void **)&c->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault));
+  AM_HIP(hipMemcpyAsync(c->pinned, dev, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  AM_HIP(hipStreamSynchronize(c->stream));
+  memcpy(host, c->pinned, n * sizeof(uint64_t));
+  return AM_OK;
+}
+
+extern "C" {
 int am_dev_alloc(am_ctx *c, size_t bytes, void **out) {
   if (!c || !out) return AM_ERR_INVALID;
   AM_HIP(hipSetDevice(c->device));

@@ -22,7 +22,7 @@
 // keyed sum: exact 128-bit LDS accumulators (64-bit atomics + carry).
 // Capacity: KCAP kills / BCAP births per read live in LDS (78 KB per group);
 // a read that exceeds them returns AM_ERR_CAPACITY (global-scratch path: next).
-#include "am_wave.h"
+#include "am_block.h"
 
 using namespace amk;
 
@@ -34,7 +34,7 @@ constexpr int OPL = 4;
 constexpr uint64_t TILE = (uint64_t)BLOCK * OPL;
 constexpr uint32_t KCAP = 2048;
 constexpr uint32_t BCAP = 1024;
-constexpr int32_t POS_MAX = 0x7FFFFFFF;
+constexpr uint64_t BIG_OPS = 4 * TILE;  // logs longer than this skip the LDS tier
 
 struct Smem {
   uint64_t *ka, *kb;  // kills: token, elem (MV: 0)
@@ -48,6 +48,35 @@ struct Smem {
   uint64_t *slo;
   int64_t *shi;
   uint32_t *spres;
+};
+
+// births / kills appended to the LDS lists; overflow sets ctr[3] (-> big-read tier)
+struct LdsSink {
+  Smem *s;
+  __device__ void births(uint64_t e, const uint64_t *tok, uint32_t n, int32_t pos) {
+    const uint32_t bi = atomicAdd(&s->ctr[1], n);
+    if (bi + n > BCAP) {
+      s->ctr[3] = 1;
+      return;
+    }
+    for (uint32_t i = 0; i < n; ++i) s->ba[bi + i] = e, s->bb[bi + i] = tok[i], s->bp[bi + i] = pos;
+  }
+  __device__ void birth(uint64_t a, uint64_t b, int32_t pos) {
+    const uint32_t bi = atomicAdd(&s->ctr[1], 1u);
+    if (bi >= BCAP) {
+      s->ctr[3] = 1;
+      return;
+    }
+    s->ba[bi] = a, s->bb[bi] = b, s->bp[bi] = pos;
+  }
+  __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
+    const uint32_t ki = atomicAdd(&s->ctr[0], n);
+    if (ki + n > KCAP) {
+      s->ctr[3] = 1;
+      return;
+    }
+    for (uint32_t i = 0; i < n; ++i) s->ka[ki + i] = tok[i], s->kb[ki + i] = e, s->kp[ki + i] = pos;
+  }
 };
 
 __device__ Smem carve(unsigned char *p) {
@@ -69,57 +98,9 @@ __device__ Smem carve(unsigned char *p) {
 }
 constexpr size_t SMEM_BYTES = (size_t)KCAP * 20 + (size_t)BCAP * 20 + (size_t)BCAP * 16 + 16 * 4 + NW * 8 * 8;
 
-__device__ __forceinline__ bool less3(uint64_t a0, uint64_t b0, int32_t p0, uint64_t a1, uint64_t b1, int32_t p1) {
-  return a0 != a1 ? a0 < a1 : (b0 != b1 ? b0 < b1 : p0 < p1);
-}
-
-// block bitonic sort of (a, b, p) in LDS, n <= cap (power-of-two padded with +inf)
-__device__ void block_sort(uint64_t *a, uint64_t *b, int32_t *p, uint32_t n, uint32_t cap) {
-  uint32_t N = 1;
-  while (N < n) N <<= 1;
-  if (N > cap) N = cap;
-  for (uint32_t i = n + threadIdx.x; i < N; i += BLOCK) {
-    a[i] = ~0ull;
-    b[i] = ~0ull;
-    if (p) p[i] = POS_MAX;
-  }
-  __syncthreads();
-  for (uint32_t k = 2; k <= N; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < N; i += BLOCK) {
-        const uint32_t x = i ^ j;
-        if (x > i) {
-          const bool up = (i & k) == 0;
-          const int32_t pi = p ? p[i] : 0, px = p ? p[x] : 0;
-          const bool gt = less3(a[x], b[x], px, a[i], b[i], pi);
-          if (gt == up) {
-            uint64_t t = a[i]; a[i] = a[x]; a[x] = t;
-            t = b[i]; b[i] = b[x]; b[x] = t;
-            if (p) { const int32_t q = p[i]; p[i] = p[x]; p[x] = q; }
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// block-wide reductions through the DPP wave reductions + LDS
-__device__ __forceinline__ uint64_t block_red_u64(Smem &s, uint64_t wave_val, int op /*0 sum,1 or,2 max,3 min*/) {
-  const uint32_t w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) s.red[w] = wave_val;
-  __syncthreads();
-  uint64_t r = s.red[0];
-  for (int i = 1; i < NW; ++i) {
-    const uint64_t x = s.red[i];
-    r = op == 0 ? r + x : op == 1 ? (r | x) : op == 2 ? (r > x ? r : x) : (r < x ? r : x);
-  }
-  __syncthreads();
-  return r;
-}
-
 template <int DMAX, int TYPE>
-__global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am_read_result R) {
+__global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                am_retry retry) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   Smem s = carve(smem_raw);
   const uint32_t tid = threadIdx.x;
@@ -128,7 +109,10 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
   const uint32_t np = nd * nd;
   const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
 
-  for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : n;
+  for (uint64_t i = blockIdx.x; i < nsel; i += gridDim.x) {
+    const uint64_t r = S.idx ? (uint64_t)uniform_u32(S.idx[sel0 + i]) : i;
     const uint64_t key = uniform_u64(B.key[r]);
     const uint32_t rtype = uniform_u32(B.type[r]);
     int32_t status = AM_OK;
@@ -145,6 +129,11 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
     }
     if (status != AM_OK) {
       if (tid == 0) R.status[r] = status;
+      continue;
+    }
+    // A log far beyond the LDS tier goes straight to the big-read path (am_big.hip).
+    if (retry.list && off1 - off0 > BIG_OPS) {
+      if (tid == 0) retry.list[atomicAdd(retry.count, 1u)] = (uint32_t)r;
       continue;
     }
 
@@ -199,6 +188,7 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
 
     Acc<DMAX> a;
     a.reset();
+    LdsSink sink{&s};
     // ---- stream the log, 1024 ops per tile ----
     for (uint64_t t0 = off0 & ~(uint64_t)(OPL - 1); t0 < off1; t0 += TILE) {
       const uint64_t g = t0 + (uint64_t)tid * OPL;
@@ -232,82 +222,16 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
           if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
           const int32_t pos = (int32_t)(p - off0);
           if (TYPE == AM_BCOUNTER) {
-            const uint32_t kind = AM_META_KIND(meta);
-            const uint32_t from = (uint32_t)(L.p1[p] & 0xFF), to = (uint32_t)((L.p1[p] >> 8) & 0xFF);
-            if (kind > AM_BC_TRANSFER || from >= nd || to >= nd) {
+            uint32_t slot;
+            int64_t v;
+            if (!bc_slot(L, p, meta, nd, slot, v)) {
               a.flags |= FLAG_BAD;
               continue;
             }
-            const uint32_t slot = kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
-            const int64_t v = (int64_t)L.p0[p];
-            const uint64_t old = atomicAdd((unsigned long long *)&s.slo[slot], (unsigned long long)v);
-            const int64_t carry = (old + (uint64_t)v < old) ? 1 : 0;
-            atomicAdd((unsigned long long *)&s.shi[slot], (unsigned long long)((v < 0 ? -1 : 0) + carry));
+            acc128_atomic(&s.slo[slot], &s.shi[slot], v < 0 ? -1 : 0, (uint64_t)v);
             atomicOr(&s.spres[slot], 1u);
-          } else if (TYPE == AM_MVREG) {
-            const uint64_t vo = L.var_off ? L.var_off[p] : 0, ve = L.var_off ? L.var_off[p + 1] : 0;
-            const uint32_t nk = (uint32_t)(ve - vo);
-            if (nk) {
-              const uint32_t i0 = atomicAdd(&s.ctr[0], nk);
-              if (i0 + nk > KCAP) {
-                s.ctr[3] = 1;
-              } else {
-                for (uint32_t i = 0; i < nk; ++i) {
-                  s.ka[i0 + i] = L.var_data[vo + i];
-                  s.kb[i0 + i] = 0;
-                  s.kp[i0 + i] = pos;
-                }
-              }
-            }
-            if (AM_META_KIND(meta) != AM_MV_RESET) {
-              const uint32_t bi = atomicAdd(&s.ctr[1], 1u);
-              if (bi >= BCAP) {
-                s.ctr[3] = 1;
-              } else {
-                s.ba[bi] = L.p0[p];
-                s.bb[bi] = L.p1[p];
-                s.bp[bi] = pos;
-              }
-            }
-          } else {  // AW-set effect entries [elem, n_add, n_rm, add..., rm...]
-            uint64_t q = L.var_off ? L.var_off[p] : 0;
-            const uint64_t qe = L.var_off ? L.var_off[p + 1] : 0;
-            while (q < qe) {
-              if (q + 3 > qe) {
-                a.flags |= FLAG_BAD;
-                break;
-              }
-              const uint64_t e = L.var_data[q], na = L.var_data[q + 1], nr = L.var_data[q + 2];
-              if (na > qe - q || nr > qe - q || q + 3 + na + nr > qe) {
-                a.flags |= FLAG_BAD;
-                break;
-              }
-              if (na) {
-                const uint32_t bi = atomicAdd(&s.ctr[1], (uint32_t)na);
-                if (bi + na > BCAP) {
-                  s.ctr[3] = 1;
-                } else {
-                  for (uint32_t i = 0; i < na; ++i) {
-                    s.ba[bi + i] = e;
-                    s.bb[bi + i] = L.var_data[q + 3 + i];
-                    s.bp[bi + i] = pos;
-                  }
-                }
-              }
-              if (nr) {
-                const uint32_t ki = atomicAdd(&s.ctr[0], (uint32_t)nr);
-                if (ki + nr > KCAP) {
-                  s.ctr[3] = 1;
-                } else {
-                  for (uint32_t i = 0; i < nr; ++i) {
-                    s.ka[ki + i] = L.var_data[q + 3 + na + i];  // token
-                    s.kb[ki + i] = e;
-                    s.kp[ki + i] = pos;
-                  }
-                }
-              }
-              q += 3 + na + nr;
-            }
+          } else if (!set_effects<TYPE>(L, p, meta, pos, sink)) {
+            a.flags |= FLAG_BAD;
           }
         }
       }
@@ -315,15 +239,22 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
     __syncthreads();
 
     // ---- scalar outputs (block reductions) ----
-    const uint32_t count = (uint32_t)block_red_u64(s, wave_sum_u32(a.count), 0);
-    const uint32_t flags = (uint32_t)block_red_u64(s, wave_or_u32(a.flags), 1);
-    const uint32_t pres = (uint32_t)block_red_u64(s, wave_or_u32(a.pres), 1);
-    const uint64_t min_excl = block_red_u64(s, wave_min_u64(a.min_excl), 3);
+    const uint32_t count = (uint32_t)block_red_u64(s.red, wave_sum_u32(a.count), 0);
+    const uint32_t flags = (uint32_t)block_red_u64(s.red, wave_or_u32(a.flags), 1);
+    const uint32_t pres = (uint32_t)block_red_u64(s.red, wave_or_u32(a.pres), 1);
+    const uint64_t min_excl = block_red_u64(s.red, wave_min_u64(a.min_excl), 3);
     uint64_t mx[DMAX];
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? block_red_u64(s, wave_max_u64(a.mx[d]), 2) : 0;
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? block_red_u64(s.red, wave_max_u64(a.mx[d]), 2) : 0;
     status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
-    if (status == AM_OK && s.ctr[3]) status = AM_ERR_CAPACITY;
+    if (status == AM_OK && s.ctr[3]) {
+      if (retry.list) {  // the births/kills did not fit in LDS: hand the read to am_big.hip
+        if (tid == 0) retry.list[atomicAdd(retry.count, 1u)] = (uint32_t)r;
+        __syncthreads();
+        continue;
+      }
+      status = AM_ERR_CAPACITY;
+    }
 
     if (status == AM_OK && TYPE == AM_BCOUNTER) {
       uint32_t *ovf = &s.ctr[8];  // no static __shared__: keeps the dynamic LDS base 16-byte aligned
@@ -376,28 +307,8 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
       block_sort(s.oa, s.ob, nullptr, no, BCAP);
       // drop duplicates and write the CSR (compaction by wave ballots)
       const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
-      uint32_t base = 0;
-      for (uint32_t c = 0; c < no; c += BLOCK) {
-        const uint32_t i = c + tid;
-        const bool keep = i < no && (i == 0 || s.oa[i] != s.oa[i - 1] || s.ob[i] != s.ob[i - 1]);
-        const uint64_t m = __ballot(keep);
-        const uint32_t w = tid >> 6, l = tid & 63;
-        const uint32_t before = __popcll(m & ((1ull << l) - 1));
-        if (l == 0) s.ctr[4 + w] = __popcll(m);
-        __syncthreads();
-        uint32_t woff = 0;
-        for (uint32_t k = 0; k < w; ++k) woff += s.ctr[4 + k];
-        const uint32_t total = s.ctr[4] + s.ctr[5] + s.ctr[6] + s.ctr[7];
-        if (keep) {
-          const uint32_t o = base + woff + before;
-          if (o < ocap) {
-            R.value.set_a[ooff + o] = s.oa[i];
-            R.value.set_b[ooff + o] = s.ob[i];
-          }
-        }
-        base += total;
-        __syncthreads();
-      }
+      const uint32_t base =
+          block_write_unique(s.oa, s.ob, no, R.value.set_a + ooff, R.value.set_b + ooff, ocap, &s.ctr[4]);
       if (base > ocap) status = AM_ERR_CAPACITY;
       else if (tid == 0) R.value.set_len[r] = base;
     }
@@ -432,14 +343,28 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
   }
 }
 
+// A mixed batch whose result lacks this type's value columns: its reads of the type
+// (if any; the count lives on the device) fail with AM_ERR_INVALID.
+__global__ void k_sets_nocols(am_read_result R, am_sel S) {
+  const uint32_t b0 = S.range[0], b1 = S.range[1];
+  for (uint32_t i = b0 + blockIdx.x * blockDim.x + threadIdx.x; i < b1; i += gridDim.x * blockDim.x)
+    R.status[S.idx[i]] = AM_ERR_INVALID;
+}
+
 template <int TYPE>
-int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
-  if (TYPE != AM_BCOUNTER && (!R->value.set_off || !R->value.set_len || !R->value.set_a || !R->value.set_b)) {
-    am_set_error("set results need value.set_off/set_len/set_a/set_b");
-    return AM_ERR_INVALID;
+int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                am_retry retry) {
+  const bool cols = TYPE == AM_BCOUNTER
+                        ? (R->value.bc_p && R->value.bc_p_pres && R->value.bc_d && R->value.bc_d_pres)
+                        : (R->value.set_off && R->value.set_len && R->value.set_a && R->value.set_b);
+  if (!cols && S.idx) {
+    hipLaunchKernelGGL(k_sets_nocols, dim3(64), dim3(256), 0, ctx->stream, *R, S);
+    AM_HIP(hipGetLastError());
+    return AM_OK;
   }
-  if (TYPE == AM_BCOUNTER && (!R->value.bc_p || !R->value.bc_p_pres || !R->value.bc_d || !R->value.bc_d_pres)) {
-    am_set_error("bcounter results need value.bc_p/bc_p_pres/bc_d/bc_d_pres");
+  if (!cols) {
+    am_set_error(TYPE == AM_BCOUNTER ? "bcounter results need value.bc_p/bc_p_pres/bc_d/bc_d_pres"
+                                     : "set results need value.set_off/set_len/set_a/set_b");
     return AM_ERR_INVALID;
   }
   if (TYPE == AM_BCOUNTER && (size_t)L->n_dc * L->n_dc + L->n_dc > KCAP) {
@@ -460,7 +385,7 @@ int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read
       attr = true;                                                                                     \
     }                                                                                                  \
     hipLaunchKernelGGL((k_sets<D, TYPE>), dim3((unsigned)blocks), dim3(BLOCK), SMEM_BYTES, ctx->stream, \
-                       *L, *B, *R);                                                                    \
+                       *L, *B, *R, S, retry);                                                          \
   }                                                                                                    \
   break;
   switch (nd <= 1 ? 1 : nd <= 2 ? 2 : nd <= 3 ? 3 : nd <= 4 ? 4 : nd <= 8 ? 8 : nd <= 16 ? 16 : 32) {
@@ -479,11 +404,12 @@ int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read
 
 }  // namespace
 
-int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
-  switch (B->type_hint) {
-    case AM_AWSET: return launch_sets<AM_AWSET>(ctx, L, B, R);
-    case AM_MVREG: return launch_sets<AM_MVREG>(ctx, L, B, R);
-    case AM_BCOUNTER: return launch_sets<AM_BCOUNTER>(ctx, L, B, R);
+int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                   uint32_t type, am_retry retry) {
+  switch (type) {
+    case AM_AWSET: return launch_sets<AM_AWSET>(ctx, L, B, R, S, retry);
+    case AM_MVREG: return launch_sets<AM_MVREG>(ctx, L, B, R, S, retry);
+    case AM_BCOUNTER: return launch_sets<AM_BCOUNTER>(ctx, L, B, R, S, retry);
     default: return AM_ERR_UNSUPPORTED;
   }
 }

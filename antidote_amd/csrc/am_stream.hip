@@ -57,15 +57,19 @@ struct Out {
 };
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
-__global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, am_read_result R) {
+__global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, am_read_result R, am_sel S) {
   using V = typename ValOf<TYPE>::T;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint64_t n = B.n_reads;
+  const uint64_t n = B.n_reads;  // column stride of per-read arrays
+  // reads to process: slots [0, nsel) -> read sbase[slot] (or the identity)
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : n;
+  const uint32_t *sbase = S.idx ? S.idx + sel0 : nullptr;
   const uint32_t nd = L.n_dc;
   const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
   const uint64_t W = (uint64_t)gridDim.x * WPB;
   const uint64_t gw = (uint64_t)blockIdx.x * WPB + uniform_u32(threadIdx.x >> 6);
-  const uint64_t n_batches = (n + WAVE - 1) / WAVE;
+  const uint64_t n_batches = (nsel + WAVE - 1) / WAVE;
   if (gw >= n_batches) return;
 
   ReadU<DMAX> u;
@@ -86,16 +90,17 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
 
   // ---- batch metadata (lane i: read rb+i), double-buffered across batches ----
   struct Meta {
-    uint64_t key, off0, off1, rb;
+    uint64_t key, off0, off1, rb, r;  // rb: first slot of the batch; r: lane's read index
     int32_t st;
     uint32_t nb;
   };
   auto load_meta = [&](uint64_t bid, Meta &M) {
     M.rb = bid * WAVE;
-    M.nb = bid < n_batches ? (uint32_t)(n - M.rb < (uint64_t)WAVE ? n - M.rb : (uint64_t)WAVE) : 0u;
-    M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK;
+    M.nb = bid < n_batches ? (uint32_t)(nsel - M.rb < (uint64_t)WAVE ? nsel - M.rb : (uint64_t)WAVE) : 0u;
+    M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK, M.r = 0;
     if (lane < M.nb) {
-      const uint64_t r = M.rb + lane;
+      const uint64_t r = sbase ? (uint64_t)sbase[M.rb + lane] : M.rb + lane;
+      M.r = r;
       const uint64_t key = B.key[r];
       const uint32_t rtype = B.type[r];
       M.key = key;
@@ -133,7 +138,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
     for (int d = 0; d < DMAX; ++d) o.ct[d] = 0;
     o.v0 = 0, o.v1 = 0, o.vflag = TYPE == AM_LWW ? 1 : 0;
     if (GENERAL && lane < M.nb) {
-      const uint64_t r = M.rb + lane;
+      const uint64_t r = M.r;
       if (B.base_ignore && !B.base_ignore[r]) {
         o.ign = 0;
         o.pres = B.base_pres[r] & u.allmask;
@@ -153,7 +158,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   // the batch's results: one coalesced store per column
   auto store_out = [&](const Meta &M) {
     if (lane < M.nb) {
-      const uint64_t r = M.rb + lane;
+      const uint64_t r = M.r;
       R.status[r] = o.status;
       if (o.status == AM_OK) {
         R.flags[r] = (uint8_t)o.flags;
@@ -236,7 +241,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   };
   auto setup_read = [&](uint32_t j) {  // per-read uniform inputs (GENERAL only)
     if (!GENERAL) return;
-    const uint64_t r = M0.rb + j;
+    const uint64_t r = lane_u64(M0.r, j);
     if (B.per_read_clock) load_clock(r, n);
     u.base_ignore = !B.base_ignore || B.base_ignore[r];
     u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
@@ -290,7 +295,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       int64_t hi = v.hi;
       uint64_t lo = v.lo;
       wave_sum_i128(hi, lo);
-      const int64_t b = (GENERAL && B.base.v0) ? uniform_u64((uint64_t)B.base.v0[M0.rb + j]) : 0;
+      const int64_t b = (GENERAL && B.base.v0) ? uniform_u64((uint64_t)B.base.v0[lane_u64(M0.r, j)]) : 0;
       add128(hi, lo, b < 0 ? -1 : 0, (uint64_t)b);
       if (status == AM_OK && hi != ((int64_t)lo < 0 ? -1 : 0)) status = AM_ERR_OVERFLOW;  // Erlang: bignum
       v0 = lo;
@@ -299,7 +304,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       uint64_t bts = 0, bval = 0;
       uint32_t bbin = 1;  // new() = {0, <<>>}
       if (GENERAL && B.base.v0) {
-        const uint64_t r = M0.rb + j;
+        const uint64_t r = lane_u64(M0.r, j);
         bts = uniform_u64((uint64_t)B.base.v0[r]);
         bval = B.base.v1 ? uniform_u64(B.base.v1[r]) : 0;
         bbin = B.base.vflag ? uniform_u32(B.base.vflag[r]) : 0;
@@ -393,7 +398,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
 }
 
 template <int D, int TYPE, bool GENERAL, bool PACKED>
-int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S) {
   // persistent-style grid: at most the resident capacity, at most one wave per 64-read batch
   static int occ = 0;
   if (occ == 0) {
@@ -409,40 +414,44 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
   hipLaunchKernelGGL((k_stream<D, TYPE, GENERAL, PACKED>), dim3((unsigned)blocks), dim3(BLOCK), 0, ctx->stream, *L, *B,
-                     *R);
+                     *R, S);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }
 
 template <int TYPE, bool GENERAL, bool PACKED>
-int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S) {
   const uint32_t nd = L->n_dc;
-  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R);
-  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R);
-  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R);
-  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R);
-  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R);
-  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R);
-  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R);
+  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
 }
 
 }  // namespace
 
 // FAST variant when the batch uses none of: partial snapshot clocks, explicit op
 // ids, TxIds, cached bases, per-read clocks (the bench's fresh snapshot read).
-int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+// With a selection (planner sub-batch) the read count lives on the device: the grid is
+// the resident capacity and surplus waves exit at once.
+int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                     uint32_t type) {
   const bool general = L->snap_pres || L->op_id || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock ||
                        B->base.v0;
   // packed view: streaming bytes per op 8 + 4*D + payload instead of 9 + 8*D + payload
   const char *pv = getenv("AM_PACKED");
   const bool packed = L->ct_meta && L->snap_delta && !L->snap_pres && !(pv && pv[0] == '0');
-  switch (B->type_hint) {
+  switch (type) {
     case AM_PN:
-      if (general) return packed ? launch<AM_PN, true, true>(ctx, L, B, R) : launch<AM_PN, true, false>(ctx, L, B, R);
-      return packed ? launch<AM_PN, false, true>(ctx, L, B, R) : launch<AM_PN, false, false>(ctx, L, B, R);
+      if (general) return packed ? launch<AM_PN, true, true>(ctx, L, B, R, S) : launch<AM_PN, true, false>(ctx, L, B, R, S);
+      return packed ? launch<AM_PN, false, true>(ctx, L, B, R, S) : launch<AM_PN, false, false>(ctx, L, B, R, S);
     case AM_LWW:
-      if (general) return packed ? launch<AM_LWW, true, true>(ctx, L, B, R) : launch<AM_LWW, true, false>(ctx, L, B, R);
-      return packed ? launch<AM_LWW, false, true>(ctx, L, B, R) : launch<AM_LWW, false, false>(ctx, L, B, R);
+      if (general)
+        return packed ? launch<AM_LWW, true, true>(ctx, L, B, R, S) : launch<AM_LWW, true, false>(ctx, L, B, R, S);
+      return packed ? launch<AM_LWW, false, true>(ctx, L, B, R, S) : launch<AM_LWW, false, false>(ctx, L, B, R, S);
     default:
       return AM_ERR_UNSUPPORTED;
   }

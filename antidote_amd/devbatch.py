@@ -23,12 +23,15 @@ class DeviceReads:
     base snapshot = ignore (fresh) unless set_base() is used."""
 
     def __init__(self, n_reads: int, n_dc: int, type_: int, clock: Sequence[int], pres: Optional[int] = None,
-                 device: str = "cuda", keys: Optional[torch.Tensor] = None, set_cap: int = 96):
+                 device: str = "cuda", keys: Optional[torch.Tensor] = None, set_cap: int = 96,
+                 types: Optional[torch.Tensor] = None):
+        """type_ = the batch's type_hint (0 = mixed: `types` gives each read's type)."""
         self.n, self.n_dc, self.type = n_reads, n_dc, type_
         dev = torch.device(device)
         self.dev = dev
         self.key = keys if keys is not None else torch.arange(n_reads, dtype=torch.int64, device=dev)
-        self.types = torch.full((n_reads,), type_, dtype=torch.uint8, device=dev)
+        self.types = types if types is not None else torch.full((n_reads,), type_, dtype=torch.uint8, device=dev)
+        present = set(int(x) for x in torch.unique(self.types).cpu().tolist()) if type_ == 0 else {type_}
         self.read_vc = _u64_tensor(list(clock), dev)
         self.read_pres = torch.tensor([pres if pres is not None else (1 << n_dc) - 1], dtype=torch.int32, device=dev)
         self.base_ignore = None
@@ -49,13 +52,13 @@ class DeviceReads:
         self.vflag = z(torch.uint8, n_reads)
         self.set_off = self.set_len = self.set_a = self.set_b = None
         self.bc_p = self.bc_pp = self.bc_d = self.bc_dp = None
-        if type_ in (abi.AM_AWSET, abi.AM_MVREG):
-            self.set_cap = set_cap
+        self.set_cap = set_cap
+        if present & {abi.AM_AWSET, abi.AM_MVREG}:
             self.set_off = torch.arange(0, (n_reads + 1) * set_cap, set_cap, dtype=torch.int64, device=dev)
             self.set_len = z(torch.int32, n_reads)
             self.set_a = z(torch.int64, n_reads * set_cap)
             self.set_b = z(torch.int64, n_reads * set_cap)
-        elif type_ == abi.AM_BCOUNTER:
+        if abi.AM_BCOUNTER in present:
             self.bc_p = z(torch.int64, n_reads, n_dc * n_dc)
             self.bc_pp = z(torch.uint8, n_reads, n_dc * n_dc)
             self.bc_d = z(torch.int64, n_reads, n_dc)
@@ -96,29 +99,31 @@ class DeviceReads:
         """Decoded values of reads idx (host), in the oracle's rendering."""
         out = []
         nd = self.n_dc
-        if self.type in (abi.AM_AWSET, abi.AM_MVREG):
+        types = self.types.cpu().numpy()
+        sl = sa = sb = bp = bpp = bd = bdp = None
+        if self.set_len is not None:
             sl = self.set_len.cpu().numpy()
             sa = self.set_a.cpu().numpy().view(np.uint64)
             sb = self.set_b.cpu().numpy().view(np.uint64)
-            for i in idx:
-                o = int(i) * self.set_cap
-                out.append([(int(sa[o + j]), int(sb[o + j])) for j in range(int(sl[i]))])
-        elif self.type == abi.AM_BCOUNTER:
+        if self.bc_p is not None:
             bp, bpp = self.bc_p.cpu().numpy(), self.bc_pp.cpu().numpy()
             bd, bdp = self.bc_d.cpu().numpy(), self.bc_dp.cpu().numpy()
-            for i in idx:
+        v0 = self.v0.cpu().numpy()
+        v1 = self.v1.cpu().numpy().view(np.uint64)
+        vf = self.vflag.cpu().numpy()
+        for i in idx:
+            t = int(types[i])
+            if t in (abi.AM_AWSET, abi.AM_MVREG):
+                o = int(i) * self.set_cap
+                out.append([(int(sa[o + j]), int(sb[o + j])) for j in range(int(sl[i]))])
+            elif t == abi.AM_BCOUNTER:
                 pd = {(j // nd, j % nd): int(bp[i, j]) for j in range(nd * nd) if bpp[i, j]}
                 dd = {j: int(bd[i, j]) for j in range(nd) if bdp[i, j]}
                 out.append((pd, dd))
-        else:
-            v0 = self.v0.cpu().numpy()
-            v1 = self.v1.cpu().numpy().view(np.uint64)
-            vf = self.vflag.cpu().numpy()
-            for i in idx:
-                if self.type == abi.AM_PN:
-                    out.append(int(v0[i]))
-                else:
-                    out.append((int(v0[i:i + 1].view(np.uint64)[0]), int(v1[i]), bool(vf[i])))
+            elif t == abi.AM_PN:
+                out.append(int(v0[i]))
+            else:
+                out.append((int(v0[i:i + 1].view(np.uint64)[0]), int(v1[i]), bool(vf[i])))
         return out
 
     def host(self, lo: int = 0, hi: Optional[int] = None):

@@ -7,13 +7,15 @@ One step = one batched snapshot read of every key this GPU owns:
      snapshot lands in HBM and is the read's MinSnapshotTime (as a ClockSI
      transaction reads at the GST, src/clocksi_interactive_coord.erl:907-912);
   2. am_materialize of all keys at that snapshot (clocksi_materializer:materialize/4
-     per key, fresh base: the first read of each key).
-Workload (BASELINE.json configs[1], "C2"): antidote_crdt_register_lww, 1M keys x 256
-ops per GPU, 3-DC vectorclocks, synthetic counter-based logs generated in HBM.
-Weak scaling: each rank owns its own 1M keys (keys shard by riak_core partition:
-partition = key mod 64, GPU = partition mod N), so value = N * 256M ops / step time.
+     per key, fresh base: the first read of each key).  Mixed-type configs (c4, c5) are
+     one mixed batch: the library's planner splits it by type on the device.
+Default workload (BASELINE.json configs[1], "c2"): antidote_crdt_register_lww, 1M keys x
+256 ops per GPU, 3-DC vectorclocks, synthetic counter-based logs generated in HBM.
+--config c1..c5 selects the other BASELINE.json configs (see CONFIGS).
+Weak scaling: each rank owns its own keys (keys shard by riak_core partition:
+partition = key mod 64, GPU = partition mod N), so value = N * ops per GPU / step time.
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 under
+Launch: python bench.py [--gpus 1 --steps K --warmup W --config c2]; for N > 1 under
 torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR from the env).
 """
 from __future__ import annotations
@@ -31,82 +33,126 @@ sys.path.insert(0, HERE)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from antidote_amd import abi  # noqa: E402
+from antidote_amd import abi, synth  # noqa: E402
 from antidote_amd.devbatch import DeviceReads, materialize  # noqa: E402
 from antidote_amd.materializer import Materializer  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 N_PARTITIONS = 64          # riak_core ring for the multi-GPU layout
+Q = 0.75                   # snapshot quantile: ~75% of each log is in the read's snapshot
 
+# Workloads (BASELINE.json configs), per GPU: weak scaling, each rank owns
+# its own keys, so the node-wide totals of C4/C5 are reached at N = 8.
 CONFIGS = {
-    # name: (type, n_dc, keys per GPU, ops per key, q)
-    "c2": (abi.AM_LWW, 3, 1 << 20, 256, 0.75),
-    "c1": (abi.AM_PN, 1, 10000, 64, 0.75),
+    "c1": dict(type=abi.AM_PN, n_dc=1, n_keys=10000, ops=64, set_cap=0,
+               desc="antidote_crdt_counter_pn, 10000 keys x 64 ops, D=1"),
+    "c2": dict(type=abi.AM_LWW, n_dc=3, n_keys=1 << 20, ops=256, set_cap=0,
+               desc="antidote_crdt_register_lww, 1048576 keys x 256 ops per GPU, D=3"),
+    "c3": dict(type=abi.AM_AWSET, n_dc=8, n_keys=1 << 20, ops=1024, set_cap=64,
+               desc="antidote_crdt_set_aw, 1048576 keys x 1024 ops per GPU, D=8, 64-element universe"),
+    "c4": dict(type=0, n_dc=3, n_keys=8 << 20, ops=16, set_cap=16,
+               desc="mixed 40% PN / 20% LWW / 20% AW-set / 20% MV, 8388608 keys x 16 ops per GPU "
+                    "(64M keys at 8 GPUs), D=3"),
+    "c5": dict(type=abi.AM_SYNTH_MV_BC, n_dc=16, n_keys=2 << 20, zipf=1.1, total_ops=128 << 20, hot_cap=1 << 20,
+               set_cap=8, desc="MV register + bounded counter (50/50), Zipf s=1.1 key popularity, 2097152 keys / "
+                               "134217728 ops per GPU (16M keys / 1G ops at 8 GPUs), hot-key cap 2^20, D=16"),
 }
 
 
 def bytes_per_op(type_: int, n_dc: int, packed: bool = True) -> int:
-    """Algorithmic HBM bytes read per op by the materialize kernel.
-    Packed view (am_pack.hip): ct_meta 8 + snapshot deltas 4*D + payload (PN 8, LWW 16);
-    full view: op_meta 1 + commit_time 8 + snapshot_time 8*D + payload."""
-    payload = 16 if type_ == abi.AM_LWW else 8
-    return (8 + 4 * n_dc + payload) if packed else (1 + 8 + 8 * n_dc + payload)
+    """Algorithmic HBM bytes read per op by its materialize kernel.
+    k_stream packed view: ct_meta 8 + snapshot deltas 4*D + payload (PN 8, LWW 16);
+    full view (k_sets, k_big_chunk): op_meta 1 + commit_time 8 + snapshot_time 8*D + payload
+    (PN 8, LWW 16; AW var_off 8; MV p0 p1 var_off 24; bcounter p0 p1 16).  Variable-length
+    effect words (AW entries, MV overridden tokens) are counted separately, 8 B each."""
+    if type_ in (abi.AM_PN, abi.AM_LWW):
+        payload = 16 if type_ == abi.AM_LWW else 8
+        return (8 + 4 * n_dc + payload) if packed else (1 + 8 + 8 * n_dc + payload)
+    payload = {abi.AM_AWSET: 8, abi.AM_MVREG: 24, abi.AM_BCOUNTER: 16}[type_]
+    return 1 + 8 + 8 * n_dc + payload
 
 
-def bytes_per_key(type_: int, n_dc: int) -> int:
+def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
     """Per read: key index 8 + type 1 + key_off 8 + key_type 1 (inputs) + outputs status 4,
     new_last_op 8, last_ct 8*D, last_ct_pres 4, last_ct_ignore 1, is_new_ss 1, count 4,
-    flags 1, value (PN 8; LWW 8+8+1)."""
-    val = 17 if type_ == abi.AM_LWW else 8
+    flags 1, value (PN 8; LWW 8+8+1; sets set_off 8 + set_len 4 + 16 per pair written;
+    bcounter (D*D + D) slots x 9)."""
+    if type_ == abi.AM_PN:
+        val = 8
+    elif type_ == abi.AM_LWW:
+        val = 17
+    elif type_ == abi.AM_BCOUNTER:
+        val = 9 * (n_dc * n_dc + n_dc)
+    else:
+        val = 12 + 16 * set_len
     return 8 + 1 + 8 + 1 + 4 + 8 + 8 * n_dc + 4 + 1 + 1 + 4 + 1 + val
 
 
-def synth_params(type_, n_dc, n_keys, n_ops, key_base):
-    p = abi.am_synth_params()
-    p.seed, p.n_keys, p.ops_per_key, p.n_dc, p.type, p.key_base, p.max_lag = (0x5EED + 2, n_keys, n_ops, n_dc,
-                                                                               type_, key_base, 8)
-    return p
+def synth_params(cfg, key_base):
+    return synth.params(cfg["n_keys"], cfg["n_dc"], cfg["type"], ops_per_key=cfg.get("ops", 0), key_base=key_base,
+                        zipf=cfg.get("zipf", 0.0), total_ops=cfg.get("total_ops", 0), hot_cap=cfg.get("hot_cap", 0))
 
 
-def cpu_baseline(p, q, budget_s=10.0, sample_keys=100_000):
+def key_columns(mat, dlog, n_keys):
+    """key_off / key_type of the device log, on the host (setup only)."""
+    ko = np.empty(n_keys + 1, np.uint64)
+    kt = np.empty(n_keys, np.uint8)
+    abi.check(mat.L.am_memcpy_d2h(mat.ctx, ko.ctypes.data, dlog.key_off, ko.nbytes), "d2h key_off")
+    abi.check(mat.L.am_memcpy_d2h(mat.ctx, kt.ctypes.data, dlog.key_type, kt.nbytes), "d2h key_type")
+    return ko, kt
+
+
+def workload_bytes(cfg, dlog, ko, kt, reads, packed):
+    """Algorithmic bytes of one am_materialize over every key of the store."""
+    lens = np.diff(ko.astype(np.int64))
+    total = float(dlog.n_var) * 8
+    set_len = reads.set_len.cpu().numpy() if reads.set_len is not None else None
+    for t in sorted(set(int(x) for x in np.unique(kt))):
+        m = kt == t
+        total += float(lens[m].sum()) * bytes_per_op(t, cfg["n_dc"], packed)
+        sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG)) else 0.0
+        total += float(m.sum()) * bytes_per_key(t, cfg["n_dc"], sl)
+    return total
+
+
+def cpu_baseline(cfg, p, budget_s=10.0):
     """The C restatement (oracle/am_oracle.c, a port of clocksi_materializer) on the host
-    cores, on a bounded sample of the same workload.  Rank 0, N=1 only."""
-    sys.path.insert(0, HERE)
-    from antidote_amd.oplog import HostBatch, HostLog, Read
+    cores, on a bounded sample of the same workload (host-regenerated keys).  Rank 0, N=1."""
+    from antidote_amd.oplog import HostBatch, Read
     from oracle import amo
     import threading
 
-    nk = min(sample_keys, p.n_keys)
-    n_ops = nk * p.ops_per_key
-    log = HostLog.__new__(HostLog)
-    log.n_dc, log.n_keys, log.n_ops, log.n_var, log.has_var = p.n_dc, nk, n_ops, 0, False
-    log.key_off = np.zeros(nk + 1, np.uint64)
-    log.key_type = np.zeros(nk, np.uint8)
-    log.key_flags = log.key_id_base = log.snap_pres = log.op_txid = log.op_id = None
-    log.op_meta = np.zeros(n_ops, np.uint8)
-    log.commit_time = np.zeros(n_ops, np.uint64)
-    log.snap_vc = np.zeros((p.n_dc, n_ops), np.uint64)
-    log.p0 = np.zeros(n_ops, np.uint64)
-    log.p1 = np.zeros(n_ops, np.uint64)
-    log.var_off = log.var_data = None
-    s = log.as_struct()
-    abi.check(abi.lib().am_synth_host(ctypes.byref(p), 0, nk, ctypes.byref(s)), "am_synth_host")
-    clock = (ctypes.c_uint64 * p.n_dc)()
-    abi.lib().am_synth_read_clock(ctypes.byref(p), q, clock)
-    hb = HostBatch(p.n_dc, [Read(k, p.type, {d: clock[d] for d in range(p.n_dc)}) for k in range(nk)])
-    b, r = hb.structs()
+    ops_hint = cfg.get("ops") or max(1, cfg.get("total_ops", 1) // cfg["n_keys"])
+    nk = int(min(100_000, p.n_keys, max(2000, 25_000_000 // ops_hint)))
+    if cfg.get("zipf"):  # spread the sample over the popularity ranks: 8 equal key ranges
+        k0s = [i * (p.n_keys // 8) for i in range(8)]
+        per = nk // 8
+    else:
+        k0s, per = [0], nk
+    clock = synth.read_clock(p, Q)
+    parts = []
+    for k0 in k0s:
+        log = synth.host_log(p, k0, per)
+        kt = log.key_type[:per]
+        reads = [Read(k, int(kt[k]), {d: clock[d] for d in range(p.n_dc)}) for k in range(per)]
+        hb = HostBatch(p.n_dc, reads, [max(cfg["set_cap"], 1)] * per)
+        s = log.as_struct()
+        b, r = hb.structs()
+        parts.append((s, b, r, per, int(log.n_ops), log, hb))
+    n_ops = sum(x[4] for x in parts)
     L = amo.lib()
     threads = max(1, min(16, os.cpu_count() or 1))
-    step = (nk + threads - 1) // threads
 
     def one_pass():
-        ts = [threading.Thread(target=L.amo_materialize_range,
-                               args=(ctypes.byref(s), ctypes.byref(b), i, min(nk, i + step), ctypes.byref(r)))
-              for i in range(0, nk, step)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+        for (s, b, r, n, _, _, _) in parts:
+            step = (n + threads - 1) // threads
+            ts = [threading.Thread(target=L.amo_materialize_range,
+                                   args=(ctypes.byref(s), ctypes.byref(b), i, min(n, i + step), ctypes.byref(r)))
+                  for i in range(0, n, step)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
 
     one_pass()  # warm (page faults)
     t0 = time.perf_counter()
@@ -118,18 +164,19 @@ def cpu_baseline(p, q, budget_s=10.0, sample_keys=100_000):
             break
     dt = time.perf_counter() - t0
     return {"value": passes * n_ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
-            "sample": f"{nk} keys x {p.ops_per_key} ops of the same workload, {passes} passes in {dt:.1f}s, "
+            "sample": f"{len(k0s) * per} keys ({n_ops} ops) of the same workload, {passes} passes in {dt:.1f}s, "
                       f"C restatement of clocksi_materializer (oracle/am_oracle.c), not BEAM"}
 
 
-def load_traffic(workload: str):
+def load_traffic(config: str, workload: str):
     """HBM bytes per materialize launch from the committed PMC summary, if it matches."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
-            return d.get("bytes_per_launch")
+        e = d.get(config, d)
+        if e.get("workload") == workload:
+            return e.get("bytes_per_launch")
     except Exception:
         pass
     return None
@@ -157,7 +204,8 @@ def main():
         pg = dist
     torch.cuda.set_device(local_rank)
 
-    type_, n_dc, n_keys, n_ops, q = CONFIGS[args.config]
+    cfg = CONFIGS[args.config]
+    n_dc, n_keys, type_ = cfg["n_dc"], cfg["n_keys"], cfg["type"]
     mat = Materializer(local_rank)
 
     # ---- RCCL communicator for the GST all-reduce (the only data-path collective) ----
@@ -181,13 +229,14 @@ def main():
     abi.check(rc, "am_comm_init")
 
     # ---- this GPU's op log, generated in HBM ----
-    p = synth_params(type_, n_dc, n_keys, n_ops, key_base=rank * n_keys)
+    p = synth_params(cfg, key_base=rank * n_keys)
     store = mat.synth_store(p)
     dlog = store.device_log()
+    ko, kt = key_columns(mat, dlog, n_keys)
+    n_ops = int(ko[-1])
 
     # ---- partition stable clocks (GST inputs): this rank owns partitions r, r+N, ... ----
-    clock = (ctypes.c_uint64 * n_dc)()
-    abi.lib().am_synth_read_clock(ctypes.byref(p), q, clock)
+    clock = synth.read_clock(p, Q)
     parts = [pp for pp in range(N_PARTITIONS) if pp % world == rank]
     pvc = np.zeros((len(parts), n_dc), np.uint64)
     for i, pp in enumerate(parts):
@@ -201,7 +250,9 @@ def main():
     last_pres = torch.zeros(1, dtype=torch.int32, device="cuda")
     changed = torch.zeros(1, dtype=torch.uint8, device="cuda")
 
-    reads = DeviceReads(n_keys, n_dc, type_, list(clock))
+    types = torch.from_numpy(kt.copy()).cuda() if type_ not in range(1, 6) else None
+    reads = DeviceReads(n_keys, n_dc, type_ if type_ in range(1, 6) else 0, clock, set_cap=max(cfg["set_cap"], 1),
+                        types=types)
     read_vc, read_pres = reads.read_vc, reads.read_pres   # the GST result is written here
 
     def step():
@@ -234,12 +285,12 @@ def main():
         dt = float(t.item())
 
     # sanity: the snapshot read used the GST and every read succeeded
-    res = reads.host(0, min(n_keys, 4096))
-    assert (res["status"] == 0).all(), "materialize returned errors"
+    st = reads.status.cpu().numpy()
+    assert (st == 0).all(), f"materialize returned errors: {np.unique(st, return_counts=True)}"
     gst = read_vc.cpu().numpy().view(np.uint64)
     assert [int(x) for x in gst] == [int(clock[d]) for d in range(n_dc)], "GST mismatch"
 
-    # ---- dominant kernel, timed alone with HIP events on the library's stream ----
+    # ---- the materialize batch, timed alone with HIP events on the library's stream ----
     kern_iters = max(5, args.steps)
     barrier()
     abi.check(mat.L.am_timer_start(mat.ctx), "timer")
@@ -249,13 +300,13 @@ def main():
     abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
     kern_ms = ms.value / kern_iters
     packed = bool(dlog.ct_meta) and os.environ.get("AM_PACKED", "1") != "0"
-    alg_bytes = n_keys * (n_ops * bytes_per_op(type_, n_dc, packed) + bytes_per_key(type_, n_dc))
+    alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
-    total_ops = world * n_keys * n_ops * args.steps
+    total_ops = world * n_ops * args.steps
     value = total_ops / dt
-    workload = f"{args.config}: antidote_crdt_register_lww, {n_keys} keys x {n_ops} ops per GPU, D={n_dc}" \
-        if type_ == abi.AM_LWW else f"{args.config}: antidote_crdt_counter_pn, {n_keys} keys x {n_ops} ops, D={n_dc}"
+    workload = f"{args.config}: {cfg['desc']}"
+    single = type_ in (abi.AM_PN, abi.AM_LWW)
     out = {
         "metric": "CRDT ops materialized/sec (whole node) + % HBM peak",
         "value": value,
@@ -268,20 +319,21 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic (counter-based splitmix64 op logs generated in HBM; seed 0x5EED+2)",
-        "config": {"workload": workload, "keys_per_gpu": n_keys, "ops_per_key": n_ops, "n_dc": n_dc,
-                   "snapshot_quantile": q, "partitions": N_PARTITIONS, "parallelism": f"partition-sharded x{world}",
+        "data": f"synthetic (counter-based splitmix64 op logs generated in HBM; seed {hex(p.seed)})",
+        "config": {"workload": workload, "keys_per_gpu": n_keys, "ops_per_gpu": n_ops, "n_dc": n_dc,
+                   "snapshot_quantile": Q, "partitions": N_PARTITIONS, "parallelism": f"partition-sharded x{world}",
                    "step": "GST min all-reduce (RCCL) + materialize all keys"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(workload),
-                     "kernel": "k_stream" if type_ in (abi.AM_PN, abi.AM_LWW) else "k_sets",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config, workload),
+                     "kernel": "k_stream" if single else "am_materialize (planner + k_stream/k_sets/k_big_*)",
                      "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "layout": "packed (ct_meta + int32 snapshot deltas)" if packed else "full"},
+                     "layout": "packed (ct_meta + int32 snapshot deltas) for PN/LWW, full columns for sets"
+                     if packed else "full"},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(p, q, budget_s=args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(cfg, p, budget_s=args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     mat.L.am_comm_destroy(comm)

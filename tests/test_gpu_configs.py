@@ -20,6 +20,9 @@ SHAPES = {
     "c4_mixed": dict(n_keys=20000, n_dc=3, type_=0, ops_per_key=16),
     "c5_mv_bc_zipf": dict(n_keys=20000, n_dc=16, type_=abi.AM_SYNTH_MV_BC, zipf=1.1, total_ops=300000,
                           hot_cap=900),
+    # hot keys far beyond the LDS tier (the big-read path, am_big.hip)
+    "c5_hot": dict(n_keys=3000, n_dc=16, type_=abi.AM_SYNTH_MV_BC, zipf=1.1, total_ops=400000, hot_cap=60000),
+    "c3_long": dict(n_keys=24, n_dc=8, type_=abi.AM_AWSET, ops_per_key=9000, universe=64),
 }
 
 
@@ -67,4 +70,36 @@ def test_config_shape_parity(mat, name):
                        int(h["flags"][i]))
                 assert got == r, (name, t, int(keys[i]), got, r)
             assert (h["status"] == 0).all(), (name, t)
+    st.close()
+
+
+@pytest.mark.parametrize("name", ["c4_mixed", "c5_mv_bc_zipf", "c5_hot"])
+def test_config_mixed_batch_parity(mat, name):
+    """The whole store read as ONE mixed-type batch (the planner splits it on the device),
+    sampled keys checked against the oracle."""
+    p = synth.params(**SHAPES[name])
+    st = mat.synth_store(p)
+    dlog = st.device_log()
+    hlog = synth.host_log(p, 0, p.n_keys)
+    ktypes = hlog.key_type[:p.n_keys].copy()
+    clock = synth.read_clock(p, 0.75)
+    dr = DeviceReads(p.n_keys, p.n_dc, 0, clock, set_cap=128, types=torch.from_numpy(ktypes).cuda())
+    torch.cuda.synchronize()
+    materialize(mat, dlog, dr)
+    mat.sync()
+    h = dr.host()
+    assert (h["status"] == 0).all(), np.unique(h["status"], return_counts=True)
+    rng = np.random.default_rng(5)
+    lens = np.diff(hlog.key_off.astype(np.int64))[:p.n_keys]
+    hot = np.argsort(-lens)[:8]  # always include the longest logs
+    sample = np.unique(np.concatenate([hot, rng.choice(p.n_keys, min(300, p.n_keys), replace=False)]))
+    reads = [Read(int(k), int(ktypes[k]), {d: clock[d] for d in range(p.n_dc)}) for k in sample]
+    ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, [128] * len(reads)))
+    vals = dr.values(sample)
+    for j, i in enumerate(sample):
+        ct = None if h["last_ct_ignore"][i] else {d: int(h["last_ct"][d, i]) for d in range(p.n_dc)
+                                                  if (int(h["last_ct_pres"][i]) >> d) & 1}
+        got = ("ok", vals[j], int(h["new_last_op"][i]), ct, bool(h["is_new_ss"][i]), int(h["count"][i]),
+               int(h["flags"][i]))
+        assert got == ref.result(j), (name, int(i), int(ktypes[i]), got, ref.result(j))
     st.close()

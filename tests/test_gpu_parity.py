@@ -269,14 +269,84 @@ def test_gpu_rccl_single_rank(mat):
     mat.L.am_comm_destroy(comm)
 
 
-def test_gpu_set_capacity_status(mat):
-    """A read whose births exceed the LDS capacity reports AM_ERR_CAPACITY (documented gap)."""
+def test_gpu_set_lds_overflow_goes_big(mat):
+    """A read whose births exceed one workgroup's LDS lists (1100 concurrent MV values)
+    is handed to the big-read tier (am_big.hip) and still matches the oracle."""
     ops = [Op(abi.AM_MVREG, 0, 10 + i, {0: 1}, ("assign", i, 1000 + i, [])) for i in range(1100)]
     log = HostLog(1, [ops])
-    st = mat.store(log)
-    got = mat.read_batch(st, [Read(0, abi.AM_MVREG, {0: 10**6})], [4096])
-    st.close()
-    assert got.result(0) == ("error", abi.AM_ERR_CAPACITY)
+    got = _batch_compare(log, [Read(0, abi.AM_MVREG, {0: 10**6})], mat, 1, cap=4096)
+    assert got.result(0)[0] == "ok" and len(got.result(0)[1]) == 1100
+
+
+def _big_key_ops(rng, t, n_dc, n_ops, partial, txids, bad_rate, concurrent):
+    ops = randlog.rand_key_ops(rng, t, n_dc, n_ops, partial=partial, txids=txids, bad_rate=bad_rate,
+                               t0=rng.randint(0, 50))
+    if concurrent and t == abi.AM_MVREG:  # many survivors: assigns that override nothing
+        for op in ops:
+            if not op.bad and op.effect[0] == "assign" and rng.random() < 0.7:
+                op.effect = ("assign", op.effect[1], op.effect[2], [])
+    return ops
+
+
+@pytest.mark.parametrize("t", SET_TYPES + (abi.AM_BCOUNTER,))
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_big_reads(mat, t, seed):
+    """Set-CRDT reads beyond the LDS tier (thousands of ops: chunked over workgroups with
+    local resolution + global hash), mixed with short reads of the same batch; partial
+    clocks, TxIds, cached bases, invalid effects, > 2048 survivors (global-memory sort)."""
+    rng = random.Random(7000 + seed * 13 + t)
+    n_dc = [2, 3, 8][seed]
+    partial, txids = seed == 1, seed == 2
+    keys, reads = [], []
+    lens = [0, 5, 300, 1500, 4100, 9000, 20000]
+    for k in range(12):
+        n_ops = lens[k % len(lens)]
+        keys.append(_big_key_ops(rng, t, n_dc, n_ops, partial, txids, 0.0005 if seed == 1 else 0.0,
+                                 concurrent=k % 3 == 0))
+        hi = keys[-1][-1].commit_time if keys[-1] else 50
+        q = rng.choice([0.3, 0.8, 1.0])
+        clock = randlog.rand_clock(rng, n_dc, int(hi * q), int(hi * q) + 6, partial=partial)
+        reads.append(Read(k, t, clock, rng.choice([None, 1, 3]) if txids else None))
+    log = HostLog(n_dc, keys, key_types=[t] * len(keys), partial=partial or None)
+    first = _batch_compare(log, reads, mat, n_dc, cap=16384)
+    reads2 = []
+    for i, r in enumerate(reads):
+        res = first.result(i)
+        if res[0] != "ok":
+            continue
+        clock2 = {d: v + rng.randint(0, 20000) for d, v in r.clock.items()}
+        reads2.append(Read(r.key, t, clock2, None, res[3], res[2], res[1]))
+    _batch_compare(log, reads2, mat, n_dc, cap=16384)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_mixed_type_batches(mat, seed):
+    """One batch mixing all five CRDT types (the planner partitions it on the device),
+    plus unknown keys / types and keys whose log holds another type."""
+    rng = random.Random(9100 + seed)
+    n_dc = [1, 3, 6][seed]
+    keys, types = [], []
+    for k in range(150):
+        t = randlog.TYPES[k % 5]
+        n_ops = rng.choice([0, 1, 7, 16, 64, 300, 5000 if k % 37 == 0 else 90])
+        keys.append(randlog.rand_key_ops(rng, t, n_dc, n_ops, partial=seed == 2, txids=seed == 1))
+        types.append(t)
+    log = HostLog(n_dc, keys, key_types=types, partial=(seed == 2) or None)
+    reads = []
+    for i in rng.sample(range(450), 450):
+        k = i % 150
+        t = types[k] if i < 420 else randlog.TYPES[(k + 1) % 5]  # tail: wrong type -> corrupted
+        hi = keys[k][-1].commit_time if keys[k] else 50
+        reads.append(Read(k, t, randlog.rand_clock(rng, n_dc, hi // 2, hi + 5, partial=seed == 2),
+                          rng.choice([None, 2]) if seed == 1 else None))
+    first = _batch_compare(log, reads, mat, n_dc, cap=8192)
+    assert any(first.result(i)[0] == "error" for i in range(len(reads)))
+    reads2 = []
+    for i, r in enumerate(reads):
+        res = first.result(i)
+        if res[0] == "ok":
+            reads2.append(Read(r.key, r.type, {d: v + 40 for d, v in r.clock.items()}, None, res[3], res[2], res[1]))
+    _batch_compare(log, reads2, mat, n_dc, cap=8192)
 
 
 def test_gpu_reference_system_shapes(mat):
