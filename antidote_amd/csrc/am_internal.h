@@ -36,7 +36,7 @@ struct am_retry {
 // scratch slot `slot` (0 planner, 1 big-read metadata, 2 big-read records): at least
 // `bytes` of device memory, valid until the next call for the same slot (stream-ordered
 // reuse; growing synchronizes the stream before freeing the old block)
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3 };
 int am_ctx_scratch(am_ctx *ctx, int slot, size_t bytes, void **out);
 // copy `n` u64 counters device -> host through the pinned buffer (synchronizes the stream)
 int am_ctx_fetch(am_ctx *ctx, const void *dev, uint32_t n_u64, uint64_t *host);
@@ -78,3 +78,29 @@ int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
 int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, uint32_t type,
                   am_retry retry);  // am_big.hip: reads beyond the LDS tier
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
+
+// Short-read tier (am_rows.hip): reads with at most short_max ops (and error reads) are
+// materialized by one 16-lane row each.  list/count (set types only): reads the tier
+// leaves to the workgroup tier -- longer logs, and reads whose births/kills overflow
+// the row's LDS lists -- appended in batch order (count lives on the device).
+struct am_rows_cfg {
+  uint32_t short_max = 0;
+  uint32_t *list = nullptr;
+  uint32_t *count = nullptr;
+};
+int am_launch_rows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
+                   const am_rows_cfg &C);
+// k_stream skips the reads the row tier took (len <= skip_le or an error status) when
+// skip_le >= 0
+int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                          uint32_t type, int64_t skip_le);
+// the batch uses partial clocks, op ids, TxIds, cached bases or per-read clocks
+inline bool am_batch_general(const am_op_log *L, const am_read_batch *B) {
+  return L->snap_pres || L->op_id || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock || B->base.v0 ||
+         B->base.set_off || B->base.bc_p || B->base.bc_d || B->base.bc_p_pres || B->base.bc_d_pres;
+}
+// the packed streaming view applies (ct_meta + int32 snapshot deltas, full clocks)
+inline bool am_log_packed(const am_op_log *L) {
+  const char *pv = getenv("AM_PACKED");
+  return L->ct_meta && L->snap_delta && !L->snap_pres && !(pv && pv[0] == '0');
+}

@@ -121,14 +121,55 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
   }
 }
 
-// Set kernels + the big-read tier for one type over selection S.
+// Short-read limits of the row tier (am_rows.hip); AM_ROWS=0 disables the tier (A/B),
+// AM_ROWS_SCALAR / AM_ROWS_SET override the limits (the set limit is capped by the
+// row's 64 LDS entries: one bounded-counter entry per op).
+uint32_t rows_max(bool set) {
+  const char *e = getenv("AM_ROWS");
+  if (e && e[0] == '0') return 0;
+  const char *v = getenv(set ? "AM_ROWS_SET" : "AM_ROWS_SCALAR");
+  uint32_t m = set ? 48u : 64u;
+  if (v) m = (uint32_t)strtoul(v, nullptr, 10);
+  if (set && m > 64) m = 64;
+  return m;
+}
+
+// PN / LWW over selection S: short reads on the row tier, the rest on k_stream.
+int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type) {
+  const uint32_t m = rows_max(false);
+  if (m == 0) return am_launch_stream_skip(ctx, L, B, R, S, type, -1);
+  am_rows_cfg C;
+  C.short_max = m;
+  int rc = am_launch_rows(ctx, L, B, R, S, type, C);
+  if (rc) return rc;
+  return am_launch_stream_skip(ctx, L, B, R, S, type, (int64_t)m);
+}
+
+// Set types over selection S: row tier -> (hand-off list) workgroup tier k_sets ->
+// (retry list) big-read tier.  rows_buf: [0] = 0, [1] = hand-off count, list at +64.
 int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
-             uint32_t *retry_buf) {
+             uint32_t *retry_buf, uint32_t *rows_buf) {
   am_retry retry;
   retry.count = retry_buf;
   retry.list = retry_buf + 1;
   AM_HIP(hipMemsetAsync(retry.count, 0, sizeof(uint32_t), ctx->stream));
-  int rc = am_launch_sets(ctx, L, B, R, S, type, retry);
+  const uint32_t m = rows_max(true);
+  int rc;
+  if (m) {
+    AM_HIP(hipMemsetAsync(rows_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
+    am_rows_cfg C;
+    C.short_max = m;
+    C.list = rows_buf + 64;
+    C.count = rows_buf + 1;
+    rc = am_launch_rows(ctx, L, B, R, S, type, C);
+    if (rc) return rc;
+    am_sel S2;
+    S2.idx = C.list;
+    S2.range = rows_buf;
+    rc = am_launch_sets(ctx, L, B, R, S2, type, retry);
+  } else {
+    rc = am_launch_sets(ctx, L, B, R, S, type, retry);
+  }
   if (rc) return rc;
   return am_launch_big(ctx, L, B, R, type, retry);
 }
@@ -158,12 +199,17 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   if (variant && strcmp(variant, "scalar") == 0 && B->type_hint <= AM_LWW) return am_launch_scalar(ctx, L, B, R);
 
   const am_sel all{};
-  if (B->type_hint == AM_PN || B->type_hint == AM_LWW) return am_launch_stream(ctx, L, B, R, all, B->type_hint);
+  if (B->type_hint == AM_PN || B->type_hint == AM_LWW) return run_scalar(ctx, L, B, R, all, B->type_hint);
+  void *rows_scr = nullptr;
+  if (B->type_hint != AM_PN && B->type_hint != AM_LWW) {
+    int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
+    if (rc) return rc;
+  }
   if (B->type_hint == AM_AWSET || B->type_hint == AM_MVREG || B->type_hint == AM_BCOUNTER) {
     void *scr = nullptr;
     int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &scr);
     if (rc) return rc;
-    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr);
+    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr);
   }
   if (B->type_hint != 0) {
     am_set_error("type_hint %u not supported", B->type_hint);
@@ -192,9 +238,9 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     S.idx = idx;
     S.range = range + 2 * (t - 1);
     if (t == AM_PN || t == AM_LWW)
-      rc = am_launch_stream(ctx, L, B, R, S, t);
+      rc = run_scalar(ctx, L, B, R, S, t);
     else
-      rc = run_sets(ctx, L, B, R, S, t, retry_buf);
+      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr);
     if (rc) return rc;
   }
   return AM_OK;

@@ -1,0 +1,632 @@
+// am_rows.hip -- materialize/4 for SHORT op logs: one 16-lane DPP row per read.
+//
+// A riak_core partition's keys are mostly short-lived or cold: the mixed (C4, 16 ops
+// per key) and Zipf (C5, 95% of keys with <= 48 ops) workloads are dominated by reads
+// whose whole log is a few cache lines.  Giving such a read a wavefront (k_stream) or a
+// workgroup (k_sets) leaves most lanes idle and pays a full wave/block reduction per
+// read.  Here each wavefront takes a batch of 64 consecutive reads and splits into four
+// 16-lane rows; row q owns reads 16q .. 16q+15 of the batch and walks them one after
+// another, 16 ops per step (one op per lane, a contiguous 128-byte segment per column
+// per row).  Per-read results come from DPP row butterflies (4 steps, no readlane), and
+// read 16q+s's results are parked in lane 16q+s -- so, as in k_stream, the batch's
+// results leave with one coalesced store per output column.
+//
+// Types:
+//   PN counter / LWW register  commutative reductions in registers (am_wave.h)
+//   add-wins set / MV register births / kills appended to the row's LDS lists, then the
+//                              closed form of am_sets.hip (a birth survives iff no kill
+//                              of the same token at a later position) by a brute-force
+//                              row scan, duplicate-free rank sort, CSR write
+//   bounded counter            included (slot, amount) pairs in the row's LDS list; lane
+//                              s owns slots s, s+16, ... and sums its slots exactly
+// A read longer than the short limit, or whose births/kills do not fit the row's LDS
+// lists, is handed to the workgroup tier (k_stream for PN/LWW skips it on its own; set
+// types get it through an ordered hand-off list).
+#include "am_block.h"
+
+using namespace amk;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int WPB = BLOCK / WAVE;
+constexpr int G = 16;
+constexpr uint32_t RB = 64;  // births per row
+constexpr uint32_t RK = 64;  // kills (bcounter: (slot, amount) entries) per row
+
+struct RowSmem {
+  uint64_t ba[RB], bb[RB];  // births: AW (elem, tok), MV (value, tok); later: survivors
+  int32_t bp[RB];           // birth position (-1: base snapshot); later: duplicate flag
+  uint64_t ka[RK], kb[RK];  // kills: (tok, elem) / MV (tok, 0); bcounter: amount in ka
+  int32_t kp[RK];           // kill position; bcounter: slot
+  uint32_t ctr[4];          // [0] kills / entries [1] births [2] distinct [3] overflow
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---- 16-lane row all-reductions: every lane of a row ends with the row's value.
+// Full EXEC required (DPP reads inactive lanes as 0).
+__device__ __forceinline__ uint32_t row_sum_u32(uint32_t v) {
+#define S_(C) v += dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ uint32_t row_or_u32(uint32_t v) {
+#define S_(C) v |= dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ uint64_t row_max_u64(uint64_t v) {
+#define S_(C) v = umax64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
+#define S_(C) v = umin64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ void row_sum_i128(int64_t &hi, uint64_t &lo) {
+#define S_(C)                                            \
+  {                                                      \
+    const uint64_t wlo = dpp64<C>(lo);                   \
+    const int64_t whi = (int64_t)dpp64<C>((uint64_t)hi); \
+    add128(hi, lo, whi, wlo);                            \
+  }
+  AMK_ROW_STEPS(S_)
+#undef S_
+}
+__device__ __forceinline__ void row_max_lww(LwwVal &v) {
+#define S_(C)                                                                        \
+  {                                                                                  \
+    const uint64_t wts = dpp64<C>(v.ts), wval = dpp64<C>(v.val);                     \
+    const uint32_t whas = dpp32<C>(v.has);                                           \
+    const bool gt = whas && (!v.has || wts > v.ts || (wts == v.ts && wval > v.val)); \
+    v.ts = gt ? wts : v.ts;                                                          \
+    v.val = gt ? wval : v.val;                                                       \
+    v.has |= whas;                                                                   \
+  }
+  AMK_ROW_STEPS(S_)
+#undef S_
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, WAVE);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, WAVE);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, uint32_t src) {
+  return (uint32_t)__shfl((int)v, (int)src, WAVE);
+}
+
+template <int TYPE>
+struct RowVal {  // per-lane value accumulator of the scalar types (unused for the others)
+  using T = PnVal;
+};
+template <>
+struct RowVal<AM_LWW> {
+  using T = LwwVal;
+};
+
+// births / kills appended to the row's LDS lists; overflow -> workgroup tier
+struct RowSink {
+  RowSmem *s;
+  __device__ void births(uint64_t e, const uint64_t *tok, uint32_t n, int32_t pos) {
+    const uint32_t bi = atomicAdd(&s->ctr[1], n);
+    if (bi + n > RB) {
+      s->ctr[3] = 1;
+      return;
+    }
+    for (uint32_t i = 0; i < n; ++i) s->ba[bi + i] = e, s->bb[bi + i] = tok[i], s->bp[bi + i] = pos;
+  }
+  __device__ void birth(uint64_t a, uint64_t b, int32_t pos) {
+    const uint32_t bi = atomicAdd(&s->ctr[1], 1u);
+    if (bi >= RB) {
+      s->ctr[3] = 1;
+      return;
+    }
+    s->ba[bi] = a, s->bb[bi] = b, s->bp[bi] = pos;
+  }
+  __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
+    const uint32_t ki = atomicAdd(&s->ctr[0], n);
+    if (ki + n > RK) {
+      s->ctr[3] = 1;
+      return;
+    }
+    for (uint32_t i = 0; i < n; ++i) s->ka[ki + i] = tok[i], s->kb[ki + i] = e, s->kp[ki + i] = pos;
+  }
+};
+
+template <int DMAX>
+struct ROut {  // per-lane buffered outputs of read (batch base + lane)
+  int32_t status;
+  uint32_t flags, pres, count, ign, newss, vflag, setlen, store;
+  int64_t nlo;
+  uint64_t ct[DMAX];
+  uint64_t v0, v1;
+};
+
+template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
+__global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                am_rows_cfg C) {
+  constexpr bool SETS = TYPE == AM_AWSET || TYPE == AM_MVREG;
+  constexpr bool BC = TYPE == AM_BCOUNTER;
+  constexpr bool LDS = SETS || BC;
+  using V = typename RowVal<TYPE>::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  RowSmem *rs = LDS ? ((RowSmem *)smem_raw) + (threadIdx.x / G) : nullptr;
+
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint32_t row = lane / G, sl = lane % G;
+  const uint64_t n = B.n_reads;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : n;
+  const uint32_t *sbase = S.idx ? S.idx + sel0 : nullptr;
+  const uint32_t nd = L.n_dc;
+  const uint32_t np = nd * nd, nslot = np + nd;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint64_t W = (uint64_t)gridDim.x * WPB;
+  const uint64_t gw = (uint64_t)blockIdx.x * WPB + uniform_u32(threadIdx.x >> 6);
+  const uint64_t n_batches = (nsel + WAVE - 1) / WAVE;
+  const uint32_t allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+
+  // batch-uniform read clock (per-read clocks are loaded per read below)
+  ReadU<DMAX> u;
+  u.allmask = allmask;
+  u.base_ignore = true, u.has_txid = false, u.txid = 0, u.cpres = 0;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) u.C0[d] = 0;
+  if (!GENERAL || !B.per_read_clock) {
+    u.spres = uniform_u32(B.read_pres[0]) & allmask;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[d]) : 0;
+  }
+
+  for (uint64_t bid = gw; bid < n_batches; bid += W) {
+    // ---- batch metadata: lane i <-> read rb + i ----
+    const uint64_t rb = bid * WAVE;
+    const uint32_t nb = (uint32_t)(nsel - rb < (uint64_t)WAVE ? nsel - rb : (uint64_t)WAVE);
+    uint64_t key = 0, off0 = 0, off1 = 0, r = 0;
+    int32_t st = AM_OK;
+    if (lane < nb) {
+      r = sbase ? (uint64_t)sbase[rb + lane] : rb + lane;
+      key = B.key[r];
+      const uint32_t rtype = B.type[r];
+      if (key >= L.n_keys) {
+        st = AM_ERR_INVALID;
+      } else {
+        off0 = L.key_off[key];
+        off1 = L.key_off[key + 1];
+        const uint32_t ktype = L.key_type[key];
+        const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;
+        if (off1 > off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES)))
+          st = AM_ERR_CORRUPTED_OPS_CACHE;  // erlang:error(corrupted_ops_cache)
+        else if (rtype != (uint32_t)TYPE)
+          st = AM_ERR_INVALID;
+      }
+      if (st != AM_OK) off1 = off0;
+    }
+    const uint64_t len = off1 - off0;
+    const bool mine = lane < nb && len <= C.short_max;  // error reads have len 0
+    // set types: long reads go to the workgroup tier through the ordered list
+    if (C.list) {
+      const bool hand = lane < nb && !mine;
+      const uint64_t hm = __ballot(hand);
+      if (hm) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(C.count, (uint32_t)__popcll(hm));
+        base = uniform_u32(base);
+        if (hand) C.list[base + __popcll(hm & ((1ull << lane) - 1))] = (uint32_t)r;
+      }
+    }
+
+    // ---- per-lane buffered result, initialised to materialize/4 of an empty log ----
+    ROut<DMAX> o;
+    o.status = st, o.store = mine ? 1u : 0u;
+    o.flags = 0, o.pres = 0, o.count = 0, o.ign = 1, o.newss = 0, o.nlo = 0, o.setlen = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) o.ct[d] = 0;
+    o.v0 = 0, o.v1 = 0, o.vflag = TYPE == AM_LWW ? 1 : 0;
+    if (GENERAL && mine) {
+      if (B.base_ignore && !B.base_ignore[r]) {
+        o.ign = 0;
+        o.pres = B.base_pres[r] & allmask;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          if (d < (int)nd && ((o.pres >> d) & 1u)) o.ct[d] = B.base_vc[(uint64_t)d * n + r];
+      }
+      if ((TYPE == AM_PN || TYPE == AM_LWW) && B.base.v0) {
+        o.v0 = (uint64_t)B.base.v0[r];
+        if (TYPE == AM_LWW) {
+          o.v1 = B.base.v1 ? B.base.v1[r] : 0;
+          o.vflag = B.base.vflag ? B.base.vflag[r] : 0;
+        }
+      }
+    }
+    // An empty log still returns the base value: sets copy the base CSR, bcounters the
+    // base slots (materialize/4 on [] applies no effect).  Done by the row below as a
+    // read with zero ops, so the value paths stay in one place.
+    const bool work = mine && st == AM_OK && (len > 0 || LDS);
+    const uint64_t wmask = __ballot(work);
+    if (wmask) {
+      uint32_t rowbits = (uint32_t)((wmask >> (row * G)) & 0xFFFFu);
+      uint32_t s = rowbits ? (uint32_t)__builtin_ctz(rowbits) : 16u;
+      // current read of the row (row-uniform values)
+      uint64_t o0 = 0, o1 = 0, rj = 0, keyj = 0, t = 0;
+      Acc<DMAX> a;
+      V v;
+      a.reset();
+      v.reset();
+      // (re)start the row's current read; uniform call (the shuffles need every lane),
+      // takes effect in rows with upd set; rows with s == 16 are idle
+      auto begin = [&](bool upd) {
+        const uint32_t j = row * G + (s < 16 ? s : 0);
+        const uint64_t n0 = shfl_u64(off0, j), n1 = shfl_u64(off1, j), nr = shfl_u64(r, j), nk = shfl_u64(key, j);
+        if (!upd) return;
+        o0 = n0, o1 = n1, rj = nr, keyj = nk;
+        t = 0;
+        if (s >= 16) return;
+        if (GENERAL) {
+          if (B.per_read_clock) {
+            u.spres = B.read_pres[rj] & allmask;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d)
+              u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? B.read_vc[(uint64_t)d * n + rj] : 0;
+          }
+          u.base_ignore = !B.base_ignore || B.base_ignore[rj];
+          u.cpres = u.base_ignore ? 0u : (B.base_pres[rj] & allmask);
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d)
+            u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? B.base_vc[(uint64_t)d * n + rj] : 0;
+          u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[rj]) && L.op_txid;
+          u.txid = u.has_txid ? B.txid[rj] : 0;
+        }
+        if (LDS) {
+          if (sl == 0) rs->ctr[0] = 0, rs->ctr[1] = 0, rs->ctr[2] = 0, rs->ctr[3] = 0;
+          wave_sync();
+          if (SETS && GENERAL && B.base.set_off) {  // base snapshot pairs: births at -1
+            const uint64_t bo = B.base.set_off[rj];
+            const uint32_t bl = B.base.set_len[rj];
+            if (bl > RB) {
+              if (sl == 0) rs->ctr[3] = 1;
+            } else {
+              for (uint32_t i = sl; i < bl; i += G) {
+                rs->ba[i] = B.base.set_a[bo + i];
+                rs->bb[i] = B.base.set_b[bo + i];
+                rs->bp[i] = -1;
+              }
+              if (sl == 0) rs->ctr[1] = bl;
+            }
+            wave_sync();
+          }
+        }
+      };
+      begin(true);
+      while (__ballot(s < 16)) {
+        const bool act = s < 16;
+        const uint64_t p = o0 + t + sl;
+        if (act && p < o1) {
+          // ---- one op: is_op_in_snapshot/7 + the type's effect ----
+          uint32_t meta = 0;
+          uint64_t ct = 0, sv[DMAX];
+          bool packed_ok = false;
+          if (PACKED) {
+            const uint64_t w = L.ct_meta[p];
+            meta = (uint32_t)(w >> 56);
+            if (!(w & AM_CT_ESC)) {
+              ct = w & (AM_CT_ESC - 1);
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d)
+                sv[d] = d < (int)nd ? ct - (uint64_t)(int64_t)L.snap_delta[(uint64_t)d * stride + p] : 0;
+              packed_ok = true;
+            }
+          }
+          if (!packed_ok) {
+            if (!PACKED) meta = L.op_meta[p];
+            ct = L.commit_time[p];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+          }
+          const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : allmask;
+          const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
+          if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, sp, txm, p, a) && !(LDS && (meta & AM_META_BAD))) {
+            if constexpr (TYPE == AM_PN || TYPE == AM_LWW) {
+              v.add(L.p0[p], TYPE == AM_LWW ? L.p1[p] : 0);
+            } else if constexpr (BC) {
+              uint32_t slot;
+              int64_t amt;
+              if (bc_slot(L, p, meta, nd, slot, amt)) {
+                const uint32_t e = atomicAdd(&rs->ctr[0], 1u);
+                if (e < RK) rs->ka[e] = (uint64_t)amt, rs->kp[e] = (int32_t)slot;
+                else rs->ctr[3] = 1;
+              } else {
+                a.flags |= FLAG_BAD;
+              }
+            } else {
+              RowSink sink{rs};
+              if (!set_effects<TYPE>(L, p, meta, (int32_t)(p - o0), sink)) a.flags |= FLAG_BAD;
+            }
+          }
+        }
+        t += G;
+        const bool fin = act && o0 + t >= o1;
+        if (__ballot(fin)) {
+          // ---- row reductions (full EXEC), then rows that finished a read emit it ----
+          const uint32_t count = row_sum_u32(a.count);
+          const uint32_t flags = row_or_u32(a.flags);
+          const uint32_t pres = row_or_u32(a.pres);
+          const uint64_t min_excl = row_min_u64(a.min_excl);
+          uint64_t mx[DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? row_max_u64(a.mx[d]) : 0;
+          V vr = v;  // rows still inside a read keep their per-lane partials
+          if constexpr (TYPE == AM_PN) row_sum_i128(vr.hi, vr.lo);
+          if constexpr (TYPE == AM_LWW) row_max_lww(vr);
+          wave_sync();
+          if (fin) {
+            const uint32_t j = row * G + s;
+            int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+            bool defer = false;
+            uint64_t v0 = 0, v1 = 0;
+            uint32_t vflag = 0, setlen = 0;
+            if constexpr (TYPE == AM_PN) {
+              int64_t hi = vr.hi;
+              uint64_t lo = vr.lo;
+              const int64_t b = (GENERAL && B.base.v0) ? B.base.v0[rj] : 0;
+              add128(hi, lo, b < 0 ? -1 : 0, (uint64_t)b);
+              if (status == AM_OK && hi != ((int64_t)lo < 0 ? -1 : 0)) status = AM_ERR_OVERFLOW;
+              v0 = lo;
+            } else if constexpr (TYPE == AM_LWW) {
+              uint64_t bts = 0, bval = 0;
+              uint32_t bbin = 1;  // new() = {0, <<>>}
+              if (GENERAL && B.base.v0) {
+                bts = (uint64_t)B.base.v0[rj];
+                bval = B.base.v1 ? B.base.v1[rj] : 0;
+                bbin = B.base.vflag ? B.base.vflag[rj] : 0;
+              }
+              const bool win = vr.has && (vr.ts > bts || (vr.ts == bts && !bbin && vr.val > bval));
+              v0 = win ? vr.ts : bts;
+              v1 = win ? vr.val : bval;
+              vflag = win ? 0 : bbin;
+            } else if constexpr (BC) {
+              if (status == AM_OK && rs->ctr[3]) defer = true;
+              if (status == AM_OK && !defer) {
+                const uint32_t ne = rs->ctr[0];
+                // pass 1: exact sums of the lane's slots, overflow check
+                uint32_t ovf = 0;
+                for (uint32_t i = sl; i < nslot; i += G) {
+                  int64_t bv = 0;
+                  if (GENERAL) {
+                    if (i < np) bv = B.base.bc_p ? B.base.bc_p[rj * np + i] : 0;
+                    else bv = B.base.bc_d ? B.base.bc_d[rj * nd + (i - np)] : 0;
+                  }
+                  int64_t hi = bv < 0 ? -1 : 0;
+                  uint64_t lo = (uint64_t)bv;
+                  for (uint32_t e = 0; e < ne; ++e)
+                    if ((uint32_t)rs->kp[e] == i) {
+                      const int64_t x = (int64_t)rs->ka[e];
+                      add128(hi, lo, x < 0 ? -1 : 0, (uint64_t)x);
+                    }
+                  if (hi != ((int64_t)lo < 0 ? -1 : 0)) ovf = 1;
+                }
+                if (ovf) atomicOr(&rs->ctr[2], 1u);
+                wave_sync();
+                if (rs->ctr[2]) {
+                  status = AM_ERR_OVERFLOW;
+                } else {  // pass 2: write the slots
+                  for (uint32_t i = sl; i < nslot; i += G) {
+                    int64_t bv = 0;
+                    uint32_t bpres = 0;
+                    if (GENERAL) {
+                      if (i < np) {
+                        bv = B.base.bc_p ? B.base.bc_p[rj * np + i] : 0;
+                        bpres = B.base.bc_p_pres ? B.base.bc_p_pres[rj * np + i] : 0;
+                      } else {
+                        bv = B.base.bc_d ? B.base.bc_d[rj * nd + (i - np)] : 0;
+                        bpres = B.base.bc_d_pres ? B.base.bc_d_pres[rj * nd + (i - np)] : 0;
+                      }
+                    }
+                    uint64_t lo = (uint64_t)bv;
+                    for (uint32_t e = 0; e < ne; ++e)
+                      if ((uint32_t)rs->kp[e] == i) lo += rs->ka[e], bpres = 1;
+                    if (i < np) {
+                      R.value.bc_p[rj * np + i] = (int64_t)lo;
+                      R.value.bc_p_pres[rj * np + i] = bpres ? 1 : 0;
+                    } else {
+                      R.value.bc_d[rj * nd + (i - np)] = (int64_t)lo;
+                      R.value.bc_d_pres[rj * nd + (i - np)] = bpres ? 1 : 0;
+                    }
+                  }
+                }
+              }
+            } else {  // add-wins set / MV register
+              if (status == AM_OK && rs->ctr[3]) defer = true;
+              if (status == AM_OK && !defer) {
+                const uint32_t nk = rs->ctr[0], nbth = rs->ctr[1];
+                // 1. a birth survives iff no kill of its kill key at a later position
+                uint32_t alive = 0;
+                for (uint32_t m = 0; m * G < nbth; ++m) {
+                  const uint32_t i = sl + m * G;
+                  if (i < nbth) {
+                    const uint64_t qa = rs->bb[i], qb = TYPE == AM_AWSET ? rs->ba[i] : 0ull;
+                    const int32_t bpos = rs->bp[i];
+                    bool al = true;
+                    for (uint32_t k = 0; k < nk; ++k)
+                      if (rs->ka[k] == qa && rs->kb[k] == qb && rs->kp[k] > bpos) al = false;
+                    if (al) alive |= 1u << m;
+                  }
+                }
+                wave_sync();
+                // 2. compact the survivors in place (row ballots keep birth order)
+                uint32_t ns = 0;
+                for (uint32_t m = 0; m * G < nbth; ++m) {
+                  const uint32_t i = sl + m * G;
+                  const bool al = i < nbth && ((alive >> m) & 1u);
+                  uint64_t xa = 0, xb = 0;
+                  if (al) xa = rs->ba[i], xb = rs->bb[i];
+                  const uint32_t rm = (uint32_t)((__ballot(al) >> (row * G)) & 0xFFFFu);
+                  wave_sync();
+                  if (al) {
+                    const uint32_t o_ = ns + (uint32_t)__popc(rm & ((1u << sl) - 1u));
+                    rs->ba[o_] = xa, rs->bb[o_] = xb;
+                  }
+                  ns += (uint32_t)__popc(rm);
+                  wave_sync();
+                }
+                // 3. duplicate flags (the state is a set: keep first occurrences)
+                for (uint32_t i = sl; i < ns; i += G) {
+                  const uint64_t xa = rs->ba[i], xb = rs->bb[i];
+                  int32_t dup = 0;
+                  for (uint32_t k = 0; k < i; ++k)
+                    if (rs->ba[k] == xa && rs->bb[k] == xb) dup = 1;
+                  rs->bp[i] = dup;
+                  if (!dup) atomicAdd(&rs->ctr[2], 1u);
+                }
+                wave_sync();
+                // 4. rank among distinct pairs = output slot (sorted by (a, b))
+                const uint32_t ndist = rs->ctr[2];
+                const uint64_t ooff = R.value.set_off[rj], ocap = R.value.set_off[rj + 1] - ooff;
+                for (uint32_t i = sl; i < ns; i += G) {
+                  if (rs->bp[i]) continue;
+                  const uint64_t xa = rs->ba[i], xb = rs->bb[i];
+                  uint32_t rank = 0;
+                  for (uint32_t k = 0; k < ns; ++k) {
+                    const uint64_t ya = rs->ba[k], yb = rs->bb[k];
+                    if (!rs->bp[k] && (ya < xa || (ya == xa && yb < xb))) ++rank;
+                  }
+                  if (rank < ocap) R.value.set_a[ooff + rank] = xa, R.value.set_b[ooff + rank] = xb;
+                }
+                if (ndist > ocap) status = AM_ERR_CAPACITY;
+                setlen = ndist;
+              }
+            }
+            // NewLastOp: id of the oldest excluded candidate - 1, else get_first_id/1
+            const uint64_t nops = o1 - o0;
+            const uint64_t idb = L.key_id_base ? L.key_id_base[keyj] : 1;
+            int64_t nlo;
+            if (min_excl != NONE)
+              nlo = ((GENERAL && L.op_id) ? (int64_t)L.op_id[min_excl] : (int64_t)(idb + (min_excl - o0))) - 1;
+            else if (nops == 0)
+              nlo = 0;
+            else
+              nlo = (GENERAL && L.op_id) ? (int64_t)L.op_id[o1 - 1] : (int64_t)(idb + nops - 1);
+            const bool ign = u.base_ignore && count == 0;
+            const uint32_t opres = ign ? 0u : (pres | u.cpres);
+            if (defer && sl == 0) C.list[atomicAdd(C.count, 1u)] = (uint32_t)rj;
+            if (lane == j) {
+              o.store = defer ? 0u : 1u;
+              o.status = status;
+              o.flags = flags & 0xFFu;
+              o.count = count;
+              o.pres = opres;
+              o.ign = ign ? 1 : 0;
+              o.newss = count > 0;
+              o.nlo = nlo;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                const uint64_t m = mx[d] > u.C0[d] ? mx[d] : u.C0[d];
+                o.ct[d] = ((opres >> d) & 1u) ? m : 0;
+              }
+              o.v0 = v0, o.v1 = v1, o.vflag = vflag, o.setlen = setlen;
+            }
+            a.reset();
+            v.reset();
+            rowbits &= ~(1u << s);
+            s = rowbits ? (uint32_t)__builtin_ctz(rowbits) : 16u;
+          }
+          wave_sync();
+          begin(fin);
+        }
+      }
+    }
+    // ---- the batch's results: one coalesced store per column ----
+    if (lane < nb && o.store) {
+      R.status[r] = o.status;
+      if (o.status == AM_OK) {
+        R.flags[r] = (uint8_t)o.flags;
+        R.new_last_op[r] = o.nlo;
+        R.last_ct_ignore[r] = (uint8_t)o.ign;
+        R.last_ct_pres[r] = o.pres;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          if (d < (int)nd) R.last_ct[(uint64_t)d * n + r] = o.ct[d];
+        R.is_new_ss[r] = (uint8_t)o.newss;
+        R.count[r] = o.count;
+        if (TYPE == AM_PN || TYPE == AM_LWW) R.value.v0[r] = (int64_t)o.v0;
+        if (TYPE == AM_LWW) {
+          R.value.v1[r] = o.v1;
+          R.value.vflag[r] = (uint8_t)o.vflag;
+        }
+        if (SETS) R.value.set_len[r] = o.setlen;
+      }
+    }
+  }
+}
+
+template <int D, int TYPE, bool GENERAL, bool PACKED>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+             const am_rows_cfg &C) {
+  constexpr bool LDS = TYPE == AM_AWSET || TYPE == AM_MVREG || TYPE == AM_BCOUNTER;
+  const size_t smem = LDS ? sizeof(RowSmem) * (BLOCK / G) : 0;
+  static int occ = 0;
+  if (occ == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rows<D, TYPE, GENERAL, PACKED>, BLOCK, smem) != hipSuccess ||
+        nb <= 0)
+      nb = 2;
+    occ = nb;
+  }
+  const uint64_t batches = (B->n_reads + WAVE - 1) / WAVE;
+  uint64_t blocks = (batches + WPB - 1) / WPB;
+  const uint64_t cap = (uint64_t)ctx->n_cu * (uint64_t)occ;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return AM_OK;
+  hipLaunchKernelGGL((k_rows<D, TYPE, GENERAL, PACKED>), dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, *B,
+                     *R, S, C);
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
+template <int TYPE, bool GENERAL, bool PACKED>
+int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+           const am_rows_cfg &C) {
+  const uint32_t nd = L->n_dc;
+  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, C);
+}
+
+template <int TYPE>
+int launch_t(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+             const am_rows_cfg &C) {
+  const bool general = am_batch_general(L, B);
+  const bool packed = am_log_packed(L);
+  if (general) return packed ? launch<TYPE, true, true>(ctx, L, B, R, S, C) : launch<TYPE, true, false>(ctx, L, B, R, S, C);
+  return packed ? launch<TYPE, false, true>(ctx, L, B, R, S, C) : launch<TYPE, false, false>(ctx, L, B, R, S, C);
+}
+
+}  // namespace
+
+int am_launch_rows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
+                   const am_rows_cfg &C) {
+  switch (type) {
+    case AM_PN: return launch_t<AM_PN>(ctx, L, B, R, S, C);
+    case AM_LWW: return launch_t<AM_LWW>(ctx, L, B, R, S, C);
+    case AM_AWSET: return launch_t<AM_AWSET>(ctx, L, B, R, S, C);
+    case AM_MVREG: return launch_t<AM_MVREG>(ctx, L, B, R, S, C);
+    case AM_BCOUNTER: return launch_t<AM_BCOUNTER>(ctx, L, B, R, S, C);
+    default: return AM_ERR_UNSUPPORTED;
+  }
+}

@@ -57,7 +57,8 @@ struct Out {
 };
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
-__global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, am_read_result R, am_sel S) {
+__global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                  int64_t skip_le) {
   using V = typename ValOf<TYPE>::T;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint64_t n = B.n_reads;  // column stride of per-read arrays
@@ -92,12 +93,12 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   struct Meta {
     uint64_t key, off0, off1, rb, r;  // rb: first slot of the batch; r: lane's read index
     int32_t st;
-    uint32_t nb;
+    uint32_t nb, skip;  // skip: the row tier (am_rows.hip) owns this read
   };
   auto load_meta = [&](uint64_t bid, Meta &M) {
     M.rb = bid * WAVE;
     M.nb = bid < n_batches ? (uint32_t)(nsel - M.rb < (uint64_t)WAVE ? nsel - M.rb : (uint64_t)WAVE) : 0u;
-    M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK, M.r = 0;
+    M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK, M.r = 0, M.skip = 0;
     if (lane < M.nb) {
       const uint64_t r = sbase ? (uint64_t)sbase[M.rb + lane] : M.rb + lane;
       M.r = r;
@@ -117,6 +118,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
           M.st = AM_ERR_INVALID;              // batch type_hint violated
       }
       if (M.st != AM_OK) M.off1 = M.off0;     // no tiles to stream
+      if (skip_le >= 0 && (int64_t)(M.off1 - M.off0) <= skip_le) M.skip = 1, M.off1 = M.off0;
     }
   };
 
@@ -157,7 +159,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   };
   // the batch's results: one coalesced store per column
   auto store_out = [&](const Meta &M) {
-    if (lane < M.nb) {
+    if (lane < M.nb && !M.skip) {
       const uint64_t r = M.r;
       R.status[r] = o.status;
       if (o.status == AM_OK) {
@@ -398,7 +400,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
 }
 
 template <int D, int TYPE, bool GENERAL, bool PACKED>
-int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S) {
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, int64_t skip_le) {
   // persistent-style grid: at most the resident capacity, at most one wave per 64-read batch
   static int occ = 0;
   if (occ == 0) {
@@ -414,21 +416,21 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
   hipLaunchKernelGGL((k_stream<D, TYPE, GENERAL, PACKED>), dim3((unsigned)blocks), dim3(BLOCK), 0, ctx->stream, *L, *B,
-                     *R, S);
+                     *R, S, skip_le);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }
 
 template <int TYPE, bool GENERAL, bool PACKED>
-int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S) {
+int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, int64_t skip_le) {
   const uint32_t nd = L->n_dc;
-  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
-  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
-  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
-  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
-  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
-  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
-  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S);
+  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
 }
 
 }  // namespace
@@ -437,22 +439,30 @@ int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_resu
 // ids, TxIds, cached bases, per-read clocks (the bench's fresh snapshot read).
 // With a selection (planner sub-batch) the read count lives on the device: the grid is
 // the resident capacity and surplus waves exit at once.
-int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                     uint32_t type) {
-  const bool general = L->snap_pres || L->op_id || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock ||
-                       B->base.v0;
+int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                          uint32_t type, int64_t skip_le) {
+  const bool general = am_batch_general(L, B);
   // packed view: streaming bytes per op 8 + 4*D + payload instead of 9 + 8*D + payload
-  const char *pv = getenv("AM_PACKED");
-  const bool packed = L->ct_meta && L->snap_delta && !L->snap_pres && !(pv && pv[0] == '0');
+  const bool packed = am_log_packed(L);
   switch (type) {
     case AM_PN:
-      if (general) return packed ? launch<AM_PN, true, true>(ctx, L, B, R, S) : launch<AM_PN, true, false>(ctx, L, B, R, S);
-      return packed ? launch<AM_PN, false, true>(ctx, L, B, R, S) : launch<AM_PN, false, false>(ctx, L, B, R, S);
+      if (general)
+        return packed ? launch<AM_PN, true, true>(ctx, L, B, R, S, skip_le)
+                      : launch<AM_PN, true, false>(ctx, L, B, R, S, skip_le);
+      return packed ? launch<AM_PN, false, true>(ctx, L, B, R, S, skip_le)
+                    : launch<AM_PN, false, false>(ctx, L, B, R, S, skip_le);
     case AM_LWW:
       if (general)
-        return packed ? launch<AM_LWW, true, true>(ctx, L, B, R, S) : launch<AM_LWW, true, false>(ctx, L, B, R, S);
-      return packed ? launch<AM_LWW, false, true>(ctx, L, B, R, S) : launch<AM_LWW, false, false>(ctx, L, B, R, S);
+        return packed ? launch<AM_LWW, true, true>(ctx, L, B, R, S, skip_le)
+                      : launch<AM_LWW, true, false>(ctx, L, B, R, S, skip_le);
+      return packed ? launch<AM_LWW, false, true>(ctx, L, B, R, S, skip_le)
+                    : launch<AM_LWW, false, false>(ctx, L, B, R, S, skip_le);
     default:
       return AM_ERR_UNSUPPORTED;
   }
+}
+
+int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                     uint32_t type) {
+  return am_launch_stream_skip(ctx, L, B, R, S, type, -1);
 }
