@@ -83,17 +83,20 @@ int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.h
 // materialized by one 16-lane row each.  list/count (set types only): reads the tier
 // leaves to the workgroup tier -- longer logs, and reads whose births/kills overflow
 // the row's LDS lists -- appended in batch order (count lives on the device).
+// mask (PN/LWW): per 64-read batch of the selection, the reads k_stream left to the row
+// tier (bit i = read rb + i); k_stream writes it, the row tier skips batches with 0.
 struct am_rows_cfg {
   uint32_t short_max = 0;
   uint32_t *list = nullptr;
   uint32_t *count = nullptr;
+  uint64_t *mask = nullptr;
 };
 int am_launch_rows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
                    const am_rows_cfg &C);
-// k_stream skips the reads the row tier took (len <= skip_le or an error status) when
-// skip_le >= 0
+// k_stream with H.mask set: reads with at most H.short_max ops (and error reads) are
+// not materialized but marked in H.mask for the row tier
 int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                          uint32_t type, int64_t skip_le);
+                          uint32_t type, const am_rows_cfg &H);
 // the batch uses partial clocks, op ids, TxIds, cached bases or per-read clocks
 inline bool am_batch_general(const am_op_log *L, const am_read_batch *B) {
   return L->snap_pres || L->op_id || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock || B->base.v0 ||

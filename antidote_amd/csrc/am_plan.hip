@@ -134,15 +134,18 @@ uint32_t rows_max(bool set) {
   return m;
 }
 
-// PN / LWW over selection S: short reads on the row tier, the rest on k_stream.
-int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type) {
+// PN / LWW over selection S: k_stream takes the long reads and marks the short ones in a
+// per-batch mask (rows_buf + 64) for the row tier, which skips batches without any.
+int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
+               uint32_t *rows_buf) {
   const uint32_t m = rows_max(false);
-  if (m == 0) return am_launch_stream_skip(ctx, L, B, R, S, type, -1);
-  am_rows_cfg C;
-  C.short_max = m;
-  int rc = am_launch_rows(ctx, L, B, R, S, type, C);
+  if (m == 0) return am_launch_stream_skip(ctx, L, B, R, S, type, am_rows_cfg{});
+  am_rows_cfg H;
+  H.short_max = m;
+  H.mask = (uint64_t *)(rows_buf + 64);
+  int rc = am_launch_stream_skip(ctx, L, B, R, S, type, H);
   if (rc) return rc;
-  return am_launch_stream_skip(ctx, L, B, R, S, type, (int64_t)m);
+  return am_launch_rows(ctx, L, B, R, S, type, H);
 }
 
 // Set types over selection S: row tier -> (hand-off list) workgroup tier k_sets ->
@@ -199,12 +202,13 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   if (variant && strcmp(variant, "scalar") == 0 && B->type_hint <= AM_LWW) return am_launch_scalar(ctx, L, B, R);
 
   const am_sel all{};
-  if (B->type_hint == AM_PN || B->type_hint == AM_LWW) return run_scalar(ctx, L, B, R, all, B->type_hint);
   void *rows_scr = nullptr;
-  if (B->type_hint != AM_PN && B->type_hint != AM_LWW) {
+  {
     int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
     if (rc) return rc;
   }
+  if (B->type_hint == AM_PN || B->type_hint == AM_LWW)
+    return run_scalar(ctx, L, B, R, all, B->type_hint, (uint32_t *)rows_scr);
   if (B->type_hint == AM_AWSET || B->type_hint == AM_MVREG || B->type_hint == AM_BCOUNTER) {
     void *scr = nullptr;
     int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &scr);
@@ -238,7 +242,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     S.idx = idx;
     S.range = range + 2 * (t - 1);
     if (t == AM_PN || t == AM_LWW)
-      rc = run_scalar(ctx, L, B, R, S, t);
+      rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
     else
       rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr);
     if (rc) return rc;

@@ -194,9 +194,11 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
     // ---- batch metadata: lane i <-> read rb + i ----
     const uint64_t rb = bid * WAVE;
     const uint32_t nb = (uint32_t)(nsel - rb < (uint64_t)WAVE ? nsel - rb : (uint64_t)WAVE);
+    const uint64_t bmask = C.mask ? uniform_u64(C.mask[bid]) : ~0ull;  // k_stream's hand-off
+    if (!bmask) continue;
     uint64_t key = 0, off0 = 0, off1 = 0, r = 0;
     int32_t st = AM_OK;
-    if (lane < nb) {
+    if (lane < nb && ((bmask >> lane) & 1u)) {
       r = sbase ? (uint64_t)sbase[rb + lane] : rb + lane;
       key = B.key[r];
       const uint32_t rtype = B.type[r];
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
       if (st != AM_OK) off1 = off0;
     }
     const uint64_t len = off1 - off0;
-    const bool mine = lane < nb && len <= C.short_max;  // error reads have len 0
+    const bool mine = lane < nb && ((bmask >> lane) & 1u) && len <= C.short_max;  // error reads have len 0
     // set types: long reads go to the workgroup tier through the ordered list
     if (C.list) {
       const bool hand = lane < nb && !mine;
@@ -310,42 +312,78 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         }
       };
       begin(true);
+      // one op's streamed columns, loaded one step ahead of their use
+      struct ROp {
+        uint64_t w;         // packed: ct_meta; full: commit_time
+        uint32_t meta, sp;  // full: op_meta; snapshot presence
+        int32_t sd[DMAX];   // packed: commit_time - snapshot entry
+        uint64_t sv[DMAX];  // full: snapshot entries
+        uint64_t tx, p0, p1;
+      };
+      auto load_op = [&](ROp &q, uint64_t p, bool valid) {
+        if (!valid) return;
+        if (PACKED) {
+          q.w = L.ct_meta[p];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) q.sd[d] = d < (int)nd ? L.snap_delta[(uint64_t)d * stride + p] : 0;
+        } else {
+          q.meta = L.op_meta[p];
+          q.w = L.commit_time[p];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) q.sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+        }
+        q.sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : allmask;
+        q.tx = (GENERAL && u.has_txid) ? L.op_txid[p] : 0;
+        if (TYPE != AM_AWSET) q.p0 = L.p0[p];
+        if (TYPE != AM_AWSET && TYPE != AM_PN) q.p1 = L.p1[p];
+      };
+      ROp cur, nxt;
+      load_op(cur, o0 + sl, s < 16 && o0 + sl < o1);
       while (__ballot(s < 16)) {
         const bool act = s < 16;
         const uint64_t p = o0 + t + sl;
+        const bool fin_next = act && o0 + t + G >= o1;
+        {  // prefetch the next step: this read at t + G, or the row's next read
+          const uint32_t rest = act ? (rowbits & ~(1u << s)) : 0u;
+          const uint32_t s2 = rest ? (uint32_t)__builtin_ctz(rest) : 16u;
+          const uint32_t j2 = row * G + (s2 < 16 ? s2 : 0);
+          const uint64_t n0 = shfl_u64(off0, j2), n1 = shfl_u64(off1, j2);
+          if (fin_next) load_op(nxt, n0 + sl, s2 < 16 && n0 + sl < n1);
+          else load_op(nxt, p + G, act && p + G < o1);
+        }
         if (act && p < o1) {
           // ---- one op: is_op_in_snapshot/7 + the type's effect ----
-          uint32_t meta = 0;
-          uint64_t ct = 0, sv[DMAX];
-          bool packed_ok = false;
+          uint32_t meta;
+          uint64_t ct, sv[DMAX];
           if (PACKED) {
-            const uint64_t w = L.ct_meta[p];
-            meta = (uint32_t)(w >> 56);
-            if (!(w & AM_CT_ESC)) {
-              ct = w & (AM_CT_ESC - 1);
+            meta = (uint32_t)(cur.w >> 56);
+            if (!(cur.w & AM_CT_ESC)) {
+              ct = cur.w & (AM_CT_ESC - 1);
 #pragma unroll
-              for (int d = 0; d < DMAX; ++d)
-                sv[d] = d < (int)nd ? ct - (uint64_t)(int64_t)L.snap_delta[(uint64_t)d * stride + p] : 0;
-              packed_ok = true;
+              for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? ct - (uint64_t)(int64_t)cur.sd[d] : 0;
+            } else {  // rare: the op does not fit the packed view
+              ct = L.commit_time[p];
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
             }
-          }
-          if (!packed_ok) {
-            if (!PACKED) meta = L.op_meta[p];
-            ct = L.commit_time[p];
+          } else {
+            meta = cur.meta;
+            ct = cur.w;
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+            for (int d = 0; d < DMAX; ++d) sv[d] = cur.sv[d];
           }
-          const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : allmask;
-          const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
-          if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, sp, txm, p, a) && !(LDS && (meta & AM_META_BAD))) {
+          const bool txm = GENERAL && u.has_txid && cur.tx == u.txid;
+          if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, cur.sp, txm, p, a) && !(LDS && (meta & AM_META_BAD))) {
             if constexpr (TYPE == AM_PN || TYPE == AM_LWW) {
-              v.add(L.p0[p], TYPE == AM_LWW ? L.p1[p] : 0);
+              v.add(cur.p0, TYPE == AM_LWW ? cur.p1 : 0);
             } else if constexpr (BC) {
-              uint32_t slot;
-              int64_t amt;
-              if (bc_slot(L, p, meta, nd, slot, amt)) {
+              const uint32_t kind = AM_META_KIND(meta);
+              const uint32_t from = (uint32_t)(cur.p1 & 0xFF), to = (uint32_t)((cur.p1 >> 8) & 0xFF);
+              if (kind <= AM_BC_TRANSFER && from < nd && to < nd) {
+                const uint32_t slot =
+                    kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
                 const uint32_t e = atomicAdd(&rs->ctr[0], 1u);
-                if (e < RK) rs->ka[e] = (uint64_t)amt, rs->kp[e] = (int32_t)slot;
+                if (e < RK) rs->ka[e] = cur.p0, rs->kp[e] = (int32_t)slot;
                 else rs->ctr[3] = 1;
               } else {
                 a.flags |= FLAG_BAD;
@@ -545,6 +583,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
           wave_sync();
           begin(fin);
         }
+        cur = nxt;
       }
     }
     // ---- the batch's results: one coalesced store per column ----

@@ -58,7 +58,7 @@ struct Out {
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
-                                                  int64_t skip_le) {
+                                                  am_rows_cfg H) {
   using V = typename ValOf<TYPE>::T;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint64_t n = B.n_reads;  // column stride of per-read arrays
@@ -118,7 +118,11 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
           M.st = AM_ERR_INVALID;              // batch type_hint violated
       }
       if (M.st != AM_OK) M.off1 = M.off0;     // no tiles to stream
-      if (skip_le >= 0 && (int64_t)(M.off1 - M.off0) <= skip_le) M.skip = 1, M.off1 = M.off0;
+      if (H.mask && M.off1 - M.off0 <= (uint64_t)H.short_max) M.skip = 1, M.off1 = M.off0;
+    }
+    if (H.mask && bid < n_batches) {  // hand short (and error) reads to the row tier
+      const uint64_t hm = __ballot(M.skip != 0);
+      if (lane == 0) H.mask[bid] = hm;
     }
   };
 
@@ -400,7 +404,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
 }
 
 template <int D, int TYPE, bool GENERAL, bool PACKED>
-int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, int64_t skip_le) {
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, const am_rows_cfg &H) {
   // persistent-style grid: at most the resident capacity, at most one wave per 64-read batch
   static int occ = 0;
   if (occ == 0) {
@@ -416,21 +420,21 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
   hipLaunchKernelGGL((k_stream<D, TYPE, GENERAL, PACKED>), dim3((unsigned)blocks), dim3(BLOCK), 0, ctx->stream, *L, *B,
-                     *R, S, skip_le);
+                     *R, S, H);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }
 
 template <int TYPE, bool GENERAL, bool PACKED>
-int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, int64_t skip_le) {
+int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, const am_rows_cfg &H) {
   const uint32_t nd = L->n_dc;
-  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
-  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
-  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
-  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
-  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
-  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
-  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, skip_le);
+  if (nd <= 1) return launch_d<1, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
+  if (nd <= 2) return launch_d<2, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
+  if (nd <= 3) return launch_d<3, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
+  if (nd <= 4) return launch_d<4, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
+  if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
+  if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
+  return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
 }
 
 }  // namespace
@@ -440,23 +444,23 @@ int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_resu
 // With a selection (planner sub-batch) the read count lives on the device: the grid is
 // the resident capacity and surplus waves exit at once.
 int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                          uint32_t type, int64_t skip_le) {
+                          uint32_t type, const am_rows_cfg &H) {
   const bool general = am_batch_general(L, B);
   // packed view: streaming bytes per op 8 + 4*D + payload instead of 9 + 8*D + payload
   const bool packed = am_log_packed(L);
   switch (type) {
     case AM_PN:
       if (general)
-        return packed ? launch<AM_PN, true, true>(ctx, L, B, R, S, skip_le)
-                      : launch<AM_PN, true, false>(ctx, L, B, R, S, skip_le);
-      return packed ? launch<AM_PN, false, true>(ctx, L, B, R, S, skip_le)
-                    : launch<AM_PN, false, false>(ctx, L, B, R, S, skip_le);
+        return packed ? launch<AM_PN, true, true>(ctx, L, B, R, S, H)
+                      : launch<AM_PN, true, false>(ctx, L, B, R, S, H);
+      return packed ? launch<AM_PN, false, true>(ctx, L, B, R, S, H)
+                    : launch<AM_PN, false, false>(ctx, L, B, R, S, H);
     case AM_LWW:
       if (general)
-        return packed ? launch<AM_LWW, true, true>(ctx, L, B, R, S, skip_le)
-                      : launch<AM_LWW, true, false>(ctx, L, B, R, S, skip_le);
-      return packed ? launch<AM_LWW, false, true>(ctx, L, B, R, S, skip_le)
-                    : launch<AM_LWW, false, false>(ctx, L, B, R, S, skip_le);
+        return packed ? launch<AM_LWW, true, true>(ctx, L, B, R, S, H)
+                      : launch<AM_LWW, true, false>(ctx, L, B, R, S, H);
+      return packed ? launch<AM_LWW, false, true>(ctx, L, B, R, S, H)
+                    : launch<AM_LWW, false, false>(ctx, L, B, R, S, H);
     default:
       return AM_ERR_UNSUPPORTED;
   }
@@ -464,5 +468,5 @@ int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *
 
 int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                      uint32_t type) {
-  return am_launch_stream_skip(ctx, L, B, R, S, type, -1);
+  return am_launch_stream_skip(ctx, L, B, R, S, type, am_rows_cfg{});
 }
