@@ -3,7 +3,19 @@
 // needs each snapshot entry relative to the op's own commit time, which fits in 32
 // bits for any realistic clock lag/skew (2^31 us = 35 min).  Ops that do not fit are
 // flagged (AM_CT_ESC) and read from the full columns, so results stay bit-exact.
-#include "am_internal.h"
+//
+// The record view (am_op_log.rec_*) flattens the add-wins-set / MV-register effects of
+// every op into (a, b, meta) records, a key's records contiguous in op order, so the set
+// kernels stream effects like any other column instead of chasing var_off -> var_data:
+//   k_op_key_mark + inclusive max-scan   op -> key
+//   k_rec_count + exclusive scan         per-op record counts -> record offsets
+//   k_rec_fill                           records (malformed effects: AM_META_BAD in ct_meta)
+//   k_rec_key_off                        per-key record ranges
+#include <hipcub/hipcub.hpp>
+
+#include "am_block.h"
+
+using namespace amk;
 
 namespace {
 
@@ -36,6 +48,148 @@ __global__ void k_pack(am_op_log L, uint64_t *ct_meta, int32_t *snap_delta) {
   }
 }
 
+// op -> key: the first op of every non-empty key gets the key index; an inclusive
+// max-scan spreads it over the key's ops
+__global__ void k_op_key_mark(const uint64_t *key_off, uint64_t n_keys, uint32_t *okey) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_keys; k += (uint64_t)gridDim.x * blockDim.x)
+    if (key_off[k] < key_off[k + 1]) okey[key_off[k]] = (uint32_t)k;
+}
+
+struct CountSink {
+  uint32_t n = 0;
+  __device__ void births(uint64_t, const uint64_t *, uint32_t c, int32_t) { n += c; }
+  __device__ void birth(uint64_t, uint64_t, int32_t) { n += 1; }
+  __device__ void kills(const uint64_t *, uint32_t c, uint64_t, int32_t) { n += c; }
+};
+struct FillSink {
+  uint64_t *ra, *rb;
+  uint32_t *rm;
+  uint64_t o;
+  uint32_t opi;
+  __device__ void births(uint64_t e, const uint64_t *tok, uint32_t c, int32_t) {
+    for (uint32_t i = 0; i < c; ++i, ++o) ra[o] = e, rb[o] = tok[i], rm[o] = opi;
+  }
+  __device__ void birth(uint64_t a, uint64_t b, int32_t) { ra[o] = a, rb[o] = b, rm[o] = opi, ++o; }
+  __device__ void kills(const uint64_t *tok, uint32_t c, uint64_t e, int32_t) {
+    for (uint32_t i = 0; i < c; ++i, ++o) ra[o] = e, rb[o] = tok[i], rm[o] = opi | AM_REC_KILL;
+  }
+};
+
+template <class Sink>
+__device__ __forceinline__ bool op_effects(const am_op_log &L, uint64_t p, uint32_t type, uint32_t meta, Sink &sk) {
+  if (type == AM_AWSET) return set_effects<AM_AWSET>(L, p, meta, 0, sk);
+  return set_effects<AM_MVREG>(L, p, meta, 0, sk);
+}
+
+__global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, uint64_t *ct_meta) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < L.n_ops; p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t type = L.key_type[okey[p]];
+    const uint32_t meta = L.op_meta[p];
+    uint64_t c = 0;
+    if ((type == AM_AWSET || type == AM_MVREG) && !(meta & AM_META_BAD)) {
+      CountSink cs;
+      if (op_effects(L, p, type, meta, cs)) c = cs.n;
+      else ct_meta[p] |= (uint64_t)AM_META_BAD << 56;  // Type:update/2 raises on this effect
+    }
+    cnt[p] = c;
+  }
+}
+
+__global__ void k_rec_fill(am_op_log L, const uint32_t *okey, const uint64_t *off, const uint64_t *ct_meta,
+                           uint64_t *ra, uint64_t *rb, uint32_t *rm) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < L.n_ops; p += (uint64_t)gridDim.x * blockDim.x) {
+    if (off[p + 1] == off[p] || ((ct_meta[p] >> 56) & AM_META_BAD)) continue;
+    const uint32_t k = okey[p];
+    FillSink fs{ra, rb, rm, off[p], (uint32_t)(p - L.key_off[k])};
+    op_effects(L, p, L.key_type[k], L.op_meta[p], fs);
+  }
+}
+
+__global__ void k_rec_key_off(const uint64_t *key_off, uint64_t n_keys, const uint64_t *off, uint64_t *rko) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= n_keys; k += (uint64_t)gridDim.x * blockDim.x)
+    rko[k] = off[key_off[k]];
+}
+
+struct MaxOp {
+  __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+
+unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536); }
+
+// builds the record view of a packed store (no-op for logs without set payloads)
+int build_records(am_store *st) {
+  am_ctx *c = st->ctx;
+  am_op_log &d = st->dev;
+  if (!d.var_off || !d.ct_meta || d.n_ops == 0 || d.n_ops > 0xFFFFFFFFull) return AM_OK;
+  const uint64_t n = d.n_ops;
+  uint32_t *okey = nullptr;
+  uint64_t *cnt = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_b = 0, t2 = 0;
+  int rc = AM_OK;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(c->stream);
+    if (okey) (void)hipFree(okey);
+    if (cnt) (void)hipFree(cnt);
+    if (tmp) (void)hipFree(tmp);
+  };
+  if (hipcub::DeviceScan::InclusiveScan(nullptr, tmp_b, okey, okey, MaxOp(), n, c->stream) != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cnt, cnt, n + 1, c->stream) != hipSuccess) {
+    am_set_error("record view: scan sizing failed");
+    return AM_ERR_HIP;
+  }
+  if (t2 > tmp_b) tmp_b = t2;
+  if (hipMalloc((void **)&okey, n * 4) != hipSuccess || hipMalloc((void **)&cnt, (n + 1) * 8) != hipSuccess ||
+      hipMalloc(&tmp, tmp_b + 16) != hipSuccess) {
+    cleanup();
+    am_set_error("record view: out of device memory");
+    return AM_ERR_NOMEM;
+  }
+  uint64_t n_rec = 0;
+  do {
+    if (hipMemsetAsync(okey, 0, n * 4, c->stream) != hipSuccess) break;
+    if (hipMemsetAsync(cnt + n, 0, 8, c->stream) != hipSuccess) break;
+    hipLaunchKernelGGL(k_op_key_mark, dim3(grid_of(d.n_keys)), dim3(256), 0, c->stream, d.key_off, d.n_keys, okey);
+    if (hipcub::DeviceScan::InclusiveScan(tmp, tmp_b, okey, okey, MaxOp(), n, c->stream) != hipSuccess) break;
+    hipLaunchKernelGGL(k_rec_count, dim3(grid_of(n)), dim3(256), 0, c->stream, d, okey, cnt,
+                       const_cast<uint64_t *>(d.ct_meta));
+    if (hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, cnt, cnt, n + 1, c->stream) != hipSuccess) break;
+    if (hipMemcpyAsync(&n_rec, cnt + n, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) break;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) break;
+    rc = -1;
+  } while (0);
+  if (rc != -1) {
+    cleanup();
+    am_set_error("record view: count pass failed");
+    return AM_ERR_HIP;
+  }
+  rc = AM_OK;
+  void *rko = nullptr, *ra = nullptr, *rb = nullptr, *rm = nullptr;
+  rc = am_dev_alloc(c, (d.n_keys + 1) * 8, &rko);
+  if (!rc) st->allocs.push_back(rko), rc = am_dev_alloc(c, (n_rec + 4) * 8, &ra);
+  if (!rc) st->allocs.push_back(ra), rc = am_dev_alloc(c, (n_rec + 4) * 8, &rb);
+  if (!rc) st->allocs.push_back(rb), rc = am_dev_alloc(c, (n_rec + 4) * 4, &rm);
+  if (!rc) st->allocs.push_back(rm);
+  if (!rc) {
+    hipLaunchKernelGGL(k_rec_fill, dim3(grid_of(n)), dim3(256), 0, c->stream, d, okey, cnt, d.ct_meta, (uint64_t *)ra,
+                       (uint64_t *)rb, (uint32_t *)rm);
+    hipLaunchKernelGGL(k_rec_key_off, dim3(grid_of(d.n_keys + 1)), dim3(256), 0, c->stream, d.key_off, d.n_keys, cnt,
+                       (uint64_t *)rko);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+      am_set_error("record view: fill pass failed");
+      rc = AM_ERR_HIP;
+    }
+  }
+  cleanup();
+  if (rc) return rc;
+  d.n_rec = n_rec;
+  d.rec_key_off = (const uint64_t *)rko;
+  d.rec_a = (const uint64_t *)ra;
+  d.rec_b = (const uint64_t *)rb;
+  d.rec_meta = (const uint32_t *)rm;
+  return AM_OK;
+}
+
 }  // namespace
 
 int am_store_pack(am_store *st) {
@@ -60,5 +214,7 @@ int am_store_pack(am_store *st) {
   AM_HIP(hipStreamSynchronize(c->stream));
   d.ct_meta = (const uint64_t *)ctm;
   d.snap_delta = (const int32_t *)sd;
-  return AM_OK;
+  const char *rv = getenv("AM_RECORDS");
+  if (rv && rv[0] == '0') return AM_OK;
+  return build_records(st);
 }

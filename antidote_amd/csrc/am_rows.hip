@@ -159,6 +159,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
   constexpr bool SETS = TYPE == AM_AWSET || TYPE == AM_MVREG;
   constexpr bool BC = TYPE == AM_BCOUNTER;
   constexpr bool LDS = SETS || BC;
+  constexpr bool REC = SETS && PACKED;  // effects from the record view (am_pack.hip)
   using V = typename RowVal<TYPE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   RowSmem *rs = LDS ? ((RowSmem *)smem_raw) + (threadIdx.x / G) : nullptr;
@@ -263,6 +264,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
       uint32_t s = rowbits ? (uint32_t)__builtin_ctz(rowbits) : 16u;
       // current read of the row (row-uniform values)
       uint64_t o0 = 0, o1 = 0, rj = 0, keyj = 0, t = 0;
+      uint64_t imask = 0, rk0 = 0, rk1 = 0;  // REC: included ops of the read, its record range
       Acc<DMAX> a;
       V v;
       a.reset();
@@ -275,7 +277,9 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         if (!upd) return;
         o0 = n0, o1 = n1, rj = nr, keyj = nk;
         t = 0;
+        imask = 0;
         if (s >= 16) return;
+        if (REC) rk0 = L.rec_key_off[keyj], rk1 = L.rec_key_off[keyj + 1];
         if (GENERAL) {
           if (B.per_read_clock) {
             u.spres = B.read_pres[rj] & allmask;
@@ -351,6 +355,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
           if (fin_next) load_op(nxt, n0 + sl, s2 < 16 && n0 + sl < n1);
           else load_op(nxt, p + G, act && p + G < o1);
         }
+        bool inc = false;  // REC: the op is included (its records apply)
         if (act && p < o1) {
           // ---- one op: is_op_in_snapshot/7 + the type's effect ----
           uint32_t meta;
@@ -388,12 +393,15 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
               } else {
                 a.flags |= FLAG_BAD;
               }
+            } else if constexpr (REC) {
+              inc = true;
             } else {
               RowSink sink{rs};
               if (!set_effects<TYPE>(L, p, meta, (int32_t)(p - o0), sink)) a.flags |= FLAG_BAD;
             }
           }
         }
+        if (REC) imask |= ((__ballot(inc) >> (row * G)) & 0xFFFFull) << t;
         t += G;
         const bool fin = act && o0 + t >= o1;
         if (__ballot(fin)) {
@@ -486,6 +494,23 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                 }
               }
             } else {  // add-wins set / MV register
+              if (REC && status == AM_OK) {  // the included ops' records -> births / kills
+                for (uint64_t q = rk0 + sl; q < rk1; q += G) {
+                  const uint32_t m = L.rec_meta[q];
+                  if (!((imask >> AM_REC_OP(m)) & 1u)) continue;
+                  const uint64_t ra = L.rec_a[q], rb = L.rec_b[q];
+                  if (m & AM_REC_KILL) {
+                    const uint32_t ki = atomicAdd(&rs->ctr[0], 1u);
+                    if (ki < RK) rs->ka[ki] = rb, rs->kb[ki] = ra, rs->kp[ki] = (int32_t)AM_REC_OP(m);
+                    else rs->ctr[3] = 1;
+                  } else {
+                    const uint32_t bi = atomicAdd(&rs->ctr[1], 1u);
+                    if (bi < RB) rs->ba[bi] = ra, rs->bb[bi] = rb, rs->bp[bi] = (int32_t)AM_REC_OP(m);
+                    else rs->ctr[3] = 1;
+                  }
+                }
+                wave_sync();
+              }
               if (status == AM_OK && rs->ctr[3]) defer = true;
               if (status == AM_OK && !defer) {
                 const uint32_t nk = rs->ctr[0], nbth = rs->ctr[1];
@@ -651,7 +676,8 @@ template <int TYPE>
 int launch_t(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
              const am_rows_cfg &C) {
   const bool general = am_batch_general(L, B);
-  const bool packed = am_log_packed(L);
+  // set types take the packed view only together with the record view
+  const bool packed = am_log_packed(L) && ((TYPE != AM_AWSET && TYPE != AM_MVREG) || L->rec_key_off);
   if (general) return packed ? launch<TYPE, true, true>(ctx, L, B, R, S, C) : launch<TYPE, true, false>(ctx, L, B, R, S, C);
   return packed ? launch<TYPE, false, true>(ctx, L, B, R, S, C) : launch<TYPE, false, false>(ctx, L, B, R, S, C);
 }

@@ -136,7 +136,23 @@ typedef struct am_op_log {
    * read that op from the full columns above.  Cuts C2 from 49 to 36 B/op. */
   const uint64_t *ct_meta;     /* [n_ops]                                            */
   const int32_t *snap_delta;   /* [n_dc][snap_stride]                                */
+  /* Set-effect record view (add-wins set and MV register keys), built on the device with
+   * the packed view.  Every effect is flattened to records (a, b, meta), a key's records
+   * contiguous and in op order: [rec_key_off[k], rec_key_off[k+1]).
+   *   AW  add token t of elem e -> birth (e, t);  remove token t of elem e -> kill (e, t)
+   *   MV  overridden token t   -> kill (0, t);   {Value, Token, _}      -> birth (Value, Token)
+   * rec_meta = op index within the key (bits 0-30) | kill << 31.  Ops carrying
+   * AM_META_BAD produce no record; an op whose variable payload is malformed (Type:update/2
+   * would raise) gets AM_META_BAD in its ct_meta meta byte instead of records.  A read
+   * then streams its ops (inclusion) and its records (effects) with no dependent loads. */
+  uint64_t n_rec;
+  const uint64_t *rec_key_off; /* [n_keys+1]                                         */
+  const uint64_t *rec_a;       /* [n_rec]                                            */
+  const uint64_t *rec_b;       /* [n_rec]                                            */
+  const uint32_t *rec_meta;    /* [n_rec]                                            */
 } am_op_log;
+#define AM_REC_KILL (1u << 31)
+#define AM_REC_OP(m) ((m) & 0x7FFFFFFFu)
 #define AM_CT_ESC (1ull << 55)
 
 /*
