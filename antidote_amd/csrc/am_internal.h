@@ -10,13 +10,15 @@
 
 #include "../../include/antidote_mat.h"
 
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_HASH = 4, AM_SCR_HASHX = 5, AM_N_SCR = 6 };
+
 struct am_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int n_cu = 256;
-  void *scratch[4] = {};         // grow-only device scratch slots (planner, big-read path)
-  size_t scratch_bytes[4] = {};
+  void *scratch[AM_N_SCR] = {};  // grow-only device scratch slots (planner, row/hash hand-offs, big-read path)
+  size_t scratch_bytes[AM_N_SCR] = {};
   uint64_t *pinned = nullptr;    // small pinned host buffer for device -> host counters
 };
 
@@ -36,7 +38,6 @@ struct am_retry {
 // scratch slot `slot` (0 planner, 1 big-read metadata, 2 big-read records): at least
 // `bytes` of device memory, valid until the next call for the same slot (stream-ordered
 // reuse; growing synchronizes the stream before freeing the old block)
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3 };
 int am_ctx_scratch(am_ctx *ctx, int slot, size_t bytes, void **out);
 // copy `n` u64 counters device -> host through the pinned buffer (synchronizes the stream)
 int am_ctx_fetch(am_ctx *ctx, const void *dev, uint32_t n_u64, uint64_t *host);
@@ -77,6 +78,12 @@ int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
                    uint32_t type, am_retry retry);
 int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, uint32_t type,
                   am_retry retry);  // am_big.hip: reads beyond the LDS tier
+// Token-table tier (am_hash.hip) for add-wins-set / MV-register reads over the packed and
+// record views: reads it cannot finish exactly, and logs beyond its length limit, go to
+// `next` (the LDS-sort tier, which hands logs beyond its own limit to the big-read tier).
+bool am_hash_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
+int am_launch_hash(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                   uint32_t type, am_retry next);
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
 
 // Short-read tier (am_rows.hip): reads with at most short_max ops (and error reads) are

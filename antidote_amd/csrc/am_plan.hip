@@ -148,16 +148,18 @@ int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   return am_launch_rows(ctx, L, B, R, S, type, H);
 }
 
-// Set types over selection S: row tier -> (hand-off list) workgroup tier k_sets ->
-// (retry list) big-read tier.  rows_buf: [0] = 0, [1] = hand-off count, list at +64.
+// Set types over selection S: row tier -> (hand-off list) token-table tier k_hsets (add-wins
+// set / MV register over the record view) -> (hand-off list) LDS-sort tier k_sets ->
+// (retry list) big-read tier.  rows_buf / hash_buf: [0] = 0, [1] = hand-off count, list at +64.
 int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
-             uint32_t *retry_buf, uint32_t *rows_buf) {
+             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *hash_buf) {
   am_retry retry;
   retry.count = retry_buf;
   retry.list = retry_buf + 1;
   AM_HIP(hipMemsetAsync(retry.count, 0, sizeof(uint32_t), ctx->stream));
   const uint32_t m = rows_max(true);
   int rc;
+  am_sel cur = S;
   if (m) {
     AM_HIP(hipMemsetAsync(rows_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
     am_rows_cfg C;
@@ -166,13 +168,20 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     C.count = rows_buf + 1;
     rc = am_launch_rows(ctx, L, B, R, S, type, C);
     if (rc) return rc;
-    am_sel S2;
-    S2.idx = C.list;
-    S2.range = rows_buf;
-    rc = am_launch_sets(ctx, L, B, R, S2, type, retry);
-  } else {
-    rc = am_launch_sets(ctx, L, B, R, S, type, retry);
+    cur.idx = C.list;
+    cur.range = rows_buf;
   }
+  if (hash_buf && am_hash_applies(L, R, type)) {
+    AM_HIP(hipMemsetAsync(hash_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
+    am_retry next;
+    next.count = hash_buf + 1;
+    next.list = hash_buf + 64;
+    rc = am_launch_hash(ctx, L, B, R, cur, type, next);
+    if (rc) return rc;
+    cur.idx = next.list;
+    cur.range = hash_buf;
+  }
+  rc = am_launch_sets(ctx, L, B, R, cur, type, retry);
   if (rc) return rc;
   return am_launch_big(ctx, L, B, R, type, retry);
 }
@@ -202,9 +211,11 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   if (variant && strcmp(variant, "scalar") == 0 && B->type_hint <= AM_LWW) return am_launch_scalar(ctx, L, B, R);
 
   const am_sel all{};
-  void *rows_scr = nullptr;
+  void *rows_scr = nullptr, *hash_scr = nullptr;
   {
     int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
+    if (!rc && B->type_hint != AM_PN && B->type_hint != AM_LWW && B->type_hint != AM_BCOUNTER)
+      rc = am_ctx_scratch(ctx, AM_SCR_HASH, (n + 64) * sizeof(uint32_t), &hash_scr);
     if (rc) return rc;
   }
   if (B->type_hint == AM_PN || B->type_hint == AM_LWW)
@@ -213,7 +224,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     void *scr = nullptr;
     int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &scr);
     if (rc) return rc;
-    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr);
+    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr, (uint32_t *)hash_scr);
   }
   if (B->type_hint != 0) {
     am_set_error("type_hint %u not supported", B->type_hint);
@@ -244,7 +255,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     if (t == AM_PN || t == AM_LWW)
       rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
     else
-      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr);
+      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr, (uint32_t *)hash_scr);
     if (rc) return rc;
   }
   return AM_OK;

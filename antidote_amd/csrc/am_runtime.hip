@@ -80,7 +80,7 @@ int am_timer_stop(am_ctx *c, float *ms) {
 }  // extern "C"
 
 int am_ctx_scratch(am_ctx *c, int slot, size_t bytes, void **out) {
-  if (!c || slot < 0 || slot >= 4 || !out) return AM_ERR_INVALID;
+  if (!c || slot < 0 || slot >= AM_N_SCR || !out) return AM_ERR_INVALID;
   if (bytes == 0) bytes = 256;
   if (c->scratch_bytes[slot] < bytes) {
     if (c->scratch[slot]) {
