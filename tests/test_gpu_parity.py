@@ -396,3 +396,77 @@ def test_gpu_packed_view_escapes(mat, t):
         reads.append(Read(k, t, clock))
     log = HostLog(3, keys, key_types=[t] * len(keys))
     _batch_compare(log, reads, mat, 3)
+
+
+def _seq_ops(t, effects, n_dc=2):
+    return [Op(t, i % n_dc, 10 + 2 * i, {d: 10 + 2 * i - 1 for d in range(n_dc)}, eff) for i, eff in enumerate(effects)]
+
+
+def test_gpu_hash_tier_guards(mat):
+    """The token-table tier (am_hash.hip: k_stream set mode + k_hrec) hands a read to the
+    LDS-sort tier whenever its table cannot decide it exactly; every case must still
+    match the oracle.  Logs of 60 .. 2000 ops (between the row tier and the tier's limit):
+      0  AW: one token under two elems (the kill key is (tok, elem))
+      1  AW: 600 live elems (more survivors than the table's survivor list)
+      2  MV: one token with two values
+      3  MV: 1500 concurrent values (more distinct tokens than table slots)
+      4  AW / 5 MV: the sentinel 2^64-1 as a token / value
+      6  AW: plain 300-op log (stays in the tier), 7  MV: plain 2000-op chain
+      8  AW: 2100 ops (beyond the tier: the LDS-sort tier takes it whole)"""
+    M = (1 << 64) - 1
+    aw, mv = abi.AM_AWSET, abi.AM_MVREG
+    keys, types = [], []
+
+    def add(t, effs):
+        keys.append(_seq_ops(t, effs))
+        types.append(t)
+
+    add(aw, [[(i % 7, [900 + (i % 40)], [])] for i in range(80)])
+    add(aw, [[(i, [1000 + i], [])] for i in range(600)])
+    add(mv, [("assign", i % 3, 77 if i % 10 == 0 else 500 + i, []) for i in range(90)])
+    add(mv, [("assign", i, 3000 + i, []) for i in range(1500)])
+    add(aw, [[(1, [M if i == 30 else 5000 + i], [])] for i in range(70)])
+    add(mv, [("assign", M if i == 40 else i, 6000 + i, [6000 + i - 1] if i else []) for i in range(70)])
+    effs, live = [], {}
+    for i in range(300):
+        e = i % 9
+        effs.append([(e, [7000 + i], live.get(e, []))])
+        live[e] = [7000 + i]
+    add(aw, effs)
+    add(mv, [("assign", i % 5, 9000 + i, [9000 + i - 1] if i else []) for i in range(2000)])
+    add(aw, [[(i % 11, [20000 + i], [20000 + i - 11] if i >= 11 else [])] for i in range(2100)])
+    log = HostLog(2, keys, key_types=types)
+    reads = []
+    for k, ops in enumerate(keys):
+        hi = ops[-1].commit_time
+        for q in (0.5, 1.0):
+            c = int(10 + (hi - 10) * q)
+            reads.append(Read(k, types[k], {0: c, 1: c}))
+    got = _batch_compare(log, reads, mat, 2, cap=4096)  # mixed batch: the planner splits it
+    assert got.result(3)[0] == "ok"  # key 1 at q=1.0: 600 survivors
+    for t in (aw, mv):  # single-type batches (type_hint path)
+        _batch_compare(log, [r for r in reads if r.type == t], mat, 2, cap=4096)
+
+
+def test_gpu_hash_tier_mixed_batch(mat):
+    """The same tier inside a mixed batch (planner selection + row-tier hand-off list),
+    with cached bases (base pairs are births at -1) on the second read."""
+    rng = random.Random(4242)
+    keys, types = [], []
+    for k in range(60):
+        t = [abi.AM_AWSET, abi.AM_MVREG, abi.AM_PN][k % 3]
+        keys.append(randlog.rand_key_ops(rng, t, 3, rng.choice([10, 70, 200, 900, 1900])))
+        types.append(t)
+    log = HostLog(3, keys, key_types=types)
+    reads = []
+    for k, ops in enumerate(keys):
+        hi = ops[-1].commit_time
+        reads.append(Read(k, types[k], randlog.rand_clock(rng, 3, int(hi * 0.6), int(hi * 0.6) + 8)))
+    first = _batch_compare(log, reads, mat, 3, cap=4096)
+    reads2 = []
+    for i, r in enumerate(reads):
+        res = first.result(i)
+        if res[0] == "ok":
+            clock2 = {d: v + rng.randint(0, 3000) for d, v in r.clock.items()}
+            reads2.append(Read(r.key, r.type, clock2, None, res[3], res[2], res[1]))
+    _batch_compare(log, reads2, mat, 3, cap=4096)
