@@ -84,6 +84,10 @@ int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_re
 bool am_hash_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
 int am_launch_hash(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                    uint32_t type, am_retry next);
+struct am_setincl;
+// k_stream's set mode (am_stream.h): inclusion pass of the token-table tier
+int am_launch_stream_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                          uint32_t type, const am_setincl &X);
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
 
 // Short-read tier (am_rows.hip): reads with at most short_max ops (and error reads) are
