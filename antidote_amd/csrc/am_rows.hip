@@ -446,43 +446,67 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
               if (status == AM_OK && rs->ctr[3]) defer = true;
               if (status == AM_OK && !defer) {
                 const uint32_t ne = rs->ctr[0];
-                // pass 1: exact sums of the lane's slots, overflow check
-                uint32_t ovf = 0;
-                for (uint32_t i = sl; i < nslot; i += G) {
-                  int64_t bv = 0;
-                  if (GENERAL) {
-                    if (i < np) bv = B.base.bc_p ? B.base.bc_p[rj * np + i] : 0;
-                    else bv = B.base.bc_d ? B.base.bc_d[rj * nd + (i - np)] : 0;
-                  }
-                  int64_t hi = bv < 0 ? -1 : 0;
-                  uint64_t lo = (uint64_t)bv;
-                  for (uint32_t e = 0; e < ne; ++e)
-                    if ((uint32_t)rs->kp[e] == i) {
-                      const int64_t x = (int64_t)rs->ka[e];
-                      add128(hi, lo, x < 0 ? -1 : 0, (uint64_t)x);
-                    }
-                  if (hi != ((int64_t)lo < 0 ? -1 : 0)) ovf = 1;
+                const uint32_t ne4 = (ne + 3) & ~3u;
+                if (sl < ne4 - ne) rs->kp[ne + sl] = -1;  // pad the slot list to whole int4 loads
+                // With every |amount| < 2^56 (and no base values) the <= 64 entries of a
+                // slot cannot leave int64: the exact overflow pass is skipped.
+                uint32_t big = (GENERAL && (B.base.bc_p || B.base.bc_d)) ? 1u : 0u;
+                for (uint32_t e = sl; e < ne; e += G) {
+                  const int64_t x = (int64_t)rs->ka[e];
+                  big |= (x >= (1ll << 56) || x < -(1ll << 56)) ? 1u : 0u;
                 }
-                if (ovf) atomicOr(&rs->ctr[2], 1u);
+                big = row_or_u32(big);
                 wave_sync();
-                if (rs->ctr[2]) {
-                  status = AM_ERR_OVERFLOW;
-                } else {  // pass 2: write the slots
-                  for (uint32_t i = sl; i < nslot; i += G) {
-                    int64_t bv = 0;
-                    uint32_t bpres = 0;
-                    if (GENERAL) {
-                      if (i < np) {
-                        bv = B.base.bc_p ? B.base.bc_p[rj * np + i] : 0;
-                        bpres = B.base.bc_p_pres ? B.base.bc_p_pres[rj * np + i] : 0;
-                      } else {
-                        bv = B.base.bc_d ? B.base.bc_d[rj * nd + (i - np)] : 0;
-                        bpres = B.base.bc_d_pres ? B.base.bc_d_pres[rj * nd + (i - np)] : 0;
+                // sum of the row's entries with slot i (int4 loads of the slot list)
+                auto slot_sum = [&](uint32_t i, int64_t &hi, uint64_t &lo) -> uint32_t {
+                  uint32_t hit = 0;
+                  const int4 *kp4 = reinterpret_cast<const int4 *>(rs->kp);
+#pragma unroll 4
+                  for (uint32_t e = 0; e < ne4; e += 4) {
+                    const int4 k = kp4[e >> 2];
+                    const int32_t ks[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                      if (ks[q] == (int32_t)i) {
+                        const int64_t x = (int64_t)rs->ka[e + q];
+                        add128(hi, lo, x < 0 ? -1 : 0, (uint64_t)x);
+                        hit = 1;
                       }
-                    }
+                  }
+                  return hit;
+                };
+                auto base_of = [&](uint32_t i, uint32_t &bpres) -> int64_t {
+                  bpres = 0;
+                  if (!GENERAL) return 0;
+                  if (i < np) {
+                    bpres = B.base.bc_p_pres ? B.base.bc_p_pres[rj * np + i] : 0;
+                    return B.base.bc_p ? B.base.bc_p[rj * np + i] : 0;
+                  }
+                  bpres = B.base.bc_d_pres ? B.base.bc_d_pres[rj * nd + (i - np)] : 0;
+                  return B.base.bc_d ? B.base.bc_d[rj * nd + (i - np)] : 0;
+                };
+                if (big) {  // pass 1: exact 128-bit sums of the lane's slots, overflow check
+                  uint32_t ovf = 0;
+                  for (uint32_t i = sl; i < nslot; i += G) {
+                    uint32_t bp;
+                    const int64_t bv = base_of(i, bp);
+                    int64_t hi = bv < 0 ? -1 : 0;
                     uint64_t lo = (uint64_t)bv;
-                    for (uint32_t e = 0; e < ne; ++e)
-                      if ((uint32_t)rs->kp[e] == i) lo += rs->ka[e], bpres = 1;
+                    slot_sum(i, hi, lo);
+                    if (hi != ((int64_t)lo < 0 ? -1 : 0)) ovf = 1;
+                  }
+                  if (ovf) atomicOr(&rs->ctr[2], 1u);
+                  wave_sync();
+                }
+                if (big && rs->ctr[2]) {
+                  status = AM_ERR_OVERFLOW;
+                } else {  // write the slots
+                  for (uint32_t i = sl; i < nslot; i += G) {
+                    uint32_t bpres;
+                    const int64_t bv = base_of(i, bpres);
+                    int64_t hi = bv < 0 ? -1 : 0;
+                    uint64_t lo = (uint64_t)bv;
+                    bpres |= slot_sum(i, hi, lo);
                     if (i < np) {
                       R.value.bc_p[rj * np + i] = (int64_t)lo;
                       R.value.bc_p_pres[rj * np + i] = bpres ? 1 : 0;

@@ -61,15 +61,18 @@ CONFIGS = {
 
 def bytes_per_op(type_: int, n_dc: int, packed: bool = True) -> int:
     """Algorithmic HBM bytes read per op by its materialize kernel.
-    k_stream packed view: ct_meta 8 + snapshot deltas 4*D + payload (PN 8, LWW 16);
-    full view (k_sets, k_big_chunk): op_meta 1 + commit_time 8 + snapshot_time 8*D + payload
-    (PN 8, LWW 16; AW var_off 8; MV p0 p1 var_off 24; bcounter p0 p1 16).  Variable-length
-    effect words (AW entries, MV overridden tokens) are counted separately, 8 B each."""
-    if type_ in (abi.AM_PN, abi.AM_LWW):
-        payload = 16 if type_ == abi.AM_LWW else 8
-        return (8 + 4 * n_dc + payload) if packed else (1 + 8 + 8 * n_dc + payload)
-    payload = {abi.AM_AWSET: 8, abi.AM_MVREG: 24, abi.AM_BCOUNTER: 16}[type_]
+    Packed view: ct_meta 8 + snapshot deltas 4*D + payload (PN 8, LWW 16, bcounter 16;
+    add-wins-set / MV-register effects come from the record view, counted per record in
+    workload_bytes).  Full view (logs without the packed view): op_meta 1 + commit_time 8 +
+    snapshot_time 8*D + payload (PN 8, LWW 16; AW var_off 8; MV p0 p1 var_off 24; bcounter
+    p0 p1 16), variable-length effect words counted separately, 8 B each."""
+    if packed:
+        return 8 + 4 * n_dc + {abi.AM_PN: 8, abi.AM_LWW: 16, abi.AM_AWSET: 0, abi.AM_MVREG: 0, abi.AM_BCOUNTER: 16}[type_]
+    payload = {abi.AM_PN: 8, abi.AM_LWW: 16, abi.AM_AWSET: 8, abi.AM_MVREG: 24, abi.AM_BCOUNTER: 16}[type_]
     return 1 + 8 + 8 * n_dc + payload
+
+
+REC_BYTES = 20  # one set-effect record: rec_a 8 + rec_b 8 + rec_meta 4 (am_pack.hip)
 
 
 def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
@@ -105,7 +108,8 @@ def key_columns(mat, dlog, n_keys):
 def workload_bytes(cfg, dlog, ko, kt, reads, packed):
     """Algorithmic bytes of one am_materialize over every key of the store."""
     lens = np.diff(ko.astype(np.int64))
-    total = float(dlog.n_var) * 8
+    records = packed and bool(dlog.rec_key_off)
+    total = float(dlog.n_rec) * REC_BYTES if records else float(dlog.n_var) * 8
     set_len = reads.set_len.cpu().numpy() if reads.set_len is not None else None
     for t in sorted(set(int(x) for x in np.unique(kt))):
         m = kt == t
@@ -325,10 +329,10 @@ def main():
                    "step": "GST min all-reduce (RCCL) + materialize all keys"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config, workload),
-                     "kernel": "k_stream" if single else "am_materialize (planner + k_stream/k_sets/k_big_*)",
+                     "kernel": "k_stream" if single else "am_materialize (all tiers: k_stream, k_rows, k_hrec, k_sets, k_big_*)",
                      "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "layout": "packed (ct_meta + int32 snapshot deltas) for PN/LWW, full columns for sets"
+                     "layout": "packed (ct_meta + int32 snapshot deltas); set effects as (a, tok, op) records"
                      if packed else "full"},
         "cpu_baseline": None,
     }
