@@ -47,10 +47,33 @@ constexpr uint32_t HB_WORDS = 72;  // (2048 + 3 ops, whole 256-op tiles) / 32
 
 constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;
-constexpr int OPL = 4;
-constexpr uint64_t TILE = WAVE * OPL;
-
+// ops per lane of a tile: 4 (16-byte loads), 2 for 8-DC clocks (measured: C3 11.8 -> 11.2 ms;
+// at D = 16 the narrower tile was slower, 4.2 -> 4.7 ms), which shrinks the double-buffered tiles
 template <int DMAX>
+constexpr int opl_of() { return DMAX == 8 ? 2 : 4; }
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int N>
+__device__ __forceinline__ void ld_u64(const uint64_t *p, uint64_t *o) {
+  const u64x2 a = *(const u64x2 *)p;
+  o[0] = a.x, o[1] = a.y;
+  if constexpr (N == 4) {
+    const u64x2 b = *(const u64x2 *)(p + 2);
+    o[2] = b.x, o[3] = b.y;
+  }
+}
+template <int N>
+__device__ __forceinline__ void ld_u32(const uint32_t *p, uint32_t *o) {
+  if constexpr (N == 4) {
+    const u32x4 a = *(const u32x4 *)p;
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w;
+  } else {
+    const u32x2 a = *(const u32x2 *)p;
+    o[0] = a.x, o[1] = a.y;
+  }
+}
+
+template <int DMAX, int OPL = opl_of<DMAX>()>
 struct Tile {
   uint32_t meta4;           // full view
   uint64_t ct[OPL];
@@ -69,8 +92,9 @@ struct Out {
   uint32_t flags, pres, count;
   uint32_t ign, newss, vflag;
   int64_t nlo;
-  uint64_t ct[DMAX];
+  uint64_t ct[DMAX];  // only with BUF_CT
   uint64_t v0, v1;
+  uint32_t fin;       // the read was finalized (wide clocks: LastOpCt already stored)
 };
 
 struct NoVal {  // set mode: the effects are resolved by k_hrec (am_hash.hip)
@@ -98,6 +122,9 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
                                                   am_rows_cfg H, am_setincl X) {
   using V = typename SOf<TYPE>::T;
   constexpr bool SETM = SOf<TYPE>::SETM;
+  constexpr int OPL = opl_of<DMAX>();
+  constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
+  constexpr bool BUF_CT = DMAX < 8;  // wide clocks: LastOpCt leaves at finalize (fewer VGPRs)
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint64_t n = B.n_reads;  // column stride of per-read arrays
   // reads to process: slots [0, nsel) -> read sbase[slot] (or the identity)
@@ -161,7 +188,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       if (SETM && M.st == AM_OK) {
         M.rk0 = L.rec_key_off[key];
         M.rk1 = L.rec_key_off[key + 1];
-        M.sh = (uint32_t)(M.off0 & 3);
+        M.sh = (uint32_t)(M.off0 & (OPL - 1));
         if (M.off1 - M.off0 > (uint64_t)X.max_ops) M.big = 1, M.skip = 1;
       }
       if (M.st != AM_OK || M.big) M.off1 = M.off0;  // no tiles to stream
@@ -186,9 +213,10 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   // Every lane computes it for its own read; reads with ops overwrite it.
   auto init_out = [&](const Meta &M) {
     o.status = M.st;
-    o.flags = 0, o.pres = 0, o.count = 0, o.ign = 1, o.newss = 0, o.nlo = 0;
+    o.flags = 0, o.pres = 0, o.count = 0, o.ign = 1, o.newss = 0, o.nlo = 0, o.fin = 0;
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) o.ct[d] = 0;
+    for (int d = 0; d < DMAX; ++d)
+      if (BUF_CT) o.ct[d] = 0;
     o.v0 = 0, o.v1 = 0, o.vflag = TYPE == AM_LWW ? 1 : 0;
     if (GENERAL && lane < M.nb) {
       const uint64_t r = M.r;
@@ -197,7 +225,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
         o.pres = B.base_pres[r] & u.allmask;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d)
-          if (d < (int)nd && ((o.pres >> d) & 1u)) o.ct[d] = B.base_vc[(uint64_t)d * n + r];
+          if (BUF_CT && d < (int)nd && ((o.pres >> d) & 1u)) o.ct[d] = B.base_vc[(uint64_t)d * n + r];
       }
       if (B.base.v0) {
         o.v0 = (uint64_t)B.base.v0[r];
@@ -226,8 +254,12 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
         R.last_ct_ignore[r] = (uint8_t)o.ign;
         R.last_ct_pres[r] = o.pres;
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d)
-          if (d < (int)nd) R.last_ct[(uint64_t)d * n + r] = o.ct[d];
+        for (int d = 0; d < DMAX; ++d) {
+          if (d >= (int)nd) continue;
+          if (BUF_CT) R.last_ct[(uint64_t)d * n + r] = o.ct[d];
+          else if (!o.fin)  // no op streamed: LastOpCt = the base snapshot_time (finalize wrote the rest)
+            R.last_ct[(uint64_t)d * n + r] = (GENERAL && ((o.pres >> d) & 1u)) ? B.base_vc[(uint64_t)d * n + r] : 0;
+        }
         R.is_new_ss[r] = (uint8_t)o.newss;
         R.count[r] = o.count;
         if (!SETM) R.value.v0[r] = (int64_t)o.v0;
@@ -260,45 +292,36 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       for (int d = 0; d < DMAX; ++d) T.sv[k][d] = 0, T.sd[k][d] = 0;
     }
     if (g < o1 && PACKED) {
-      const u64x2 c01 = *(const u64x2 *)(L.ct_meta + g), c23 = *(const u64x2 *)(L.ct_meta + g + 2);
-      T.ctm[0] = c01.x, T.ctm[1] = c01.y, T.ctm[2] = c23.x, T.ctm[3] = c23.y;
+      ld_u64<OPL>(L.ct_meta + g, T.ctm);
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d < (int)nd) {
-          const u32x4 s = *(const u32x4 *)(L.snap_delta + (uint64_t)d * stride + g);
-          T.sd[0][d] = (int32_t)s.x, T.sd[1][d] = (int32_t)s.y, T.sd[2][d] = (int32_t)s.z, T.sd[3][d] = (int32_t)s.w;
+          uint32_t sdv[OPL];
+          ld_u32<OPL>((const uint32_t *)L.snap_delta + (uint64_t)d * stride + g, sdv);
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) T.sd[k][d] = (int32_t)sdv[k];
         }
       }
     } else if (g < o1) {
-      T.meta4 = *(const uint32_t *)(L.op_meta + g);
-      const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
-      T.ct[0] = c01.x, T.ct[1] = c01.y, T.ct[2] = c23.x, T.ct[3] = c23.y;
+      T.meta4 = OPL == 4 ? *(const uint32_t *)(L.op_meta + g) : (uint32_t)*(const uint16_t *)(L.op_meta + g);
+      ld_u64<OPL>(L.commit_time + g, T.ct);
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d < (int)nd) {
-          const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
-          const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
-          T.sv[0][d] = s01.x, T.sv[1][d] = s01.y, T.sv[2][d] = s23.x, T.sv[3][d] = s23.y;
+          uint64_t svv[OPL];
+          ld_u64<OPL>(L.snap_vc + (uint64_t)d * stride + g, svv);
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) T.sv[k][d] = svv[k];
         }
       }
     }
     if (g < o1) {
       if (GENERAL && L.snap_pres) {
-        const u32x4 s = *(const u32x4 *)(L.snap_pres + g);
-        T.sp[0] = s.x, T.sp[1] = s.y, T.sp[2] = s.z, T.sp[3] = s.w;
+        ld_u32<OPL>(L.snap_pres + g, T.sp);
       }
-      if (SOf<TYPE>::NEED_P0) {
-        const u64x2 a01 = *(const u64x2 *)(L.p0 + g), a23 = *(const u64x2 *)(L.p0 + g + 2);
-        T.p0[0] = a01.x, T.p0[1] = a01.y, T.p0[2] = a23.x, T.p0[3] = a23.y;
-      }
-      if (SOf<TYPE>::NEED_P1) {
-        const u64x2 b01 = *(const u64x2 *)(L.p1 + g), b23 = *(const u64x2 *)(L.p1 + g + 2);
-        T.p1[0] = b01.x, T.p1[1] = b01.y, T.p1[2] = b23.x, T.p1[3] = b23.y;
-      }
-      if (GENERAL && L.op_txid && B.txid) {
-        const u64x2 x01 = *(const u64x2 *)(L.op_txid + g), x23 = *(const u64x2 *)(L.op_txid + g + 2);
-        T.tx[0] = x01.x, T.tx[1] = x01.y, T.tx[2] = x23.x, T.tx[3] = x23.y;
-      }
+      if (SOf<TYPE>::NEED_P0) ld_u64<OPL>(L.p0 + g, T.p0);
+      if (SOf<TYPE>::NEED_P1) ld_u64<OPL>(L.p1 + g, T.p1);
+      if (GENERAL && L.op_txid && B.txid) ld_u64<OPL>(L.op_txid + g, T.tx);
     }
   };
   auto setup_read = [&](uint32_t j) {  // per-read uniform inputs (GENERAL only)
@@ -344,12 +367,12 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       }
     }
     if constexpr (SETM) {  // the tile's 256 inclusion bits -> 8 words of the slot's bitmap
-      uint32_t wv = ib << (4 * (lane & 7));
-      wv |= (uint32_t)__shfl_xor((int)wv, 1);
-      wv |= (uint32_t)__shfl_xor((int)wv, 2);
-      wv |= (uint32_t)__shfl_xor((int)wv, 4);
-      const uint64_t wi = (t - (o0 & ~(uint64_t)3)) / 32 + (lane >> 3);
-      if ((lane & 7) == 0 && wi < HB_WORDS) X.bitmap[(M0.rb + j) * HB_WORDS + wi] = wv;
+      constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
+      uint32_t wv = ib << (OPL * (lane % LPW));
+#pragma unroll
+      for (uint32_t m = 1; m < LPW; m <<= 1) wv |= (uint32_t)__shfl_xor((int)wv, (int)m);
+      const uint64_t wi = (t - (o0 & ~(uint64_t)(OPL - 1))) / 32 + lane / LPW;
+      if (lane % LPW == 0 && wi < HB_WORDS) X.bitmap[(M0.rb + j) * HB_WORDS + wi] = wv;
     }
   };
   // Reduce read j of batch M0 across the wave and park its results in lane j.
@@ -410,9 +433,18 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         const uint64_t m = mx[d] > u.C0[d] ? mx[d] : u.C0[d];
-        o.ct[d] = ((opres >> d) & 1u) ? m : 0;
+        if (BUF_CT) o.ct[d] = ((opres >> d) & 1u) ? m : 0;
       }
       o.v0 = v0, o.v1 = v1, o.vflag = vflag;
+      o.fin = 1;
+    }
+    if (!BUF_CT && status == AM_OK) {  // wide clocks: lane d stores entry d of LastOpCt
+      const uint64_t r = lane_u64(M0.r, j);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const uint64_t m = mx[d] > u.C0[d] ? mx[d] : u.C0[d];
+        if ((uint32_t)d == lane && d < (int)nd) R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? m : 0;
+      }
     }
     a.reset();
     v.reset();
