@@ -94,6 +94,9 @@ class am_synth_params(ctypes.Structure):
 
 
 AM_SYNTH_MV_BC = 6
+AM_ERR_COLD_PATH = 5
+AM_SNAPSHOT_THRESHOLD = 10
+AM_SNAPCACHE_ABSENT = 0xFFFFFFFF
 
 
 # (name, restype, argtypes) of every exported symbol declared in include/antidote_mat.h
@@ -123,6 +126,14 @@ SIGNATURES = [
     ("am_gst_finalize", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                 c_void_p]),
     ("am_key_partition", c_uint32, [c_int64, c_uint32]),
+    ("am_snapcache_create", c_int, [c_void_p, c_uint32, c_uint64, POINTER(c_void_p)]),
+    ("am_snapcache_destroy", c_int, [c_void_p]),
+    ("am_snapcache_read", c_int, [c_void_p, c_void_p, POINTER(am_op_log), POINTER(am_read_batch),
+                                  POINTER(am_read_result)]),
+    ("am_snapcache_read_host", c_int, [c_void_p, c_void_p, c_void_p, POINTER(am_read_batch),
+                                       POINTER(am_read_result)]),
+    ("am_snapcache_get", c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint32), c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
     ("am_synth_store", c_int, [c_void_p, POINTER(am_synth_params), POINTER(c_void_p)]),
     ("am_synth_read_clock", c_int, [POINTER(am_synth_params), c_double, c_void_p]),
     ("am_synth_host_sizes", c_int, [POINTER(am_synth_params), c_uint64, c_uint64, POINTER(c_uint64),

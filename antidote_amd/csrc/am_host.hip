@@ -3,6 +3,7 @@
 // into one device arena, runs am_materialize on the store's resident log and
 // copies the result columns back.
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "am_internal.h"
@@ -21,7 +22,10 @@ struct Arena {
 
 }  // namespace
 
-extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr) {
+// Stages a host batch into one device arena, runs `run` on the device batch/result and
+// copies the result columns back.
+static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr,
+                    const std::function<int(const am_read_batch *, am_read_result *)> &run) {
   if (!c || !st || !hb || !hr || !hb->key || !hb->type || !hb->read_vc || !hb->read_pres) return AM_ERR_INVALID;
   const uint64_t n = hb->n_reads;
   if (n == 0) return AM_OK;
@@ -94,7 +98,7 @@ extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_
   out(hr->value.bc_d_pres, n * nd, (void **)&dr.value.bc_d_pres);
   if (!hr->status || !hr->new_last_op || !hr->last_ct || !hr->last_ct_pres || !hr->last_ct_ignore || !hr->is_new_ss ||
       !hr->count || !hr->flags) {
-    am_set_error("am_materialize_host: every result column is required");
+    am_set_error("host batch: every result column is required");
     return AM_ERR_INVALID;
   }
 
@@ -122,15 +126,30 @@ extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_
     *outs[i].dptr = arena + out_off[i];
   }
   if (e == hipSuccess) {
-    rc = am_launch_materialize(c, &st->dev, &db, &dr);
+    rc = run(&db, &dr);
     for (size_t i = 0; i < outs.size() && e == hipSuccess && !rc; ++i)
       e = hipMemcpyAsync(outs[i].h, arena + out_off[i], outs[i].bytes, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   }
   (void)hipFree(arena);
   if (e != hipSuccess) {
-    am_set_error("am_materialize_host: %s", hipGetErrorString(e));
+    am_set_error("host batch: %s", hipGetErrorString(e));
     return AM_ERR_HIP;
   }
   return rc;
+}
+
+extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr) {
+  if (!st) return AM_ERR_INVALID;
+  return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr) {
+    return am_launch_materialize(c, &st->dev, db, dr);
+  });
+}
+
+extern "C" int am_snapcache_read_host(am_ctx *c, am_snapcache *sc, const am_store *st, const am_read_batch *hb,
+                                      am_read_result *hr) {
+  if (!st || !sc) return AM_ERR_INVALID;
+  return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr) {
+    return am_snapcache_read(c, sc, &st->dev, db, dr);
+  });
 }

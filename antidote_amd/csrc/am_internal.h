@@ -10,7 +10,7 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_HASH = 4, AM_SCR_HASHX = 5, AM_N_SCR = 6 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_HASH = 4, AM_SCR_HASHX = 5, AM_SCR_SNAP = 6, AM_N_SCR = 7 };
 
 struct am_ctx {
   int device = 0;

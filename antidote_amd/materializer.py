@@ -43,6 +43,53 @@ class Store:
             pass
 
 
+class SnapshotCache:
+    """A partition's snapshot cache on the device: reads run materializer_vnode:internal_read/7
+    (src/materializer_vnode.erl:371-376) -- base from the cache, materialize/4, write-back."""
+
+    def __init__(self, mat: "Materializer", store: "Store", n_keys: int):
+        self.mat, self.store = mat, store
+        self.handle = ctypes.c_void_p()
+        abi.check(mat.L.am_snapcache_create(mat.ctx, store.n_dc, n_keys, ctypes.byref(self.handle)),
+                  "am_snapcache_create")
+
+    def read(self, reads: Sequence[Read]) -> HostBatch:
+        """internal_read/7 (ShouldGC = false) for reads of distinct keys; read.base_* are ignored.
+        Per read: ('ok', Value, ...) or ('error', AM_ERR_COLD_PATH) when the log would be read."""
+        hb = HostBatch(self.store.n_dc, reads)
+        b, r = hb.structs()
+        abi.check(self.mat.L.am_snapcache_read_host(self.mat.ctx, self.handle, self.store.handle, ctypes.byref(b),
+                                                    ctypes.byref(r)), "am_snapcache_read_host")
+        return hb
+
+    def entries(self, key: int):
+        """[(clock, last_op_id, v0, v1, vflag)] newest first, or None before the key's first read."""
+        import numpy as np
+        nd, cap = self.store.n_dc, abi.AM_SNAPSHOT_THRESHOLD
+        n = ctypes.c_uint32()
+        vc = np.zeros(cap * nd, np.uint64)
+        pres = np.zeros(cap, np.uint32)
+        lo = np.zeros(cap, np.int64)
+        v0 = np.zeros(cap, np.int64)
+        v1 = np.zeros(cap, np.uint64)
+        vf = np.zeros(cap, np.uint8)
+        abi.check(self.mat.L.am_snapcache_get(self.mat.ctx, self.handle, key, ctypes.byref(n), vc.ctypes.data,
+                                              pres.ctypes.data, lo.ctypes.data, v0.ctypes.data, v1.ctypes.data,
+                                              vf.ctypes.data), "am_snapcache_get")
+        if n.value == abi.AM_SNAPCACHE_ABSENT:
+            return None
+        out = []
+        for e in range(n.value):
+            clock = {d: int(vc[e * nd + d]) for d in range(nd) if (int(pres[e]) >> d) & 1}
+            out.append((clock, int(lo[e]), int(v0[e]), int(v1[e]), int(vf[e])))
+        return out
+
+    def close(self):
+        if self.handle:
+            self.mat.L.am_snapcache_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
 class Materializer:
     """A context on one GPU (device index = local rank)."""
 
@@ -80,6 +127,10 @@ class Materializer:
         abi.check(self.L.am_materialize_host(self.ctx, store.handle, ctypes.byref(b), ctypes.byref(r)),
                   "am_materialize_host")
         return hb
+
+    # ---- snapshot cache (materializer_vnode snapshot_cache-P in HBM) ----
+    def snapshot_cache(self, store: Store, n_keys: int) -> "SnapshotCache":
+        return SnapshotCache(self, store, n_keys)
 
     def materialize(self, type_: int, txid: Optional[int], min_snapshot_time: Dict[int, int],
                     ops_newest_first: Sequence[Tuple[int, Op]], base_clock: Optional[Dict[int, int]] = None,

@@ -24,6 +24,11 @@
  *                           src/stable_time_functions.erl:42-48) and the gr-mode
  *                           broadcast of dc_utilities:get_stable_snapshot/0
  *                           (src/dc_utilities.erl:246-279)
+ *   am_snapcache_read       materializer_vnode:internal_read/7 with the snapshot cache
+ *                           in HBM: get_from_snapshot_cache/5, vector_orddict:
+ *                           get_smaller/2 + insert_bigger/3, materialize_snapshot/7,
+ *                           internal_store_ss/4 (src/materializer_vnode.erl:342-509,
+ *                           src/vector_orddict.erl:75-140)
  *   am_key_partition        log_utilities:get_key_partition/1 for integer keys
  *                           (src/log_utilities.erl:60-79,100-118)
  *
@@ -70,6 +75,8 @@ enum am_status {
   AM_ERR_UNEXPECTED_OPERATION = 2,  /* {error, {unexpected_operation, Effect, Type}}*/
   AM_ERR_OVERFLOW = 3,              /* result outside int64 (Erlang would bignum)   */
   AM_ERR_CAPACITY = 4,              /* set result larger than the caller's capacity */
+  AM_ERR_COLD_PATH = 5,             /* no cached snapshot at or below the read clock:
+                                       get_from_snapshot_log (the log, not the cache) */
   AM_ERR_INVALID = -1,
   AM_ERR_HIP = -2,
   AM_ERR_RCCL = -3,
@@ -247,6 +254,35 @@ int am_materialize(am_ctx *ctx, const am_op_log *dev_log, const am_read_batch *d
 /* Host pointers for batch/result; the log is the store's device log.  Blocks. */
 int am_materialize_host(am_ctx *ctx, const am_store *st, const am_read_batch *host_batch,
                         am_read_result *host_res);
+
+/* ---- snapshot cache (materializer_vnode snapshot_cache-P) ----
+ * Replaces get_from_snapshot_cache/5 + materialize_snapshot/7 + internal_store_ss/4 around
+ * materialize/4, i.e. materializer_vnode:internal_read/7 (src/materializer_vnode.erl:371-376,
+ * 384-413, 469-509, 342-364) and vector_orddict get_smaller / insert_bigger
+ * (src/vector_orddict.erl:75-87, 127-140): per key at most AM_SNAPSHOT_THRESHOLD snapshots,
+ * newest first, in HBM.  PN counter and LWW register values. */
+#define AM_SNAPSHOT_THRESHOLD 10   /* src/materializer_vnode.erl:37 */
+#define AM_SNAPSHOT_MIN 3          /* :39 */
+#define AM_MIN_OP_STORE_SS 5       /* :47 */
+#define AM_SNAPCACHE_ABSENT 0xFFFFFFFFu
+typedef struct am_snapcache am_snapcache;
+int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcache **out);
+int am_snapcache_destroy(am_snapcache *cache);
+/* internal_read/7 (ShouldGC = false) for a batch of reads: each read's base comes from the
+ * cache (the batch's base members are ignored), materialize/4 runs on it, and the result is
+ * written back under materialize_snapshot/7's policy.  Per read status: AM_ERR_COLD_PATH
+ * when no cached snapshot is vectorclock:le the read clock; AM_ERR_INVALID for a key read
+ * a second time in the same batch (the first read, by index, owns the key);
+ * AM_ERR_UNSUPPORTED for set / bounded-counter reads.  Device pointers, async. */
+int am_snapcache_read(am_ctx *ctx, am_snapcache *cache, const am_op_log *dev_log, const am_read_batch *dev_batch,
+                      am_read_result *dev_res);
+/* The same with host batch/result (blocks). */
+int am_snapcache_read_host(am_ctx *ctx, am_snapcache *cache, const am_store *st, const am_read_batch *host_batch,
+                           am_read_result *host_res);
+/* One key's entries (newest first) to host arrays of AM_SNAPSHOT_THRESHOLD (vc: x n_dc);
+ * *n_entries = AM_SNAPCACHE_ABSENT before the key's first read.  NULL arrays are skipped. */
+int am_snapcache_get(am_ctx *ctx, const am_snapcache *cache, uint64_t key, uint32_t *n_entries, uint64_t *vc,
+                     uint32_t *pres, int64_t *last_op, int64_t *v0, uint64_t *v1, uint8_t *vflag);
 
 /* ---- GST (global stable time) ---- */
 /* lanes[0..n_dc-1] = per-DC min over the partitions that have the DC (absent = UINT64_MAX);
