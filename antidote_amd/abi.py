@@ -97,6 +97,9 @@ AM_SYNTH_MV_BC = 6
 AM_ERR_COLD_PATH = 5
 AM_SNAPSHOT_THRESHOLD = 10
 AM_SNAPCACHE_ABSENT = 0xFFFFFFFF
+AM_GC_PRUNED_ALL = 0x1
+AM_GC_TRIGGER = 0x2
+AM_OPS_THRESHOLD = 50
 
 
 # (name, restype, argtypes) of every exported symbol declared in include/antidote_mat.h
@@ -134,6 +137,9 @@ SIGNATURES = [
                                        POINTER(am_read_result)]),
     ("am_snapcache_get", c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint32), c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p]),
+    ("am_snapcache_gc_threshold", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("am_store_update", c_int, [c_void_p, c_void_p, POINTER(am_op_log), c_void_p, c_void_p, c_void_p, c_void_p,
+                                POINTER(c_void_p)]),
     ("am_synth_store", c_int, [c_void_p, POINTER(am_synth_params), POINTER(c_void_p)]),
     ("am_synth_read_clock", c_int, [POINTER(am_synth_params), c_double, c_void_p]),
     ("am_synth_host_sizes", c_int, [POINTER(am_synth_params), c_uint64, c_uint64, POINTER(c_uint64),

@@ -1,0 +1,370 @@
+// am_gc.hip -- op-cache ingestion + garbage collection on the device.
+//
+// The reference keeps one ETS tuple per key, {Key, {Length, ListLen}, OpCounter, Op_1..}
+// (include/antidote.hrl:81-90), appends with op_insert_gc/3 (src/materializer_vnode.erl:
+// 622-647: OpCounter += 1, the op stored as {NewId, Payload}) and prunes with prune_ops/2 +
+// check_filter/7 (:565-604): an op survives iff materializer:belongs_to_snapshot_op(
+// Threshold, CommitTime, SnapshotTime) (src/materializer.erl:102-106), i.e. it is NOT
+// covered by Threshold = vectorclock:min of the retained snapshot clocks
+// (snapshot_insert_gc/4, :515-563).  Survivors keep their ids and their order.
+//
+// On the device an op log is CSR over keys, so one batched call rebuilds it:
+//   k_upd_count    one wave per key: survivor count (ballot popcounts) and payload words
+//   exclusive scans (hipcub) -> new key_off / var_off bases
+//   k_upd_scatter  one wave per key: survivors, then the key's new ops, copied column by
+//                  column with coalesced stores (positions from ballot prefix counts)
+// followed by am_store_pack (packed + record views) on the new store.  Each column is
+// read once and written once: HBM-bound stream compaction, no atomics.
+//
+// Deliberate differences from the ETS layout (both are ETS tuple artefacts):
+//   - ListLen / RESIZE_THRESHOLD sizing does not exist: the CSR log is exactly sized.
+//   - prune_ops' quirk of keeping element(FIRST_OP+Len) (a 0 "op") when every op is
+//     pruned (:580-583) is reported as AM_GC_PRUNED_ALL with zero ops kept.
+#include <hipcub/hipcub.hpp>
+
+#include "am_internal.h"
+
+namespace {
+
+constexpr int WAVE_SZ = 64;
+constexpr uint32_t OPS_THRESHOLD = 50;  // src/materializer_vnode.erl:41
+
+struct UpdArgs {
+  am_op_log L;                 // the store's current log (device)
+  am_op_log N;                 // new ops, CSR over the same keys (device); N.key_off null => none
+  const uint64_t *counter;     // [n_keys] OpCounter, or null => derived from L
+  const uint8_t *mask;         // [n_keys] prune this key, or null => no pruning
+  const uint64_t *thr_vc;      // [n_dc][n_keys]
+  const uint32_t *thr_pres;    // [n_keys]
+};
+
+__device__ __forceinline__ uint32_t lane() { return threadIdx.x & (WAVE_SZ - 1); }
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o, WAVE_SZ);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const uint32_t l = lane();
+  for (int o = 1; o < WAVE_SZ; o <<= 1) {
+    const uint64_t t = (uint64_t)__shfl_up((unsigned long long)v, (unsigned)o, WAVE_SZ);
+    if (l >= (uint32_t)o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_bcast(uint64_t v, uint32_t src) {
+  return (uint64_t)__shfl((unsigned long long)v, (int)src, WAVE_SZ);
+}
+
+__device__ __forceinline__ uint32_t all_mask(uint32_t n_dc) { return n_dc >= 32 ? 0xFFFFFFFFu : ((1u << n_dc) - 1u); }
+
+// check_filter's predicate: belongs_to_snapshot_op(Thr, {Dc, CT}, SS) = not le(SS[Dc := CT], Thr)
+// with vectorclock:le over keys(X) ++ keys(Thr), a missing entry reading 0.
+__device__ __forceinline__ bool survives(const am_op_log &L, uint64_t p, const UpdArgs &A, uint64_t k,
+                                         uint32_t tpres) {
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t all = all_mask(L.n_dc);
+  const uint32_t dc = AM_META_DC(L.op_meta[p]);
+  const uint32_t xpres = ((L.snap_pres ? L.snap_pres[p] : all) | (1u << dc)) & all;
+  const uint64_t ct = L.commit_time[p];
+  for (uint32_t d = 0; d < L.n_dc; ++d) {
+    if (!((xpres >> d) & 1u)) continue;
+    const uint64_t x = d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p];
+    const uint64_t t = ((tpres >> d) & 1u) ? A.thr_vc[(uint64_t)d * A.L.n_keys + k] : 0;
+    if (x > t) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint64_t var_len(const am_op_log &L, uint64_t p) {
+  return L.var_off ? L.var_off[p + 1] - L.var_off[p] : 0;
+}
+
+__global__ void k_upd_count(UpdArgs A, uint64_t *cnt, uint64_t *vcnt) {
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
+  for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE_SZ) + threadIdx.x / WAVE_SZ; k < A.L.n_keys; k += waves) {
+    const uint64_t o0 = A.L.key_off[k], o1 = A.L.key_off[k + 1];
+    const bool prune = A.mask && A.mask[k];
+    const uint32_t tpres = prune ? A.thr_pres[k] : 0;
+    uint64_t kept = 0, vk = 0;
+    for (uint64_t b = o0; b < o1; b += WAVE_SZ) {
+      const uint64_t p = b + lane();
+      const bool in = p < o1;
+      const bool keep = in && (!prune || survives(A.L, p, A, k, tpres));
+      kept += __popcll(__ballot(keep));
+      if (A.L.var_off) vk += wave_sum(keep ? var_len(A.L, p) : 0);
+    }
+    uint64_t nn = 0, nv = 0;
+    if (A.N.key_off) {
+      const uint64_t n0 = A.N.key_off[k], n1 = A.N.key_off[k + 1];
+      nn = n1 - n0;
+      if (A.N.var_off) nv = A.N.var_off[n1] - A.N.var_off[n0];
+    }
+    if (lane() == 0) {
+      cnt[k] = kept + nn;
+      vcnt[k] = vk + nv;
+    }
+  }
+}
+
+struct OutCols {
+  uint64_t *key_id_base, *counter;
+  uint8_t *key_type, *key_flags, *gc_flags, *gap;
+  uint8_t *op_meta;
+  uint64_t *commit_time, *snap_vc;
+  uint32_t *snap_pres;
+  uint64_t *op_txid, *op_id, *p0, *p1, *var_off, *var_data;
+  uint64_t stride;
+};
+
+__device__ __forceinline__ void put_op(const am_op_log &S, uint64_t p, const OutCols &O, uint64_t q, uint64_t id,
+                                       uint64_t vq) {
+  const uint64_t ss = S.snap_stride ? S.snap_stride : S.n_ops;
+  const uint32_t all = all_mask(S.n_dc);
+  O.op_meta[q] = S.op_meta[p];
+  O.commit_time[q] = S.commit_time[p];
+  for (uint32_t d = 0; d < S.n_dc; ++d) O.snap_vc[(uint64_t)d * O.stride + q] = S.snap_vc[(uint64_t)d * ss + p];
+  if (O.snap_pres) O.snap_pres[q] = S.snap_pres ? S.snap_pres[p] : all;
+  if (O.op_txid) O.op_txid[q] = S.op_txid ? S.op_txid[p] : ~0ull;
+  O.op_id[q] = id;
+  O.p0[q] = S.p0[p];
+  O.p1[q] = S.p1 ? S.p1[p] : 0;
+  if (O.var_off) {
+    O.var_off[q] = vq;
+    if (S.var_off)
+      for (uint64_t i = S.var_off[p], e = S.var_off[p + 1]; i < e; ++i) O.var_data[vq++] = S.var_data[i];
+  }
+}
+
+__global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vcnt, OutCols O) {
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
+  const uint64_t lt = (1ull << lane()) - 1ull;
+  for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE_SZ) + threadIdx.x / WAVE_SZ; k < A.L.n_keys; k += waves) {
+    const uint64_t o0 = A.L.key_off[k], o1 = A.L.key_off[k + 1];
+    const uint64_t idb = A.L.key_id_base ? A.L.key_id_base[k] : 1;
+    const uint64_t counter = A.counter ? A.counter[k]
+                             : o1 > o0 ? (A.L.op_id ? A.L.op_id[o1 - 1] : idb + (o1 - o0) - 1)
+                                       : idb - 1;
+    const bool prune = A.mask && A.mask[k];
+    const uint32_t tpres = prune ? A.thr_pres[k] : 0;
+    uint64_t q = cnt[k], vq = vcnt[k];
+    uint64_t kept = 0, first_id = 0, last_id = 0;
+    for (uint64_t b = o0; b < o1; b += WAVE_SZ) {
+      const uint64_t p = b + lane();
+      const bool in = p < o1;
+      const bool keep = in && (!prune || survives(A.L, p, A, k, tpres));
+      const uint64_t m = __ballot(keep);
+      if (!m) continue;
+      const uint64_t vl = keep ? var_len(A.L, p) : 0;
+      const uint64_t vincl = A.L.var_off ? wave_incl_scan(vl) : 0;
+      const uint64_t id = in ? (A.L.op_id ? A.L.op_id[p] : idb + (p - o0)) : 0;
+      if (keep) put_op(A.L, p, O, q + __popcll(m & lt), id, vq + vincl - vl);
+      const uint32_t lo = __ffsll((unsigned long long)m) - 1, hi = 63 - __clzll((long long)m);
+      const uint64_t id_lo = wave_bcast(id, lo), id_hi = wave_bcast(id, hi);
+      if (kept == 0) first_id = id_lo;
+      last_id = id_hi;
+      kept += __popcll(m);
+      q += __popcll(m);
+      vq += wave_bcast(vincl, 63);
+    }
+    uint64_t nn = 0;
+    uint32_t ntype = 0, nflags = 0;
+    if (A.N.key_off) {
+      const uint64_t n0 = A.N.key_off[k], n1 = A.N.key_off[k + 1];
+      nn = n1 - n0;
+      ntype = A.N.key_type ? A.N.key_type[k] : 0;
+      nflags = A.N.key_flags ? A.N.key_flags[k] : 0;
+      for (uint64_t b = n0; b < n1; b += WAVE_SZ) {
+        const uint64_t p = b + lane();
+        const bool in = p < n1;
+        const uint64_t vl = in ? var_len(A.N, p) : 0;
+        const uint64_t vincl = A.N.var_off ? wave_incl_scan(vl) : 0;
+        // op_insert_gc: NewId = ets:update_counter(OpsCache, Key, {3, 1})
+        if (in) put_op(A.N, p, O, q + lane(), counter + 1 + (p - n0), vq + vincl - vl);
+        const uint64_t w = (n1 - b) < WAVE_SZ ? (n1 - b) : WAVE_SZ;
+        q += w;
+        vq += wave_bcast(vincl, 63);
+      }
+    }
+    if (lane() == 0) {
+      const uint64_t nops_old = o1 - o0;
+      const uint32_t otype = A.L.key_type[k];
+      const uint32_t oflags = A.L.key_flags ? A.L.key_flags[k] : 0;
+      const bool mixed = nops_old && nn && ntype != otype;
+      O.key_type[k] = (uint8_t)(nops_old ? otype : (nn ? ntype : otype));
+      O.key_flags[k] = (uint8_t)(oflags | nflags | (mixed ? AM_KEY_MIXED_TYPES : 0));
+      O.counter[k] = counter + nn;
+      O.key_id_base[k] = kept ? first_id : counter + 1;
+      // ids stay dense from key_id_base iff the survivors are consecutive and end at OpCounter
+      const bool gap = kept && (last_id - first_id + 1 != kept || (nn && last_id != counter));
+      O.gap[k] = gap ? 1 : 0;
+      uint8_t f = 0;
+      if (prune && !kept) f |= AM_GC_PRUNED_ALL;  // check_filter's NewSize == 0 (:580)
+      if ((counter + nn) / OPS_THRESHOLD > counter / OPS_THRESHOLD) f |= AM_GC_TRIGGER;
+      if (O.gc_flags) O.gc_flags[k] = f;
+    }
+  }
+}
+
+unsigned grid_keys(uint64_t n_keys) {
+  const uint64_t g = (n_keys + 3) / 4;  // 4 waves per 256-thread block
+  return (unsigned)(g == 0 ? 1 : g < 8192 ? g : 8192);
+}
+
+}  // namespace
+
+extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *dev_new, const uint8_t *prune_mask,
+                               const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags, am_store **out) {
+  if (!c || !st || !out) return AM_ERR_INVALID;
+  const am_op_log &L = st->dev;
+  if (prune_mask && (!thr_vc || !thr_pres)) {
+    am_set_error("am_store_update: prune_mask needs thr_vc and thr_pres");
+    return AM_ERR_INVALID;
+  }
+  if (dev_new && (!dev_new->key_off || dev_new->n_keys != L.n_keys || dev_new->n_dc != L.n_dc ||
+                  (dev_new->n_ops && (!dev_new->op_meta || !dev_new->commit_time || !dev_new->snap_vc || !dev_new->p0)))) {
+    am_set_error("am_store_update: the new-op log must be CSR over the store's keys with the same n_dc");
+    return AM_ERR_INVALID;
+  }
+  AM_HIP(hipSetDevice(c->device));
+  const uint64_t nk = L.n_keys;
+  UpdArgs A{};
+  A.L = L;
+  if (dev_new) A.N = *dev_new;
+  A.counter = st->counter;
+  A.mask = prune_mask;
+  A.thr_vc = thr_vc;
+  A.thr_pres = thr_pres;
+
+  // ---- pass 1: counts + exclusive scans
+  uint64_t *cnt = nullptr, *vcnt = nullptr;
+  uint8_t *gap = nullptr, *gap_max = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_b = 0, t2 = 0;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(c->stream);
+    if (cnt) (void)hipFree(cnt);
+    if (vcnt) (void)hipFree(vcnt);
+    if (gap) (void)hipFree(gap);
+    if (gap_max) (void)hipFree(gap_max);
+    if (tmp) (void)hipFree(tmp);
+  };
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, cnt, cnt, nk + 1, c->stream) != hipSuccess ||
+      hipcub::DeviceReduce::Max(nullptr, t2, gap, gap_max, nk ? nk : 1, c->stream) != hipSuccess) {
+    am_set_error("am_store_update: scan sizing failed");
+    return AM_ERR_HIP;
+  }
+  if (t2 > tmp_b) tmp_b = t2;
+  if (hipMalloc((void **)&cnt, (nk + 1) * 8) != hipSuccess || hipMalloc((void **)&vcnt, (nk + 1) * 8) != hipSuccess ||
+      hipMalloc((void **)&gap, nk + 1) != hipSuccess || hipMalloc((void **)&gap_max, 8) != hipSuccess ||
+      hipMalloc(&tmp, tmp_b + 16) != hipSuccess) {
+    cleanup();
+    am_set_error("am_store_update: out of device memory");
+    return AM_ERR_NOMEM;
+  }
+  uint64_t tot[2] = {0, 0};
+  bool ok = hipMemsetAsync(cnt + nk, 0, 8, c->stream) == hipSuccess &&
+            hipMemsetAsync(vcnt + nk, 0, 8, c->stream) == hipSuccess &&
+            hipMemsetAsync(gap, 0, nk + 1, c->stream) == hipSuccess;
+  if (ok && nk) {
+    hipLaunchKernelGGL(k_upd_count, dim3(grid_keys(nk)), dim3(256), 0, c->stream, A, cnt, vcnt);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  ok = ok && hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, cnt, cnt, nk + 1, c->stream) == hipSuccess &&
+       hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, vcnt, vcnt, nk + 1, c->stream) == hipSuccess &&
+       hipMemcpyAsync(&tot[0], cnt + nk, 8, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+       hipMemcpyAsync(&tot[1], vcnt + nk, 8, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+       hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) {
+    cleanup();
+    am_set_error("am_store_update: count pass failed");
+    return AM_ERR_HIP;
+  }
+  const uint64_t n_out = tot[0], v_out = tot[1];
+
+  // ---- the new store's columns (padded like am_store_create)
+  am_store *ns = new am_store();
+  ns->ctx = c;
+  am_op_log &d = ns->dev;
+  const uint64_t na = am_round_up(n_out, AM_OP_PAD) + AM_OP_PAD;
+  const bool has_pres = L.snap_pres || (dev_new && dev_new->snap_pres);
+  const bool has_txid = L.op_txid || (dev_new && dev_new->op_txid);
+  const bool has_var = L.var_off || (dev_new && dev_new->var_off);
+  d.n_dc = L.n_dc;
+  d.n_keys = nk;
+  d.n_ops = n_out;
+  d.n_var = has_var ? v_out : 0;
+  d.snap_stride = na;
+  int rc = AM_OK;
+  auto alloc = [&](size_t bytes) -> void * {
+    void *p = nullptr;
+    if (rc) return nullptr;
+    rc = am_dev_alloc(c, bytes, &p);
+    if (rc) return nullptr;
+    ns->allocs.push_back(p);
+    if (hipMemsetAsync(p, 0, bytes, c->stream) != hipSuccess) rc = AM_ERR_HIP;
+    return p;
+  };
+  OutCols O{};
+  O.stride = na;
+  O.key_id_base = (uint64_t *)alloc(nk * 8 + 8);
+  O.counter = (uint64_t *)alloc(nk * 8 + 8);
+  O.key_type = (uint8_t *)alloc(nk + 8);
+  O.key_flags = (uint8_t *)alloc(nk + 8);
+  O.gc_flags = gc_flags;
+  O.gap = gap;
+  O.op_meta = (uint8_t *)alloc(na);
+  O.commit_time = (uint64_t *)alloc(na * 8);
+  O.snap_vc = (uint64_t *)alloc((size_t)L.n_dc * na * 8);
+  O.snap_pres = has_pres ? (uint32_t *)alloc(na * 4) : nullptr;
+  O.op_txid = has_txid ? (uint64_t *)alloc(na * 8) : nullptr;
+  O.op_id = (uint64_t *)alloc(na * 8);
+  O.p0 = (uint64_t *)alloc(na * 8);
+  O.p1 = (uint64_t *)alloc(na * 8);
+  O.var_off = has_var ? (uint64_t *)alloc((n_out + 1) * 8) : nullptr;
+  O.var_data = has_var ? (uint64_t *)alloc(v_out * 8 + 32) : nullptr;
+  uint64_t *key_off = (uint64_t *)alloc((nk + 1) * 8);
+  if (rc) {
+    cleanup();
+    am_store_destroy(ns);
+    return rc;
+  }
+  uint8_t any_gap = 0;
+  ok = hipMemcpyAsync(key_off, cnt, (nk + 1) * 8, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
+  if (ok && has_var) ok = hipMemcpyAsync(O.var_off + n_out, vcnt + nk, 8, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
+  if (ok && nk) {
+    hipLaunchKernelGGL(k_upd_scatter, dim3(grid_keys(nk)), dim3(256), 0, c->stream, A, cnt, vcnt, O);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  ok = ok && hipcub::DeviceReduce::Max(tmp, tmp_b, gap, gap_max, nk ? nk : 1, c->stream) == hipSuccess &&
+       hipMemcpyAsync(&any_gap, gap_max, 1, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+       hipStreamSynchronize(c->stream) == hipSuccess;
+  cleanup();
+  if (!ok) {
+    am_store_destroy(ns);
+    am_set_error("am_store_update: scatter pass failed");
+    return AM_ERR_HIP;
+  }
+  d.key_off = key_off;
+  d.key_id_base = O.key_id_base;
+  d.key_type = O.key_type;
+  d.key_flags = O.key_flags;
+  d.op_meta = O.op_meta;
+  d.commit_time = O.commit_time;
+  d.snap_vc = O.snap_vc;
+  d.snap_pres = O.snap_pres;
+  d.op_txid = O.op_txid;
+  d.op_id = any_gap ? O.op_id : nullptr;  // dense ids keep the kernels on their fast paths
+  d.p0 = O.p0;
+  d.p1 = O.p1;
+  d.var_off = O.var_off;
+  d.var_data = O.var_data;
+  ns->counter = O.counter;
+  rc = am_store_pack(ns);
+  if (rc) {
+    am_store_destroy(ns);
+    return rc;
+  }
+  *out = ns;
+  return AM_OK;
+}

@@ -47,6 +47,8 @@ struct am_store {
   am_ctx *ctx = nullptr;
   am_op_log dev{};               // device view
   std::vector<void *> allocs;    // owned device allocations
+  uint64_t *counter = nullptr;   // [n_keys] OpCounter (ops-cache tuple element 3) after
+                                 // am_store_update; null => the newest op's id
 };
 
 void am_set_error(const char *fmt, ...);

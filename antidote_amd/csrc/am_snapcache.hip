@@ -216,6 +216,30 @@ ScView view(const am_snapcache *c) {
 }
 unsigned grid(uint64_t n) { return (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096); }
 
+// snapshot_insert_gc/4's threshold (src/materializer_vnode.erl:522-527): PrunedSnapshots =
+// sublist(Dict, 1, SNAPSHOT_MIN) (newest first), CommitTime = vectorclock:min over them
+// (dict merge: a DC present in any of the clocks is kept, with the min over those having it)
+__global__ void k_sc_threshold(ScView C, uint8_t *mask, uint64_t *thr_vc, uint32_t *thr_pres) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < C.n_keys;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t cnt = C.cnt[k];
+    const uint32_t m = (cnt == ABSENT) ? 0 : (cnt < SMIN ? cnt : SMIN);
+    uint32_t pres = 0;
+    for (uint32_t e = 0; e < m; ++e) pres |= C.pres[k * CAP + e];
+    for (uint32_t d = 0; d < C.n_dc; ++d) {
+      uint64_t t = ~0ull;
+      for (uint32_t e = 0; e < m; ++e)
+        if ((C.pres[k * CAP + e] >> d) & 1u) {
+          const uint64_t v = C.vc[(k * CAP + e) * C.n_dc + d];
+          t = v < t ? v : t;
+        }
+      thr_vc[(uint64_t)d * C.n_keys + k] = ((pres >> d) & 1u) ? t : 0;
+    }
+    thr_pres[k] = pres;
+    mask[k] = m ? 1 : 0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -312,6 +336,16 @@ int am_snapcache_read(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am
   hipLaunchKernelGGL(k_sc_release, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B);
   AM_HIP(hipGetLastError());
   return rc;
+}
+
+int am_snapcache_gc_threshold(am_ctx *ctx, const am_snapcache *c, uint8_t *mask, uint64_t *thr_vc,
+                              uint32_t *thr_pres) {
+  if (!ctx || !c || !mask || !thr_vc || !thr_pres) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(ctx->device));
+  if (c->n_keys == 0) return AM_OK;
+  hipLaunchKernelGGL(k_sc_threshold, dim3(grid(c->n_keys)), dim3(256), 0, ctx->stream, view(c), mask, thr_vc, thr_pres);
+  AM_HIP(hipGetLastError());
+  return AM_OK;
 }
 
 int am_snapcache_get(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t *n_entries, uint64_t *vc,

@@ -4,6 +4,8 @@
         -> Materializer.materialize(type, txid, min_snapshot_time, response)
     materializer_vnode:read/6 batched   (src/materializer_vnode.erl:96-102)
         -> Materializer.read_batch(store, reads)
+    materializer_vnode:op_insert_gc/3 + prune_ops/2 (src/materializer_vnode.erl:565-647)
+        -> Store.update(new_log, prune)
     stable_time_functions:get_min_time/1 + meta_data_sender:update_stable/3
         -> antidote_amd.gst
 
@@ -31,6 +33,85 @@ class Store:
         abi.check(abi.lib().am_store_log(self.handle, ctypes.byref(s)), "am_store_log")
         return s
 
+    def update(self, new_log: Optional[HostLog] = None, prune: Any = None):
+        """Op-cache ingestion + GC (am_store_update): returns (new Store, gc_flags[n_keys]).
+
+        prune: None, a SnapshotCache (its snapshot_insert_gc thresholds, computed on the
+        device by am_snapcache_gc_threshold), or host arrays (mask[n_keys], thr_vc[n_dc][n_keys],
+        thr_pres[n_keys]).  new_log: ops appended per key (op_insert_gc/3), ids assigned."""
+        import numpy as np
+        L = self.mat.L
+        n_keys = int(self.device_log().n_keys)
+        bufs: List[_DevBuf] = []
+        tmp_store = None
+        try:
+            flags = _DevBuf(self.mat, max(n_keys, 1))
+            bufs.append(flags)
+            mask = thr = pres = None
+            if isinstance(prune, SnapshotCache):
+                mask, thr, pres = (_DevBuf(self.mat, max(n_keys, 1)), _DevBuf(self.mat, max(n_keys, 1) * 8 * self.n_dc),
+                                   _DevBuf(self.mat, max(n_keys, 1) * 4))
+                bufs += [mask, thr, pres]
+                abi.check(L.am_snapcache_gc_threshold(self.mat.ctx, prune.handle, mask.ptr, thr.ptr, pres.ptr),
+                          "am_snapcache_gc_threshold")
+            elif prune is not None:
+                m, t, pr = prune
+                mask = _DevBuf.of(self.mat, np.ascontiguousarray(m, np.uint8))
+                thr = _DevBuf.of(self.mat, np.ascontiguousarray(t, np.uint64))
+                pres = _DevBuf.of(self.mat, np.ascontiguousarray(pr, np.uint32))
+                bufs += [mask, thr, pres]
+            new_dev = None
+            if new_log is not None:
+                tmp_store = self.mat.store(new_log)
+                new_dev = tmp_store.device_log()
+            h = ctypes.c_void_p()
+            abi.check(L.am_store_update(self.mat.ctx, self.handle, ctypes.byref(new_dev) if new_dev is not None else None,
+                                        mask.ptr if mask else None, thr.ptr if thr else None,
+                                        pres.ptr if pres else None, flags.ptr, ctypes.byref(h)), "am_store_update")
+            out = np.zeros(max(n_keys, 1), np.uint8)
+            flags.download(out)
+            return Store(self.mat, h, self.n_dc), out[:n_keys]
+        finally:
+            for b in bufs:
+                b.free()
+            if tmp_store is not None:
+                tmp_store.close()
+
+    def download(self) -> Dict[str, Any]:
+        """The device log's columns as numpy arrays (for parity checks); op_id is always
+        filled (dense ids from key_id_base when the store keeps no explicit column)."""
+        import numpy as np
+        s = self.device_log()
+        nk, n, nd = int(s.n_keys), int(s.n_ops), int(s.n_dc)
+        stride = int(s.snap_stride) or n
+
+        def get(ptr, count, dt):
+            a = np.zeros(max(count, 1), dt)
+            if ptr and count:
+                abi.check(self.mat.L.am_memcpy_d2h(self.mat.ctx, a.ctypes.data, ptr, count * a.itemsize), "d2h")
+            return a[:count]
+        key_off = get(s.key_off, nk + 1, np.uint64)
+        out = {"key_off": key_off, "key_type": get(s.key_type, nk, np.uint8),
+               "key_flags": get(s.key_flags, nk, np.uint8) if s.key_flags else np.zeros(nk, np.uint8),
+               "op_meta": get(s.op_meta, n, np.uint8), "commit_time": get(s.commit_time, n, np.uint64),
+               "snap_vc": get(s.snap_vc, nd * stride, np.uint64).reshape(nd, stride)[:, :n] if n else np.zeros((nd, 0), np.uint64),
+               "snap_pres": get(s.snap_pres, n, np.uint32) if s.snap_pres else None,
+               "op_txid": get(s.op_txid, n, np.uint64) if s.op_txid else None,
+               "p0": get(s.p0, n, np.uint64), "p1": get(s.p1, n, np.uint64),
+               "var_off": get(s.var_off, n + 1, np.uint64) if s.var_off else None,
+               "var_data": get(s.var_data, int(s.n_var), np.uint64) if s.var_off else None,
+               "explicit_op_id": bool(s.op_id)}
+        if s.op_id:
+            out["op_id"] = get(s.op_id, n, np.uint64)
+        else:
+            idb = get(s.key_id_base, nk, np.uint64) if s.key_id_base else np.ones(nk, np.uint64)
+            ids = np.zeros(n, np.uint64)
+            for k in range(nk):
+                o0, o1 = int(key_off[k]), int(key_off[k + 1])
+                ids[o0:o1] = np.arange(o1 - o0, dtype=np.uint64) + idb[k]
+            out["op_id"] = ids
+        return out
+
     def close(self):
         if self.handle:
             abi.lib().am_store_destroy(self.handle)
@@ -41,6 +122,34 @@ class Store:
             self.close()
         except Exception:
             pass
+
+
+class _DevBuf:
+    """A device allocation through the library's own allocator (am_dev_alloc)."""
+
+    def __init__(self, mat: "Materializer", nbytes: int):
+        self.mat, self.nbytes, self.p = mat, nbytes, ctypes.c_void_p()
+        abi.check(mat.L.am_dev_alloc(mat.ctx, nbytes, ctypes.byref(self.p)), "am_dev_alloc")
+
+    @property
+    def ptr(self):
+        return self.p.value
+
+    @classmethod
+    def of(cls, mat, arr):
+        b = cls(mat, max(arr.nbytes, 1))
+        if arr.nbytes:
+            abi.check(mat.L.am_memcpy_h2d(mat.ctx, b.ptr, arr.ctypes.data, arr.nbytes), "am_memcpy_h2d")
+        return b
+
+    def download(self, arr):
+        abi.check(self.mat.L.am_memcpy_d2h(self.mat.ctx, arr.ctypes.data, self.ptr, min(arr.nbytes, self.nbytes)),
+                  "am_memcpy_d2h")
+
+    def free(self):
+        if self.p:
+            self.mat.L.am_dev_free(self.mat.ctx, self.p)
+            self.p = ctypes.c_void_p()
 
 
 class SnapshotCache:

@@ -29,6 +29,11 @@
  *                           get_smaller/2 + insert_bigger/3, materialize_snapshot/7,
  *                           internal_store_ss/4 (src/materializer_vnode.erl:342-509,
  *                           src/vector_orddict.erl:75-140)
+ *   am_store_update         op-cache ingestion + GC: materializer_vnode:op_insert_gc/3
+ *                           appends (src/materializer_vnode.erl:622-647) and prune_ops/2
+ *                           + check_filter/7 (:565-604) as one batched log rebuild
+ *   am_snapcache_gc_threshold  the prune threshold of snapshot_insert_gc/4 (:515-535):
+ *                           vectorclock:min over the first SNAPSHOT_MIN cached snapshots
  *   am_key_partition        log_utilities:get_key_partition/1 for integer keys
  *                           (src/log_utilities.erl:60-79,100-118)
  *
@@ -283,6 +288,33 @@ int am_snapcache_read_host(am_ctx *ctx, am_snapcache *cache, const am_store *st,
  * *n_entries = AM_SNAPCACHE_ABSENT before the key's first read.  NULL arrays are skipped. */
 int am_snapcache_get(am_ctx *ctx, const am_snapcache *cache, uint64_t key, uint32_t *n_entries, uint64_t *vc,
                      uint32_t *pres, int64_t *last_op, int64_t *v0, uint64_t *v1, uint8_t *vflag);
+
+/* The prune threshold snapshot_insert_gc/4 computes (src/materializer_vnode.erl:519-527):
+ * for each key with cached snapshots, Thr = vectorclock:min (dict merge: a DC present in
+ * any clock is kept) over the newest min(n, SNAPSHOT_MIN) entries.  Device outputs:
+ * mask[n_keys] (1 = the key has a threshold), thr_vc[n_dc][n_keys], thr_pres[n_keys] --
+ * exactly the prune arguments of am_store_update. */
+int am_snapcache_gc_threshold(am_ctx *ctx, const am_snapcache *cache, uint8_t *mask, uint64_t *thr_vc,
+                              uint32_t *thr_pres);
+
+/* ---- op-cache ingestion + garbage collection ----
+ * Builds a new store from `st` (st is unchanged; destroy it when no read uses it):
+ *   1. prune_ops/2 (src/materializer_vnode.erl:565-604): for keys with prune_mask[k] != 0
+ *      only ops with materializer:belongs_to_snapshot_op(Thr_k, CommitTime, SnapshotTime)
+ *      (src/materializer.erl:102-106) survive, in order, keeping their op ids;
+ *   2. op_insert_gc/3 (:622-647): the ops of dev_new (CSR over the same keys, oldest ->
+ *      newest; its op_id column is ignored) are appended with ids OpCounter+1, +2, ...
+ * Either step may be skipped (dev_new / prune_mask NULL).  Device pointers: prune_mask
+ * [n_keys], thr_vc [n_dc][n_keys], thr_pres [n_keys]; gc_flags [n_keys] (or NULL) receives
+ * AM_GC_* per key.  Differences from the ETS tuple: no ListLen sizing (the log is exactly
+ * sized), and a key whose ops are all pruned keeps 0 ops (flag AM_GC_PRUNED_ALL) where
+ * prune_ops keeps element(FIRST_OP+Len), a 0 placeholder (:580-583).  Blocks. */
+#define AM_GC_PRUNED_ALL 0x1u  /* every op of the key was pruned                          */
+#define AM_GC_TRIGGER 0x2u     /* some NewId rem OPS_THRESHOLD == 0: op_insert_gc would have
+                                  run a GC read (:635) -- the caller's cue to prune next    */
+#define AM_OPS_THRESHOLD 50    /* src/materializer_vnode.erl:41 */
+int am_store_update(am_ctx *ctx, const am_store *st, const am_op_log *dev_new, const uint8_t *prune_mask,
+                    const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags, am_store **out);
 
 /* ---- GST (global stable time) ---- */
 /* lanes[0..n_dc-1] = per-DC min over the partitions that have the DC (absent = UINT64_MAX);
