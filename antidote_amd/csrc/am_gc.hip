@@ -296,34 +296,37 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   d.n_var = has_var ? v_out : 0;
   d.snap_stride = na;
   int rc = AM_OK;
-  auto alloc = [&](size_t bytes) -> void * {
+  // every element below `used` is written by k_upd_scatter; only the pad tail is zeroed
+  auto alloc = [&](size_t bytes, size_t used) -> void * {
     void *p = nullptr;
     if (rc) return nullptr;
     rc = am_dev_alloc(c, bytes, &p);
     if (rc) return nullptr;
     ns->allocs.push_back(p);
-    if (hipMemsetAsync(p, 0, bytes, c->stream) != hipSuccess) rc = AM_ERR_HIP;
+    if (bytes > used && hipMemsetAsync((char *)p + used, 0, bytes - used, c->stream) != hipSuccess) rc = AM_ERR_HIP;
     return p;
   };
   OutCols O{};
   O.stride = na;
-  O.key_id_base = (uint64_t *)alloc(nk * 8 + 8);
-  O.counter = (uint64_t *)alloc(nk * 8 + 8);
-  O.key_type = (uint8_t *)alloc(nk + 8);
-  O.key_flags = (uint8_t *)alloc(nk + 8);
+  O.key_id_base = (uint64_t *)alloc(nk * 8 + 8, nk * 8);
+  O.counter = (uint64_t *)alloc(nk * 8 + 8, nk * 8);
+  O.key_type = (uint8_t *)alloc(nk + 8, nk);
+  O.key_flags = (uint8_t *)alloc(nk + 8, nk);
   O.gc_flags = gc_flags;
   O.gap = gap;
-  O.op_meta = (uint8_t *)alloc(na);
-  O.commit_time = (uint64_t *)alloc(na * 8);
-  O.snap_vc = (uint64_t *)alloc((size_t)L.n_dc * na * 8);
-  O.snap_pres = has_pres ? (uint32_t *)alloc(na * 4) : nullptr;
-  O.op_txid = has_txid ? (uint64_t *)alloc(na * 8) : nullptr;
-  O.op_id = (uint64_t *)alloc(na * 8);
-  O.p0 = (uint64_t *)alloc(na * 8);
-  O.p1 = (uint64_t *)alloc(na * 8);
-  O.var_off = has_var ? (uint64_t *)alloc((n_out + 1) * 8) : nullptr;
-  O.var_data = has_var ? (uint64_t *)alloc(v_out * 8 + 32) : nullptr;
-  uint64_t *key_off = (uint64_t *)alloc((nk + 1) * 8);
+  O.op_meta = (uint8_t *)alloc(na, n_out);
+  O.commit_time = (uint64_t *)alloc(na * 8, n_out * 8);
+  O.snap_vc = (uint64_t *)alloc((size_t)L.n_dc * na * 8, (size_t)L.n_dc * na * 8);  // DC tails zeroed below
+  O.snap_pres = has_pres ? (uint32_t *)alloc(na * 4, n_out * 4) : nullptr;
+  O.op_txid = has_txid ? (uint64_t *)alloc(na * 8, n_out * 8) : nullptr;
+  O.op_id = (uint64_t *)alloc(na * 8, n_out * 8);
+  O.p0 = (uint64_t *)alloc(na * 8, n_out * 8);
+  O.p1 = (uint64_t *)alloc(na * 8, n_out * 8);
+  O.var_off = has_var ? (uint64_t *)alloc((n_out + 1) * 8, (n_out + 1) * 8) : nullptr;
+  O.var_data = has_var ? (uint64_t *)alloc(v_out * 8 + 32, v_out * 8) : nullptr;
+  uint64_t *key_off = (uint64_t *)alloc((nk + 1) * 8, (nk + 1) * 8);
+  for (uint32_t dd = 0; !rc && dd < L.n_dc && na > n_out; ++dd)
+    if (hipMemsetAsync(O.snap_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 8, c->stream) != hipSuccess) rc = AM_ERR_HIP;
   if (rc) {
     cleanup();
     am_store_destroy(ns);
