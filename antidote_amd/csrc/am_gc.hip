@@ -136,6 +136,10 @@ __device__ __forceinline__ void put_op(const am_op_log &S, uint64_t p, const Out
   }
 }
 
+// DK > 0: n_dc == DK -- every column of a chunk is loaded up front into registers (all
+// loads in flight before the predicate), the survivor is written from registers.
+// DK == 0: any n_dc, predicate and copy straight from memory.
+template <int DK>
 __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vcnt, OutCols O) {
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
   const uint64_t lt = (1ull << lane()) - 1ull;
@@ -149,16 +153,67 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
     const uint32_t tpres = prune ? A.thr_pres[k] : 0;
     uint64_t q = cnt[k], vq = vcnt[k];
     uint64_t kept = 0, first_id = 0, last_id = 0;
+    constexpr int DR = DK > 0 ? DK : 1;
+    uint64_t thr[DR];
+    if constexpr (DK > 0)
+      for (int d = 0; d < DK; ++d) thr[d] = (prune && ((tpres >> d) & 1u)) ? A.thr_vc[(uint64_t)d * A.L.n_keys + k] : 0;
+    const uint64_t sstride = A.L.snap_stride ? A.L.snap_stride : A.L.n_ops;
+    const uint32_t all = all_mask(A.L.n_dc);
     for (uint64_t b = o0; b < o1; b += WAVE_SZ) {
       const uint64_t p = b + lane();
       const bool in = p < o1;
-      const bool keep = in && (!prune || survives(A.L, p, A, k, tpres));
+      bool keep;
+      uint64_t x[DR], ct = 0, v0 = 0, v1 = 0;
+      uint32_t meta = 0, spres = all;
+      if constexpr (DK > 0) {
+        if (in) {
+          meta = A.L.op_meta[p];
+          ct = A.L.commit_time[p];
+          for (int d = 0; d < DK; ++d) x[d] = A.L.snap_vc[(uint64_t)d * sstride + p];
+          v0 = A.L.p0[p];
+          v1 = A.L.p1 ? A.L.p1[p] : 0;
+          if (A.L.snap_pres) spres = A.L.snap_pres[p];
+        }
+        keep = in;
+        if (in && prune) {
+          const uint32_t dc = AM_META_DC(meta);
+          const uint32_t xpres = (spres | (1u << dc)) & all;
+          bool sv = false;
+          for (int d = 0; d < DK; ++d) {
+            const uint64_t xv = (uint32_t)d == dc ? ct : x[d];
+            sv |= ((xpres >> d) & 1u) && xv > thr[d];
+          }
+          keep = sv;
+        }
+      } else {
+        keep = in && (!prune || survives(A.L, p, A, k, tpres));
+      }
       const uint64_t m = __ballot(keep);
       if (!m) continue;
       const uint64_t vl = keep ? var_len(A.L, p) : 0;
       const uint64_t vincl = A.L.var_off ? wave_incl_scan(vl) : 0;
       const uint64_t id = in ? (A.L.op_id ? A.L.op_id[p] : idb + (p - o0)) : 0;
-      if (keep) put_op(A.L, p, O, q + __popcll(m & lt), id, vq + vincl - vl);
+      if (keep) {
+        const uint64_t qq = q + __popcll(m & lt);
+        if constexpr (DK > 0) {
+          O.op_meta[qq] = (uint8_t)meta;
+          O.commit_time[qq] = ct;
+          for (int d = 0; d < DK; ++d) O.snap_vc[(uint64_t)d * O.stride + qq] = x[d];
+          if (O.snap_pres) O.snap_pres[qq] = spres;
+          if (O.op_txid) O.op_txid[qq] = A.L.op_txid ? A.L.op_txid[p] : ~0ull;
+          O.op_id[qq] = id;
+          O.p0[qq] = v0;
+          O.p1[qq] = v1;
+          if (O.var_off) {
+            uint64_t w = vq + vincl - vl;
+            O.var_off[qq] = w;
+            if (A.L.var_off)
+              for (uint64_t i = A.L.var_off[p], e = A.L.var_off[p + 1]; i < e; ++i) O.var_data[w++] = A.L.var_data[i];
+          }
+        } else {
+          put_op(A.L, p, O, qq, id, vq + vincl - vl);
+        }
+      }
       const uint32_t lo = __ffsll((unsigned long long)m) - 1, hi = 63 - __clzll((long long)m);
       const uint64_t id_lo = wave_bcast(id, lo), id_hi = wave_bcast(id, hi);
       if (kept == 0) first_id = id_lo;
@@ -336,7 +391,14 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   ok = hipMemcpyAsync(key_off, cnt, (nk + 1) * 8, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
   if (ok && has_var) ok = hipMemcpyAsync(O.var_off + n_out, vcnt + nk, 8, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
   if (ok && nk) {
-    hipLaunchKernelGGL(k_upd_scatter, dim3(grid_keys(nk)), dim3(256), 0, c->stream, A, cnt, vcnt, O);
+    const dim3 g(grid_keys(nk)), t(256);
+    switch (L.n_dc) {
+      case 1: hipLaunchKernelGGL(k_upd_scatter<1>, g, t, 0, c->stream, A, cnt, vcnt, O); break;
+      case 2: hipLaunchKernelGGL(k_upd_scatter<2>, g, t, 0, c->stream, A, cnt, vcnt, O); break;
+      case 3: hipLaunchKernelGGL(k_upd_scatter<3>, g, t, 0, c->stream, A, cnt, vcnt, O); break;
+      case 4: hipLaunchKernelGGL(k_upd_scatter<4>, g, t, 0, c->stream, A, cnt, vcnt, O); break;
+      default: hipLaunchKernelGGL(k_upd_scatter<0>, g, t, 0, c->stream, A, cnt, vcnt, O); break;
+    }
     ok = hipGetLastError() == hipSuccess;
   }
   ok = ok && hipcub::DeviceReduce::Max(tmp, tmp_b, gap, gap_max, nk ? nk : 1, c->stream) == hipSuccess &&
