@@ -13,7 +13,8 @@
 //   exclusive scans (hipcub) -> new key_off / var_off bases
 //   k_upd_scatter  one wave per key: survivors, then the key's new ops, copied column by
 //                  column with coalesced stores (positions from ballot prefix counts)
-// followed by am_store_pack (packed + record views) on the new store.  Each column is
+// with the packed view (am_packop.h) written from the same registers, then the record view
+// (am_store_pack_records) of the new store.  Each column is
 // read once and written once: HBM-bound stream compaction, no atomics.
 //
 // Deliberate differences from the ETS layout (both are ETS tuple artefacts):
@@ -23,6 +24,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include "am_internal.h"
+#include "am_packop.h"
+
+int am_store_pack_records(am_store *st);  // am_pack.hip
 
 namespace {
 
@@ -114,6 +118,8 @@ struct OutCols {
   uint64_t *commit_time, *snap_vc;
   uint32_t *snap_pres;
   uint64_t *op_txid, *op_id, *p0, *p1, *var_off, *var_data;
+  uint64_t *ct_meta;            // packed view of the new log (am_packop.h)
+  int32_t *snap_delta;
   uint64_t stride;
 };
 
@@ -121,10 +127,19 @@ __device__ __forceinline__ void put_op(const am_op_log &S, uint64_t p, const Out
                                        uint64_t vq) {
   const uint64_t ss = S.snap_stride ? S.snap_stride : S.n_ops;
   const uint32_t all = all_mask(S.n_dc);
-  O.op_meta[q] = S.op_meta[p];
-  O.commit_time[q] = S.commit_time[p];
-  for (uint32_t d = 0; d < S.n_dc; ++d) O.snap_vc[(uint64_t)d * O.stride + q] = S.snap_vc[(uint64_t)d * ss + p];
-  if (O.snap_pres) O.snap_pres[q] = S.snap_pres ? S.snap_pres[p] : all;
+  const uint32_t meta = S.op_meta[p];
+  const uint64_t ct = S.commit_time[p];
+  const uint32_t pres = S.snap_pres ? S.snap_pres[p] : all;
+  O.op_meta[q] = (uint8_t)meta;
+  O.commit_time[q] = ct;
+  bool esc = false;
+  for (uint32_t d = 0; d < S.n_dc; ++d) {
+    const uint64_t v = S.snap_vc[(uint64_t)d * ss + p];
+    O.snap_vc[(uint64_t)d * O.stride + q] = v;
+    O.snap_delta[(uint64_t)d * O.stride + q] = am_pack_delta(ct, v, ((pres & all) >> d) & 1u, esc);
+  }
+  O.ct_meta[q] = am_pack_ct_meta(ct, meta, esc);
+  if (O.snap_pres) O.snap_pres[q] = pres;
   if (O.op_txid) O.op_txid[q] = S.op_txid ? S.op_txid[p] : ~0ull;
   O.op_id[q] = id;
   O.p0[q] = S.p0[p];
@@ -198,7 +213,12 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
         if constexpr (DK > 0) {
           O.op_meta[qq] = (uint8_t)meta;
           O.commit_time[qq] = ct;
-          for (int d = 0; d < DK; ++d) O.snap_vc[(uint64_t)d * O.stride + qq] = x[d];
+          bool esc = false;
+          for (int d = 0; d < DK; ++d) {
+            O.snap_vc[(uint64_t)d * O.stride + qq] = x[d];
+            O.snap_delta[(uint64_t)d * O.stride + qq] = am_pack_delta(ct, x[d], ((spres & all) >> d) & 1u, esc);
+          }
+          O.ct_meta[qq] = am_pack_ct_meta(ct, meta, esc);
           if (O.snap_pres) O.snap_pres[qq] = spres;
           if (O.op_txid) O.op_txid[qq] = A.L.op_txid ? A.L.op_txid[p] : ~0ull;
           O.op_id[qq] = id;
@@ -379,9 +399,13 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   O.p1 = (uint64_t *)alloc(na * 8, n_out * 8);
   O.var_off = has_var ? (uint64_t *)alloc((n_out + 1) * 8, (n_out + 1) * 8) : nullptr;
   O.var_data = has_var ? (uint64_t *)alloc(v_out * 8 + 32, v_out * 8) : nullptr;
+  O.ct_meta = (uint64_t *)alloc(na * 8, n_out * 8);
+  O.snap_delta = (int32_t *)alloc((size_t)L.n_dc * na * 4, (size_t)L.n_dc * na * 4);  // DC tails zeroed below
   uint64_t *key_off = (uint64_t *)alloc((nk + 1) * 8, (nk + 1) * 8);
   for (uint32_t dd = 0; !rc && dd < L.n_dc && na > n_out; ++dd)
-    if (hipMemsetAsync(O.snap_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 8, c->stream) != hipSuccess) rc = AM_ERR_HIP;
+    if (hipMemsetAsync(O.snap_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 8, c->stream) != hipSuccess ||
+        hipMemsetAsync(O.snap_delta + (uint64_t)dd * na + n_out, 0, (na - n_out) * 4, c->stream) != hipSuccess)
+      rc = AM_ERR_HIP;
   if (rc) {
     cleanup();
     am_store_destroy(ns);
@@ -424,8 +448,10 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   d.p1 = O.p1;
   d.var_off = O.var_off;
   d.var_data = O.var_data;
+  d.ct_meta = O.ct_meta;
+  d.snap_delta = O.snap_delta;
   ns->counter = O.counter;
-  rc = am_store_pack(ns);
+  rc = am_store_pack_records(ns);  // the packed view was written by k_upd_scatter
   if (rc) {
     am_store_destroy(ns);
     return rc;

@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "am_block.h"
+#include "am_packop.h"
 
 using namespace amk;
 
@@ -27,24 +28,12 @@ __global__ void k_pack(am_op_log L, uint64_t *ct_meta, int32_t *snap_delta) {
     const uint64_t ct = L.commit_time[q];
     const uint32_t meta = L.op_meta[q];
     const uint32_t pres = L.snap_pres ? L.snap_pres[q] & all : all;
-    bool esc = ct >= AM_CT_ESC;
+    bool esc = false;
     for (uint32_t d = 0; d < L.n_dc; ++d) {
-      int32_t v = 0;
-      if ((pres >> d) & 1u) {
-        const uint64_t s = L.snap_vc[(uint64_t)d * stride + q];
-        if (s <= ct) {
-          const uint64_t diff = ct - s;
-          if (diff <= 0x7FFFFFFFull) v = (int32_t)diff;
-          else esc = true;
-        } else {
-          const uint64_t diff = s - ct;
-          if (diff <= 0x7FFFFFFFull) v = -(int32_t)diff;
-          else esc = true;
-        }
-      }
-      snap_delta[(uint64_t)d * stride + q] = v;
+      const bool pr = (pres >> d) & 1u;
+      snap_delta[(uint64_t)d * stride + q] = am_pack_delta(ct, pr ? L.snap_vc[(uint64_t)d * stride + q] : 0, pr, esc);
     }
-    ct_meta[q] = (esc ? AM_CT_ESC : ct) | ((uint64_t)meta << 56);
+    ct_meta[q] = am_pack_ct_meta(ct, meta, esc);
   }
 }
 
@@ -191,6 +180,13 @@ int build_records(am_store *st) {
 }
 
 }  // namespace
+
+// the record view only, for a store whose packed view was written by its builder (am_gc.hip)
+int am_store_pack_records(am_store *st) {
+  const char *rv = getenv("AM_RECORDS");
+  if (rv && rv[0] == '0') return AM_OK;
+  return build_records(st);
+}
 
 int am_store_pack(am_store *st) {
   am_ctx *c = st->ctx;

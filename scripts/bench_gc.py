@@ -53,7 +53,7 @@ def main():
     ms = float(np.median(times))
     print(json.dumps({"metric": "op-cache GC (prune_ops) ops/s", "ops_in": n_in, "ops_kept": n_kept,
                       "ms_per_update_wall": ms, "value": n_in / ms * 1e3, "unit": "ops/s",
-                      "alg_bytes_per_update": alg, "kernels": "k_upd_count + k_upd_scatter (+ k_pack of the new store)",
+                      "alg_bytes_per_update": alg, "kernels": "k_upd_count + k_upd_scatter (writes the packed view of the new store too)",
                       "config": {"workload": f"c2 log: LWW, {args.keys} keys x {args.ops} ops, D={n_dc}, "
                                              f"threshold = synth clock q={args.q}"}}))
     store.close()
