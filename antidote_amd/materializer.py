@@ -6,6 +6,8 @@
         -> Materializer.read_batch(store, reads)
     materializer_vnode:op_insert_gc/3 + prune_ops/2 (src/materializer_vnode.erl:565-647)
         -> Store.update(new_log, prune)
+    materializer_vnode:load_from_log_to_tables/2 + load_ops/2 (:288-319)
+        -> Materializer.load_ops(n_dc, ops_by_key, key_types)
     stable_time_functions:get_min_time/1 + meta_data_sender:update_stable/3
         -> antidote_amd.gst
 
@@ -222,6 +224,18 @@ class Materializer:
         s = log.as_struct()
         abi.check(self.L.am_store_create(self.ctx, ctypes.byref(s), ctypes.byref(h)), "am_store_create")
         return Store(self, h, log.n_dc)
+
+    def load_ops(self, n_dc: int, ops_by_key: Sequence[Sequence[Op]], key_types=None) -> Store:
+        """load_ops/2 (src/materializer_vnode.erl:312-319): every committed op of every key, in
+        log order, through op_insert_gc/3 -- one am_store_update of an empty ops cache, ids
+        1, 2, ... per key.  The write-triggered GC reads of op_insert_gc are not replayed
+        during the load (the keys come back flagged AM_GC_TRIGGER for a prune pass)."""
+        empty = self.store(HostLog(n_dc, [[] for _ in ops_by_key], key_types=key_types))
+        try:
+            st, _flags = empty.update(new_log=HostLog(n_dc, ops_by_key, key_types=key_types))
+            return st
+        finally:
+            empty.close()
 
     def synth_store(self, params: abi.am_synth_params) -> Store:
         h = ctypes.c_void_p()

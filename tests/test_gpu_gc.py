@@ -251,3 +251,30 @@ def test_gpu_gc_from_snapshot_cache(mat):
     finally:
         cache.close()
         store.close()
+
+
+def test_gpu_load_ops_bulk_rebuild(mat):
+    """load_from_log_to_tables/2 -> load_ops/2 (src/materializer_vnode.erl:288-319): replaying a
+    partition's committed ops through op_insert_gc/3 into an empty ops cache gives every key
+    ids 1..n in log order -- the same log am_store_create uploads, and the same reads."""
+    rng = random.Random(99)
+    n_dc, n_keys = 4, 40
+    types = [randlog.TYPES[k % 5] for k in range(n_keys)]
+    keys = [randlog.rand_key_ops(rng, types[k], n_dc, rng.choice([0, 1, 9, 64, 130]), partial=(k % 3 == 0))
+            for k in range(n_keys)]
+    loaded = mat.load_ops(n_dc, keys, key_types=types)
+    direct = mat.store(HostLog(n_dc, keys, key_types=types))
+    try:
+        DL, DD = loaded.download(), direct.download()
+        for k in range(n_keys):
+            assert _key_ops(DL, k) == _key_ops(DD, k), k
+            assert [i for i, _ in _key_ops(DL, k)] == list(range(1, len(keys[k]) + 1))
+        assert not DL["explicit_op_id"]
+        reads = [Read(k, types[k], {d: max(0, (keys[k][-1].commit_time if keys[k] else 30) - rng.randint(0, 40))
+                                    for d in range(n_dc)}) for k in range(n_keys)]
+        a, b = mat.read_batch(loaded, reads), mat.read_batch(direct, reads)
+        for i in range(n_keys):
+            assert a.result(i) == b.result(i), i
+    finally:
+        loaded.close()
+        direct.close()
