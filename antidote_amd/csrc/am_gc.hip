@@ -40,6 +40,7 @@ struct UpdArgs {
   const uint8_t *mask;         // [n_keys] prune this key, or null => no pruning
   const uint64_t *thr_vc;      // [n_dc][n_keys]
   const uint32_t *thr_pres;    // [n_keys]
+  uint64_t *keep_bits;         // [n_ops/64 + 2] survivor bitmap of pruned keys (count -> scatter)
 };
 
 __device__ __forceinline__ uint32_t lane() { return threadIdx.x & (WAVE_SZ - 1); }
@@ -95,8 +96,15 @@ __global__ void k_upd_count(UpdArgs A, uint64_t *cnt, uint64_t *vcnt) {
       const uint64_t p = b + lane();
       const bool in = p < o1;
       const bool keep = in && (!prune || survives(A.L, p, A, k, tpres));
-      kept += __popcll(__ballot(keep));
+      const uint64_t m = __ballot(keep);
+      kept += __popcll(m);
       if (A.L.var_off) vk += wave_sum(keep ? var_len(A.L, p) : 0);
+      if (prune && m) {  // chunk bits at op positions b..b+63 (two words; neighbours share them)
+        const uint32_t sh = (uint32_t)(b & 63);
+        if (lane() == 0) atomicOr((unsigned long long *)&A.keep_bits[b >> 6], (unsigned long long)(m << sh));
+        if (lane() == 1 && sh && (m >> (64 - sh)))
+          atomicOr((unsigned long long *)&A.keep_bits[(b >> 6) + 1], (unsigned long long)(m >> (64 - sh)));
+      }
     }
     uint64_t nn = 0, nv = 0;
     if (A.N.key_off) {
@@ -165,23 +173,30 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
                              : o1 > o0 ? (A.L.op_id ? A.L.op_id[o1 - 1] : idb + (o1 - o0) - 1)
                                        : idb - 1;
     const bool prune = A.mask && A.mask[k];
-    const uint32_t tpres = prune ? A.thr_pres[k] : 0;
     uint64_t q = cnt[k], vq = vcnt[k];
     uint64_t kept = 0, first_id = 0, last_id = 0;
     constexpr int DR = DK > 0 ? DK : 1;
-    uint64_t thr[DR];
-    if constexpr (DK > 0)
-      for (int d = 0; d < DK; ++d) thr[d] = (prune && ((tpres >> d) & 1u)) ? A.thr_vc[(uint64_t)d * A.L.n_keys + k] : 0;
     const uint64_t sstride = A.L.snap_stride ? A.L.snap_stride : A.L.n_ops;
     const uint32_t all = all_mask(A.L.n_dc);
     for (uint64_t b = o0; b < o1; b += WAVE_SZ) {
       const uint64_t p = b + lane();
       const bool in = p < o1;
-      bool keep;
+      // survivors of a pruned key come from the count pass's bitmap: a chunk with none is
+      // skipped without touching its columns, and the predicate is not evaluated again
+      uint64_t mb = 0;
+      if (prune) {
+        const uint32_t sh = (uint32_t)(b & 63);
+        const uint64_t w0 = A.keep_bits[b >> 6];
+        mb = w0 >> sh;
+        if (sh) mb |= A.keep_bits[(b >> 6) + 1] << (64 - sh);
+        if (o1 - b < WAVE_SZ) mb &= (1ull << (o1 - b)) - 1ull;
+        if (!mb) continue;
+      }
+      const bool keep = prune ? ((mb >> lane()) & 1ull) != 0 : in;
       uint64_t x[DR], ct = 0, v0 = 0, v1 = 0;
       uint32_t meta = 0, spres = all;
       if constexpr (DK > 0) {
-        if (in) {
+        if (keep) {
           meta = A.L.op_meta[p];
           ct = A.L.commit_time[p];
           for (int d = 0; d < DK; ++d) x[d] = A.L.snap_vc[(uint64_t)d * sstride + p];
@@ -189,19 +204,6 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
           v1 = A.L.p1 ? A.L.p1[p] : 0;
           if (A.L.snap_pres) spres = A.L.snap_pres[p];
         }
-        keep = in;
-        if (in && prune) {
-          const uint32_t dc = AM_META_DC(meta);
-          const uint32_t xpres = (spres | (1u << dc)) & all;
-          bool sv = false;
-          for (int d = 0; d < DK; ++d) {
-            const uint64_t xv = (uint32_t)d == dc ? ct : x[d];
-            sv |= ((xpres >> d) & 1u) && xv > thr[d];
-          }
-          keep = sv;
-        }
-      } else {
-        keep = in && (!prune || survives(A.L, p, A, k, tpres));
       }
       const uint64_t m = __ballot(keep);
       if (!m) continue;
@@ -322,6 +324,7 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
     if (vcnt) (void)hipFree(vcnt);
     if (gap) (void)hipFree(gap);
     if (gap_max) (void)hipFree(gap_max);
+    if (A.keep_bits) (void)hipFree(A.keep_bits);
     if (tmp) (void)hipFree(tmp);
   };
   if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, cnt, cnt, nk + 1, c->stream) != hipSuccess ||
@@ -332,7 +335,8 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   if (t2 > tmp_b) tmp_b = t2;
   if (hipMalloc((void **)&cnt, (nk + 1) * 8) != hipSuccess || hipMalloc((void **)&vcnt, (nk + 1) * 8) != hipSuccess ||
       hipMalloc((void **)&gap, nk + 1) != hipSuccess || hipMalloc((void **)&gap_max, 8) != hipSuccess ||
-      hipMalloc(&tmp, tmp_b + 16) != hipSuccess) {
+      hipMalloc(&tmp, tmp_b + 16) != hipSuccess ||
+      (prune_mask && hipMalloc((void **)&A.keep_bits, (L.n_ops / 64 + 2) * 8) != hipSuccess)) {
     cleanup();
     am_set_error("am_store_update: out of device memory");
     return AM_ERR_NOMEM;
@@ -340,7 +344,8 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   uint64_t tot[2] = {0, 0};
   bool ok = hipMemsetAsync(cnt + nk, 0, 8, c->stream) == hipSuccess &&
             hipMemsetAsync(vcnt + nk, 0, 8, c->stream) == hipSuccess &&
-            hipMemsetAsync(gap, 0, nk + 1, c->stream) == hipSuccess;
+            hipMemsetAsync(gap, 0, nk + 1, c->stream) == hipSuccess &&
+            (!A.keep_bits || hipMemsetAsync(A.keep_bits, 0, (L.n_ops / 64 + 2) * 8, c->stream) == hipSuccess);
   if (ok && nk) {
     hipLaunchKernelGGL(k_upd_count, dim3(grid_keys(nk)), dim3(256), 0, c->stream, A, cnt, vcnt);
     ok = hipGetLastError() == hipSuccess;
