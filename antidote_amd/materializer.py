@@ -39,8 +39,8 @@ class Store:
         """Op-cache ingestion + GC (am_store_update): returns (new Store, gc_flags[n_keys]).
 
         prune: None, a SnapshotCache (its snapshot_insert_gc thresholds, computed on the
-        device by am_snapcache_gc_threshold), or host arrays (mask[n_keys], thr_vc[n_dc][n_keys],
-        thr_pres[n_keys]).  new_log: ops appended per key (op_insert_gc/3), ids assigned."""
+        device by am_snapcache_gc_threshold), host arrays (mask[n_keys], thr_vc[n_dc][n_keys],
+        thr_pres[n_keys]), or the same as device buffers (Materializer.device_array).  new_log: ops appended per key (op_insert_gc/3), ids assigned."""
         import numpy as np
         L = self.mat.L
         n_keys = int(self.device_log().n_keys)
@@ -56,6 +56,8 @@ class Store:
                 bufs += [mask, thr, pres]
                 abi.check(L.am_snapcache_gc_threshold(self.mat.ctx, prune.handle, mask.ptr, thr.ptr, pres.ptr),
                           "am_snapcache_gc_threshold")
+            elif prune is not None and isinstance(prune[0], _DevBuf):
+                mask, thr, pres = prune        # device-resident (caller-owned)
             elif prune is not None:
                 m, t, pr = prune
                 mask = _DevBuf.of(self.mat, np.ascontiguousarray(m, np.uint8))
@@ -224,6 +226,11 @@ class Materializer:
         s = log.as_struct()
         abi.check(self.L.am_store_create(self.ctx, ctypes.byref(s), ctypes.byref(h)), "am_store_create")
         return Store(self, h, log.n_dc)
+
+    def device_array(self, arr) -> "_DevBuf":
+        """A caller-owned copy of a host array in HBM (free with .free())."""
+        import numpy as np
+        return _DevBuf.of(self, np.ascontiguousarray(arr))
 
     def load_ops(self, n_dc: int, ops_by_key: Sequence[Sequence[Op]], key_types=None) -> Store:
         """load_ops/2 (src/materializer_vnode.erl:312-319): every committed op of every key, in

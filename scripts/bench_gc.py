@@ -4,7 +4,7 @@ One update = prune_ops over every key of a 1M-key x 256-op LWW log (D = 3) at a 
 that keeps about half of each log (the synth read clock at q = 0.5), plus, with --ingest N,
 N appended ops per key (op_insert_gc).  Prints one JSON line: ops in / kept / appended, wall
 ms per update (device allocation + both kernels + the packed view of the new store), and
-the algorithmic bytes of the compaction: every input column read once (op_meta 1 +
+the algorithmic bytes of the compaction (thresholds resident in HBM, as the snapshot cache's are): every input column read once (op_meta 1 +
 commit_time 8 + snapshot_time 8*D + p0 8 + p1 8) plus every output column written once
 (the same + op_id 8).  Kernel durations come from rocprofv3 (scripts/gpu_gc.sh)."""
 import argparse
@@ -38,13 +38,14 @@ def main():
     mask = np.ones(args.keys, np.uint8)
     thr = np.repeat(np.asarray(clock, np.uint64)[:, None], args.keys, axis=1)
     pres = np.full(args.keys, (1 << n_dc) - 1, np.uint32)
-    s1, _ = store.update(prune=(mask, thr, pres))   # warm-up
+    prune = (mat.device_array(mask), mat.device_array(thr), mat.device_array(pres))  # resident in HBM
+    s1, _ = store.update(prune=prune)   # warm-up
     n_kept = int(s1.device_log().n_ops)
     s1.close()
     times = []
     for _ in range(args.steps):
         t0 = time.perf_counter()
-        s1, _ = store.update(prune=(mask, thr, pres))
+        s1, _ = store.update(prune=prune)
         times.append((time.perf_counter() - t0) * 1e3)
         s1.close()
     n_in = args.keys * args.ops
@@ -56,6 +57,8 @@ def main():
                       "alg_bytes_per_update": alg, "kernels": "k_upd_count + k_upd_scatter (writes the packed view of the new store too)",
                       "config": {"workload": f"c2 log: LWW, {args.keys} keys x {args.ops} ops, D={n_dc}, "
                                              f"threshold = synth clock q={args.q}"}}))
+    for b in prune:
+        b.free()
     store.close()
     mat.close()
 
