@@ -309,7 +309,7 @@ int am_snapcache_gc_threshold(am_ctx *ctx, const am_snapcache *cache, uint8_t *m
  * AM_GC_* per key.  Differences from the ETS tuple: no ListLen sizing (the log is exactly
  * sized), and a key whose ops are all pruned keeps 0 ops (flag AM_GC_PRUNED_ALL) where
  * prune_ops keeps element(FIRST_OP+Len), a 0 placeholder (:580-583).  Blocks. */
-#define AM_GC_PRUNED_ALL 0x1u  /* every op of the key was pruned                          */
+#define AM_GC_PRUNED_ALL 0x1u  /* check_filter kept nothing (NewSize == 0, :580), empty logs too */
 #define AM_GC_TRIGGER 0x2u     /* some NewId rem OPS_THRESHOLD == 0: op_insert_gc would have
                                   run a GC read (:635) -- the caller's cue to prune next    */
 #define AM_OPS_THRESHOLD 50    /* src/materializer_vnode.erl:41 */
