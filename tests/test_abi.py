@@ -91,3 +91,14 @@ def test_synth_host_regenerates_deterministically():
     # LWW timestamps unique per key
     ts = a.p0.reshape(50, 32)
     assert all(len(set(r.tolist())) == 32 for r in ts)
+
+
+def test_gc_entry_points_reject_bad_arguments_without_a_gpu():
+    """am_store_update / am_snapcache_gc_threshold validate before touching the device:
+    a missing context, store or output is AM_ERR_INVALID (never a silent no-op)."""
+    from antidote_amd import abi
+    L = abi.lib()
+    out = ctypes.c_void_p()
+    assert L.am_store_update(None, None, None, None, None, None, None, ctypes.byref(out)) == abi.AM_ERR_INVALID
+    assert L.am_snapcache_gc_threshold(None, None, None, None, None) == abi.AM_ERR_INVALID
+    assert abi.AM_OPS_THRESHOLD == 50 and abi.AM_GC_PRUNED_ALL == 1 and abi.AM_GC_TRIGGER == 2
