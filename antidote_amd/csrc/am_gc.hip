@@ -285,7 +285,7 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
 
 unsigned grid_keys(uint64_t n_keys) {
   const uint64_t g = (n_keys + 3) / 4;  // 4 waves per 256-thread block
-  return (unsigned)(g == 0 ? 1 : g < 8192 ? g : 8192);
+  return (unsigned)(g == 0 ? 1 : g < 65536 ? g : 65536);
 }
 
 }  // namespace
