@@ -13,6 +13,7 @@ for s in $STEPS; do
     pytest) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; ok $? pytest ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; ok $? smoke ;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err; ok $? bench ;;
+    gc) timeout -k 10 300 python scripts/bench_gc.py > $OUT/gc_bench.json 2> $OUT/gc_bench.err; ok $? gc ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1; ok $? prof ;;
   esac
 done
