@@ -16,8 +16,10 @@
 //                   earlier positions, so nothing else crosses chunks.
 //   k_big_hash      exported births -> per-read open-addressing hash on the kill key
 //   k_big_kill      each exported kill probes the hash: same key, earlier birth -> dead
-//   k_big_finish    one workgroup per big read: survivors sorted (LDS, or global scratch
-//                   when they do not fit), de-duplicated, CSR + scalar outputs
+//   k_big_finish    one workgroup per big read: survivors sorted into the reference's
+//                   order (LDS, or global scratch when they do not fit) -- AW: elem, newest
+//                   birth first, the effect's token order, base tokens last; MV: (value,
+//                   token), de-duplicated -- CSR + scalar outputs
 // Chunk-local resolution makes the global traffic proportional to what escapes a chunk:
 // for the MV register's override chain that is about one birth per chunk.
 // Bounded counters (keyed sums) use the same chunking: per-chunk LDS slot sums, flushed
@@ -62,6 +64,9 @@ struct BigSlots {  // bounded counter: ns slots per big read (P: D*D, D: D)
 struct BigRec {
   uint64_t *ba, *bb;  // births: output pair
   int32_t *bp;        // birth position (-1 = base snapshot)
+  uint32_t *bs;       // birth: index in the effect's token list (base: in the base list)
+  uint64_t *ot;       // finish: AW survivor tokens (global-scratch sort)
+  int32_t *oi;        // finish: AW survivor index (global-scratch sort payload)
   uint8_t *dead;
   uint64_t *ka, *kb;  // exported kills: kill key
   int32_t *kp;
@@ -173,6 +178,7 @@ __global__ void __launch_bounds__(1024) k_big_offsets(const uint32_t *nbig_p, Bi
 struct ChunkSmem {
   uint64_t lb_a[LB], lb_b[LB];
   int32_t lb_p[LB];
+  uint32_t lb_s[LB];
   uint64_t lk_a[LK], lk_b[LK];
   int32_t lk_p[LK];
   uint32_t ctr[8];  // [0] kills [1] births
@@ -184,9 +190,9 @@ struct ChunkSink {
   BigRec G;
   BigAcc *acc;
   uint64_t rec0;
-  __device__ void gbirth(uint64_t a, uint64_t b, int32_t pos) {
+  __device__ void gbirth(uint64_t a, uint64_t b, int32_t pos, uint32_t sub) {
     const uint64_t i = rec0 + atomicAdd(&acc->nbirth, 1u);
-    G.ba[i] = a, G.bb[i] = b, G.bp[i] = pos;
+    G.ba[i] = a, G.bb[i] = b, G.bp[i] = pos, G.bs[i] = sub;
   }
   template <int TYPE>
   __device__ void gkill(uint64_t tok, uint64_t e, int32_t pos) {
@@ -194,12 +200,13 @@ struct ChunkSink {
     G.ka[i] = tok, G.kb[i] = TYPE == AM_AWSET ? e : 0ull, G.kp[i] = pos;
   }
   __device__ void births(uint64_t e, const uint64_t *tok, uint32_t n, int32_t pos) {
-    for (uint32_t i = 0; i < n; ++i) birth(e, tok[i], pos);
+    for (uint32_t i = 0; i < n; ++i) birth_s(e, tok[i], pos, i);
   }
-  __device__ void birth(uint64_t a, uint64_t b, int32_t pos) {
+  __device__ void birth(uint64_t a, uint64_t b, int32_t pos) { birth_s(a, b, pos, 0); }
+  __device__ void birth_s(uint64_t a, uint64_t b, int32_t pos, uint32_t sub) {
     const uint32_t bi = atomicAdd(&s->ctr[1], 1u);
-    if (bi < LB) s->lb_a[bi] = a, s->lb_b[bi] = b, s->lb_p[bi] = pos;
-    else gbirth(a, b, pos);  // LDS full: unresolved, straight to the global records
+    if (bi < LB) s->lb_a[bi] = a, s->lb_b[bi] = b, s->lb_p[bi] = pos, s->lb_s[bi] = sub;
+    else gbirth(a, b, pos, sub);  // LDS full: unresolved, straight to the global records
   }
   __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
     for (uint32_t i = 0; i < n; ++i) {
@@ -256,7 +263,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
     if (TYPE != AM_BCOUNTER && c == 0 && B.base.set_off) {  // base snapshot pairs: births at -1 (no later kill in
       const uint64_t bo = B.base.set_off[r];  // this chunk can be ruled out, so global)
       const uint32_t bl = B.base.set_len[r];
-      for (uint32_t i = tid; i < bl; i += BLOCK) sink.gbirth(B.base.set_a[bo + i], B.base.set_b[bo + i], -1);
+      for (uint32_t i = tid; i < bl; i += BLOCK) sink.gbirth(B.base.set_a[bo + i], B.base.set_b[bo + i], -1, i);
     }
 
     Acc<DMAX> a;
@@ -347,7 +354,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
         else h = mid;
       }
       const bool dead = l > 0 && s.lk_a[l - 1] == qa && s.lk_b[l - 1] == qb && s.lk_p[l - 1] > s.lb_p[i];
-      if (!dead) sink.gbirth(s.lb_a[i], s.lb_b[i], s.lb_p[i]);
+      if (!dead) sink.gbirth(s.lb_a[i], s.lb_b[i], s.lb_p[i], s.lb_s[i]);
     }
     for (uint32_t i = tid; i < nk; i += BLOCK) {  // the latest kill of each key
       if (i + 1 == nk || s.lk_a[i + 1] != s.lk_a[i] || s.lk_b[i + 1] != s.lk_b[i])
@@ -400,7 +407,8 @@ __global__ void k_big_kill(const uint32_t *nbig_p, const BigRead *br, const BigA
 
 // ---- finish: survivors sorted + CSR, scalar outputs ----
 struct FinSmem {
-  uint64_t oa[SCAP], ob[SCAP];
+  uint64_t oa[SCAP], ob[SCAP], ot[SCAP];
+  int32_t oi[SCAP];
   uint32_t ctr[8];
   uint64_t red[4];
 };
@@ -447,21 +455,39 @@ __global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch
       const bool in_lds = alive <= SCAP;
       uint64_t *oa = in_lds ? s.oa : G.ka + R0.rec0;
       uint64_t *ob = in_lds ? s.ob : G.kb + R0.rec0;
+      uint64_t *ot = in_lds ? s.ot : G.ot + R0.rec0;
+      int32_t *oi = in_lds ? s.oi : G.oi + R0.rec0;
       if (tid == 0) s.ctr[0] = 0;
       __syncthreads();
       for (uint32_t i0 = 0; i0 < A.nbirth; i0 += BLOCK) {  // stable-order compaction is not
         const uint32_t i = i0 + tid;                         // needed: the sort follows
         if (i < A.nbirth && !G.dead[R0.rec0 + i]) {
           const uint32_t o = atomicAdd(&s.ctr[0], 1u);
-          oa[o] = G.ba[R0.rec0 + i];
-          ob[o] = G.bb[R0.rec0 + i];
+          const uint64_t y = R0.rec0 + i;
+          oa[o] = G.ba[y];
+          if (TYPE == AM_AWSET) {  // (elem, newest birth first, token order); base last
+            ob[o] = ((uint64_t)(uint32_t)(0x7FFFFFFF - G.bp[y]) << 32) | G.bs[y];
+            ot[o] = G.bb[y];
+            oi[o] = (int32_t)o;
+          } else {
+            ob[o] = G.bb[y];
+          }
         }
       }
       __syncthreads();
-      block_sort(oa, ob, nullptr, alive, in_lds ? SCAP : (uint32_t)R0.cap);
       const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
-      const uint32_t distinct =
-          block_write_unique(oa, ob, alive, R.value.set_a + ooff, R.value.set_b + ooff, ocap, &s.ctr[4]);
+      uint32_t distinct;
+      if (TYPE == AM_AWSET) {
+        block_sort(oa, ob, oi, alive, in_lds ? SCAP : (uint32_t)R0.cap);
+        for (uint32_t j = tid; j < alive && j < ocap; j += BLOCK) {
+          R.value.set_a[ooff + j] = oa[j];
+          R.value.set_b[ooff + j] = ot[oi[j]];
+        }
+        distinct = alive;
+      } else {
+        block_sort(oa, ob, nullptr, alive, in_lds ? SCAP : (uint32_t)R0.cap);
+        distinct = block_write_unique(oa, ob, alive, R.value.set_a + ooff, R.value.set_b + ooff, ocap, &s.ctr[4]);
+      }
       if (distinct > ocap) status = AM_ERR_CAPACITY;
       else if (tid == 0) R.value.set_len[r] = distinct;
     }
@@ -562,11 +588,12 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   rc = am_ctx_fetch(ctx, tot, 2, h);
   if (rc) return rc;
   const uint64_t n_chunks = h[0], n_rec = h[1];
-  // records: births (a, b, p, dead), kills (a, b, p) -- n_rec each; hash 2*n_rec slots
+  // records: births (a, b, p, sub, dead), kills (a, b, p) -- n_rec each; hash 2*n_rec
+  // slots; the finish pass's AW token / index scratch -- n_rec each
   const size_t rb = am_round_up(n_rec * 8, 256), r4 = am_round_up(n_rec * 4, 256), r1 = am_round_up(n_rec, 256);
   const size_t hb = am_round_up(2 * n_rec * 4, 256);
   void *recs = nullptr;
-  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 4 * rb + 2 * r4 + r1 + hb, &recs);
+  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 5 * rb + 4 * r4 + r1 + hb, &recs);
   if (rc) return rc;
   char *q = (char *)recs;
   BigRec G;
@@ -576,6 +603,9 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   G.kb = (uint64_t *)q, q += rb;
   G.bp = (int32_t *)q, q += r4;
   G.kp = (int32_t *)q, q += r4;
+  G.bs = (uint32_t *)q, q += r4;
+  G.ot = (uint64_t *)q, q += rb;
+  G.oi = (int32_t *)q, q += r4;
   G.dead = (uint8_t *)q, q += r1;
   G.H = (uint32_t *)q;
   AM_HIP(hipMemsetAsync(G.dead, 0, n_rec, ctx->stream));

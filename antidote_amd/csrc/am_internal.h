@@ -10,14 +10,14 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_HASH = 4, AM_SCR_HASHX = 5, AM_SCR_SNAP = 6, AM_N_SCR = 7 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_N_SCR = 7 };
 
 struct am_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int n_cu = 256;
-  void *scratch[AM_N_SCR] = {};  // grow-only device scratch slots (planner, row/hash hand-offs, big-read path)
+  void *scratch[AM_N_SCR] = {};  // grow-only device scratch slots (planner, row/group hand-offs, big-read path)
   size_t scratch_bytes[AM_N_SCR] = {};
   uint64_t *pinned = nullptr;    // small pinned host buffer for device -> host counters
 };
@@ -41,7 +41,6 @@ struct am_retry {
 int am_ctx_scratch(am_ctx *ctx, int slot, size_t bytes, void **out);
 // copy `n` u64 counters device -> host through the pinned buffer (synchronizes the stream)
 int am_ctx_fetch(am_ctx *ctx, const void *dev, uint32_t n_u64, uint64_t *host);
-int am_launch_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R);
 
 struct am_store {
   am_ctx *ctx = nullptr;
@@ -80,16 +79,16 @@ int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
                    uint32_t type, am_retry retry);
 int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, uint32_t type,
                   am_retry retry);  // am_big.hip: reads beyond the LDS tier
-// Token-table tier (am_hash.hip) for add-wins-set / MV-register reads over the packed and
-// record views: reads it cannot finish exactly, and logs beyond its length limit, go to
-// `next` (the LDS-sort tier, which hands logs beyond its own limit to the big-read tier).
-bool am_hash_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
-int am_launch_hash(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                   uint32_t type, am_retry next);
-struct am_setincl;
-// k_stream's set mode (am_stream.h): inclusion pass of the token-table tier
-int am_launch_stream_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                          uint32_t type, const am_setincl &X);
+// Token-group tier (am_group.hip) for add-wins-set / MV-register reads over the packed view
+// and the token-group view: rows = true is the 16-lane-row kernel for short logs, false the
+// workgroup-per-read kernel.  Reads it does not take (ungrouped keys, base-snapshot pairs,
+// longer logs; for the row kernel also anything beyond its row limits) go to `next`.
+bool am_group_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
+int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                    uint32_t type, am_retry next, bool rows);
+// the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
+int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp_a,
+                          uint64_t *grp_b, uint32_t *key_ngrp);
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
 
 // Short-read tier (am_rows.hip): reads with at most short_max ops (and error reads) are
@@ -116,7 +115,4 @@ inline bool am_batch_general(const am_op_log *L, const am_read_batch *B) {
          B->base.set_off || B->base.bc_p || B->base.bc_d || B->base.bc_p_pres || B->base.bc_d_pres;
 }
 // the packed streaming view applies (ct_meta + int32 snapshot deltas, full clocks)
-inline bool am_log_packed(const am_op_log *L) {
-  const char *pv = getenv("AM_PACKED");
-  return L->ct_meta && L->snap_delta && !L->snap_pres && !(pv && pv[0] == '0');
-}
+inline bool am_log_packed(const am_op_log *L) { return L->ct_meta && L->snap_delta && !L->snap_pres; }

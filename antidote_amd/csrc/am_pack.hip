@@ -4,13 +4,15 @@
 // bits for any realistic clock lag/skew (2^31 us = 35 min).  Ops that do not fit are
 // flagged (AM_CT_ESC) and read from the full columns, so results stay bit-exact.
 //
-// The record view (am_op_log.rec_*) flattens the add-wins-set / MV-register effects of
-// every op into (a, b, meta) records, a key's records contiguous in op order, so the set
-// kernels stream effects like any other column instead of chasing var_off -> var_data:
+// The token-group view (am_op_log.rec_* / grp_* / key_ngrp, include/antidote_mat.h)
+// flattens the add-wins-set / MV-register effects of every op into u32 birth / kill records
+// of per-key token groups, a key's records contiguous in op order, so the set kernels
+// stream effects like any other column instead of chasing var_off -> var_data:
 //   k_op_key_mark + inclusive max-scan   op -> key
-//   k_rec_count + exclusive scan         per-op record counts -> record offsets
-//   k_rec_fill                           records (malformed effects: AM_META_BAD in ct_meta)
+//   k_rec_count + exclusive scan         per-op record counts -> record offsets (malformed
+//                                        effects: AM_META_BAD in op_meta and ct_meta)
 //   k_rec_key_off                        per-key record ranges
+//   k_grp_build (am_group.hip)           per key: token groups in output order + u32 records
 #include <hipcub/hipcub.hpp>
 
 #include "am_block.h"
@@ -50,47 +52,27 @@ struct CountSink {
   __device__ void birth(uint64_t, uint64_t, int32_t) { n += 1; }
   __device__ void kills(const uint64_t *, uint32_t c, uint64_t, int32_t) { n += c; }
 };
-struct FillSink {
-  uint64_t *ra, *rb;
-  uint32_t *rm;
-  uint64_t o;
-  uint32_t opi;
-  __device__ void births(uint64_t e, const uint64_t *tok, uint32_t c, int32_t) {
-    for (uint32_t i = 0; i < c; ++i, ++o) ra[o] = e, rb[o] = tok[i], rm[o] = opi;
-  }
-  __device__ void birth(uint64_t a, uint64_t b, int32_t) { ra[o] = a, rb[o] = b, rm[o] = opi, ++o; }
-  __device__ void kills(const uint64_t *tok, uint32_t c, uint64_t e, int32_t) {
-    for (uint32_t i = 0; i < c; ++i, ++o) ra[o] = e, rb[o] = tok[i], rm[o] = opi | AM_REC_KILL;
-  }
-};
-
 template <class Sink>
 __device__ __forceinline__ bool op_effects(const am_op_log &L, uint64_t p, uint32_t type, uint32_t meta, Sink &sk) {
   if (type == AM_AWSET) return set_effects<AM_AWSET>(L, p, meta, 0, sk);
   return set_effects<AM_MVREG>(L, p, meta, 0, sk);
 }
 
-__global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, uint64_t *ct_meta) {
+__global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, uint64_t *ct_meta, uint8_t *op_meta) {
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < L.n_ops; p += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t type = L.key_type[okey[p]];
     const uint32_t meta = L.op_meta[p];
     uint64_t c = 0;
     if ((type == AM_AWSET || type == AM_MVREG) && !(meta & AM_META_BAD)) {
       CountSink cs;
-      if (op_effects(L, p, type, meta, cs)) c = cs.n;
-      else ct_meta[p] |= (uint64_t)AM_META_BAD << 56;  // Type:update/2 raises on this effect
+      if (op_effects(L, p, type, meta, cs)) {
+        c = cs.n;
+      } else {  // Type:update/2 raises on this effect: flagged in both views, no records
+        ct_meta[p] |= (uint64_t)AM_META_BAD << 56;
+        op_meta[p] = (uint8_t)(meta | AM_META_BAD);
+      }
     }
     cnt[p] = c;
-  }
-}
-
-__global__ void k_rec_fill(am_op_log L, const uint32_t *okey, const uint64_t *off, const uint64_t *ct_meta,
-                           uint64_t *ra, uint64_t *rb, uint32_t *rm) {
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < L.n_ops; p += (uint64_t)gridDim.x * blockDim.x) {
-    if (off[p + 1] == off[p] || ((ct_meta[p] >> 56) & AM_META_BAD)) continue;
-    const uint32_t k = okey[p];
-    FillSink fs{ra, rb, rm, off[p], (uint32_t)(p - L.key_off[k])};
-    op_effects(L, p, L.key_type[k], L.op_meta[p], fs);
   }
 }
 
@@ -141,7 +123,7 @@ int build_records(am_store *st) {
     hipLaunchKernelGGL(k_op_key_mark, dim3(grid_of(d.n_keys)), dim3(256), 0, c->stream, d.key_off, d.n_keys, okey);
     if (hipcub::DeviceScan::InclusiveScan(tmp, tmp_b, okey, okey, MaxOp(), n, c->stream) != hipSuccess) break;
     hipLaunchKernelGGL(k_rec_count, dim3(grid_of(n)), dim3(256), 0, c->stream, d, okey, cnt,
-                       const_cast<uint64_t *>(d.ct_meta));
+                       const_cast<uint64_t *>(d.ct_meta), const_cast<uint8_t *>(d.op_meta));
     if (hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, cnt, cnt, n + 1, c->stream) != hipSuccess) break;
     if (hipMemcpyAsync(&n_rec, cnt + n, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) break;
     if (hipStreamSynchronize(c->stream) != hipSuccess) break;
@@ -153,19 +135,21 @@ int build_records(am_store *st) {
     return AM_ERR_HIP;
   }
   rc = AM_OK;
-  void *rko = nullptr, *ra = nullptr, *rb = nullptr, *rm = nullptr;
+  void *rko = nullptr, *rg = nullptr, *ga = nullptr, *gb = nullptr, *ng = nullptr;
   rc = am_dev_alloc(c, (d.n_keys + 1) * 8, &rko);
-  if (!rc) st->allocs.push_back(rko), rc = am_dev_alloc(c, (n_rec + 4) * 8, &ra);
-  if (!rc) st->allocs.push_back(ra), rc = am_dev_alloc(c, (n_rec + 4) * 8, &rb);
-  if (!rc) st->allocs.push_back(rb), rc = am_dev_alloc(c, (n_rec + 4) * 4, &rm);
-  if (!rc) st->allocs.push_back(rm);
+  if (!rc) st->allocs.push_back(rko), rc = am_dev_alloc(c, (n_rec + 4) * 4, &rg);
+  if (!rc) st->allocs.push_back(rg), rc = am_dev_alloc(c, (n_rec + 4) * 8, &ga);
+  if (!rc) st->allocs.push_back(ga), rc = am_dev_alloc(c, (n_rec + 4) * 8, &gb);
+  if (!rc) st->allocs.push_back(gb), rc = am_dev_alloc(c, (d.n_keys + 1) * 4, &ng);
+  if (!rc) st->allocs.push_back(ng);
   if (!rc) {
-    hipLaunchKernelGGL(k_rec_fill, dim3(grid_of(n)), dim3(256), 0, c->stream, d, okey, cnt, d.ct_meta, (uint64_t *)ra,
-                       (uint64_t *)rb, (uint32_t *)rm);
     hipLaunchKernelGGL(k_rec_key_off, dim3(grid_of(d.n_keys + 1)), dim3(256), 0, c->stream, d.key_off, d.n_keys, cnt,
                        (uint64_t *)rko);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
-      am_set_error("record view: fill pass failed");
+    am_op_log v = d;
+    v.rec_key_off = (const uint64_t *)rko;
+    rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)ga, (uint64_t *)gb, (uint32_t *)ng);
+    if (!rc && (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)) {
+      am_set_error("token-group view: build pass failed");
       rc = AM_ERR_HIP;
     }
   }
@@ -173,20 +157,17 @@ int build_records(am_store *st) {
   if (rc) return rc;
   d.n_rec = n_rec;
   d.rec_key_off = (const uint64_t *)rko;
-  d.rec_a = (const uint64_t *)ra;
-  d.rec_b = (const uint64_t *)rb;
-  d.rec_meta = (const uint32_t *)rm;
+  d.rec_g = (const uint32_t *)rg;
+  d.grp_a = (const uint64_t *)ga;
+  d.grp_b = (const uint64_t *)gb;
+  d.key_ngrp = (const uint32_t *)ng;
   return AM_OK;
 }
 
 }  // namespace
 
 // the record view only, for a store whose packed view was written by its builder (am_gc.hip)
-int am_store_pack_records(am_store *st) {
-  const char *rv = getenv("AM_RECORDS");
-  if (rv && rv[0] == '0') return AM_OK;
-  return build_records(st);
-}
+int am_store_pack_records(am_store *st) { return build_records(st); }
 
 int am_store_pack(am_store *st) {
   am_ctx *c = st->ctx;
@@ -210,7 +191,5 @@ int am_store_pack(am_store *st) {
   AM_HIP(hipStreamSynchronize(c->stream));
   d.ct_meta = (const uint64_t *)ctm;
   d.snap_delta = (const int32_t *)sd;
-  const char *rv = getenv("AM_RECORDS");
-  if (rv && rv[0] == '0') return AM_OK;
   return build_records(st);
 }

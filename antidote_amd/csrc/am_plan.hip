@@ -2,9 +2,10 @@
 //
 // A read batch from a partition's read servers mixes CRDT types (each
 // materializer_vnode:read/6 call names its Type, src/materializer_vnode.erl:97-102).
-// Every type has its own kernel (k_stream: PN counter, LWW register; k_sets: add-wins
-// set, MV register, bounded counter; am_big.hip: set reads beyond the LDS tier), so a
-// mixed batch is split on the device, never on the host:
+// Every type has its own kernels (k_stream + row tier: PN counter, LWW register;
+// am_group.hip: add-wins set, MV register; row tier + k_sets: bounded counter; k_sets /
+// am_big.hip: set reads the group tier does not take), so a mixed batch is split on the
+// device, never on the host:
 //   k_plan_count    per 1024-read block: class histogram (class = kernel the read needs;
 //                   reads with an unknown type or key get their status here)
 //   k_plan_scan     one workgroup: per-class block offsets and the [begin, end) range of
@@ -121,65 +122,61 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
   }
 }
 
-// Short-read limits of the row tier (am_rows.hip); AM_ROWS=0 disables the tier (A/B),
-// AM_ROWS_SCALAR / AM_ROWS_SET override the limits (the set limit is capped by the
-// row's 64 LDS entries: one bounded-counter entry per op).
-uint32_t rows_max(bool set) {
-  const char *e = getenv("AM_ROWS");
-  if (e && e[0] == '0') return 0;
-  const char *v = getenv(set ? "AM_ROWS_SET" : "AM_ROWS_SCALAR");
-  uint32_t m = set ? 48u : 64u;
-  if (v) m = (uint32_t)strtoul(v, nullptr, 10);
-  if (set && m > 64) m = 64;
-  return m;
-}
+// Short-read limit of the row tier (am_rows.hip): at most 64 ops (one 16-lane row, 4 steps)
+// for PN / LWW, 48 for the bounded counter (the row's 64 LDS slot entries).
+constexpr uint32_t ROWS_SCALAR = 64, ROWS_BC = 48;
 
 // PN / LWW over selection S: k_stream takes the long reads and marks the short ones in a
 // per-batch mask (rows_buf + 64) for the row tier, which skips batches without any.
 int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
                uint32_t *rows_buf) {
-  const uint32_t m = rows_max(false);
-  if (m == 0) return am_launch_stream_skip(ctx, L, B, R, S, type, am_rows_cfg{});
   am_rows_cfg H;
-  H.short_max = m;
+  H.short_max = ROWS_SCALAR;
   H.mask = (uint64_t *)(rows_buf + 64);
   int rc = am_launch_stream_skip(ctx, L, B, R, S, type, H);
   if (rc) return rc;
   return am_launch_rows(ctx, L, B, R, S, type, H);
 }
 
-// Set types over selection S: row tier -> (hand-off list) token-table tier k_hsets (add-wins
-// set / MV register over the record view) -> (hand-off list) LDS-sort tier k_sets ->
-// (retry list) big-read tier.  rows_buf / hash_buf: [0] = 0, [1] = hand-off count, list at +64.
+// Set types over selection S.
+//   add-wins set / MV register: token-group tier, row kernel (short logs) -> (hand-off list)
+//     workgroup kernel -> (hand-off list) LDS-sort tier k_sets -> (retry list) big-read tier
+//   bounded counter: row tier -> (hand-off list) k_sets -> (retry list) big-read tier
+// rows_buf / grp_buf: [0] = 0, [1] = hand-off count, list at +64.
 int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
-             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *hash_buf) {
+             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf) {
   am_retry retry;
   retry.count = retry_buf;
   retry.list = retry_buf + 1;
   AM_HIP(hipMemsetAsync(retry.count, 0, sizeof(uint32_t), ctx->stream));
-  const uint32_t m = rows_max(true);
   int rc;
   am_sel cur = S;
-  if (m) {
+  if (type == AM_BCOUNTER) {
     AM_HIP(hipMemsetAsync(rows_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
     am_rows_cfg C;
-    C.short_max = m;
+    C.short_max = ROWS_BC;
     C.list = rows_buf + 64;
     C.count = rows_buf + 1;
     rc = am_launch_rows(ctx, L, B, R, S, type, C);
     if (rc) return rc;
     cur.idx = C.list;
     cur.range = rows_buf;
-  }
-  if (hash_buf && am_hash_applies(L, R, type)) {
-    AM_HIP(hipMemsetAsync(hash_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
-    am_retry next;
-    next.count = hash_buf + 1;
-    next.list = hash_buf + 64;
-    rc = am_launch_hash(ctx, L, B, R, cur, type, next);
+  } else if (grp_buf && am_group_applies(L, R, type)) {
+    AM_HIP(hipMemsetAsync(rows_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
+    AM_HIP(hipMemsetAsync(grp_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
+    am_retry n1, n2;
+    n1.count = rows_buf + 1;
+    n1.list = rows_buf + 64;
+    n2.count = grp_buf + 1;
+    n2.list = grp_buf + 64;
+    rc = am_launch_group(ctx, L, B, R, S, type, n1, true);
     if (rc) return rc;
-    cur.idx = next.list;
-    cur.range = hash_buf;
+    cur.idx = n1.list;
+    cur.range = rows_buf;
+    rc = am_launch_group(ctx, L, B, R, cur, type, n2, false);
+    if (rc) return rc;
+    cur.idx = n2.list;
+    cur.range = grp_buf;
   }
   rc = am_launch_sets(ctx, L, B, R, cur, type, retry);
   if (rc) return rc;
@@ -207,15 +204,12 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     am_set_error("n_reads %llu exceeds the 32-bit read index of one batch", (unsigned long long)n);
     return AM_ERR_INVALID;
   }
-  const char *variant = getenv("AM_KERNEL");  // "scalar" = the one-read-per-wave kernel (A/B only)
-  if (variant && strcmp(variant, "scalar") == 0 && B->type_hint <= AM_LWW) return am_launch_scalar(ctx, L, B, R);
-
   const am_sel all{};
-  void *rows_scr = nullptr, *hash_scr = nullptr;
+  void *rows_scr = nullptr, *grp_scr = nullptr;
   {
     int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
     if (!rc && B->type_hint != AM_PN && B->type_hint != AM_LWW && B->type_hint != AM_BCOUNTER)
-      rc = am_ctx_scratch(ctx, AM_SCR_HASH, (n + 64) * sizeof(uint32_t), &hash_scr);
+      rc = am_ctx_scratch(ctx, AM_SCR_GRP, (n + 64) * sizeof(uint32_t), &grp_scr);
     if (rc) return rc;
   }
   if (B->type_hint == AM_PN || B->type_hint == AM_LWW)
@@ -224,7 +218,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     void *scr = nullptr;
     int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &scr);
     if (rc) return rc;
-    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr, (uint32_t *)hash_scr);
+    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr, (uint32_t *)grp_scr);
   }
   if (B->type_hint != 0) {
     am_set_error("type_hint %u not supported", B->type_hint);
@@ -255,7 +249,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     if (t == AM_PN || t == AM_LWW)
       rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
     else
-      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr, (uint32_t *)hash_scr);
+      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr, (uint32_t *)grp_scr);
     if (rc) return rc;
   }
   return AM_OK;

@@ -13,15 +13,12 @@
 //
 // Types:
 //   PN counter / LWW register  commutative reductions in registers (am_wave.h)
-//   add-wins set / MV register births / kills appended to the row's LDS lists, then the
-//                              closed form of am_sets.hip (a birth survives iff no kill
-//                              of the same token at a later position) by a brute-force
-//                              row scan, duplicate-free rank sort, CSR write
 //   bounded counter            included (slot, amount) pairs in the row's LDS list; lane
 //                              s owns slots s, s+16, ... and sums its slots exactly
-// A read longer than the short limit, or whose births/kills do not fit the row's LDS
-// lists, is handed to the workgroup tier (k_stream for PN/LWW skips it on its own; set
-// types get it through an ordered hand-off list).
+// (short add-wins-set / MV-register reads have their own row kernel, am_group.hip).
+// A read longer than the short limit, or whose entries do not fit the row's LDS list, is
+// handed to the workgroup tier (k_stream for PN/LWW skips it on its own; the bounded
+// counter gets it through a hand-off list).
 #include "am_block.h"
 
 using namespace amk;
@@ -31,80 +28,13 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;
 constexpr int G = 16;
-constexpr uint32_t RB = 64;  // births per row
-constexpr uint32_t RK = 64;  // kills (bcounter: (slot, amount) entries) per row
+constexpr uint32_t RK = 64;  // bounded counter: (slot, amount) entries per row
 
 struct RowSmem {
-  uint64_t ba[RB], bb[RB];  // births: AW (elem, tok), MV (value, tok); later: survivors
-  int32_t bp[RB];           // birth position (-1: base snapshot); later: duplicate flag
-  uint64_t ka[RK], kb[RK];  // kills: (tok, elem) / MV (tok, 0); bcounter: amount in ka
-  int32_t kp[RK];           // kill position; bcounter: slot
-  uint32_t ctr[4];          // [0] kills / entries [1] births [2] distinct [3] overflow
+  uint64_t ka[RK];  // amount
+  int32_t kp[RK];   // slot
+  uint32_t ctr[4];  // [0] entries [2] overflow of a slot sum [3] list overflow
 };
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// ---- 16-lane row all-reductions: every lane of a row ends with the row's value.
-// Full EXEC required (DPP reads inactive lanes as 0).
-__device__ __forceinline__ uint32_t row_sum_u32(uint32_t v) {
-#define S_(C) v += dpp32<C>(v);
-  AMK_ROW_STEPS(S_)
-#undef S_
-  return v;
-}
-__device__ __forceinline__ uint32_t row_or_u32(uint32_t v) {
-#define S_(C) v |= dpp32<C>(v);
-  AMK_ROW_STEPS(S_)
-#undef S_
-  return v;
-}
-__device__ __forceinline__ uint64_t row_max_u64(uint64_t v) {
-#define S_(C) v = umax64(v, dpp64<C>(v));
-  AMK_ROW_STEPS(S_)
-#undef S_
-  return v;
-}
-__device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
-#define S_(C) v = umin64(v, dpp64<C>(v));
-  AMK_ROW_STEPS(S_)
-#undef S_
-  return v;
-}
-__device__ __forceinline__ void row_sum_i128(int64_t &hi, uint64_t &lo) {
-#define S_(C)                                            \
-  {                                                      \
-    const uint64_t wlo = dpp64<C>(lo);                   \
-    const int64_t whi = (int64_t)dpp64<C>((uint64_t)hi); \
-    add128(hi, lo, whi, wlo);                            \
-  }
-  AMK_ROW_STEPS(S_)
-#undef S_
-}
-__device__ __forceinline__ void row_max_lww(LwwVal &v) {
-#define S_(C)                                                                        \
-  {                                                                                  \
-    const uint64_t wts = dpp64<C>(v.ts), wval = dpp64<C>(v.val);                     \
-    const uint32_t whas = dpp32<C>(v.has);                                           \
-    const bool gt = whas && (!v.has || wts > v.ts || (wts == v.ts && wval > v.val)); \
-    v.ts = gt ? wts : v.ts;                                                          \
-    v.val = gt ? wval : v.val;                                                       \
-    v.has |= whas;                                                                   \
-  }
-  AMK_ROW_STEPS(S_)
-#undef S_
-}
-
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, WAVE);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, WAVE);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, uint32_t src) {
-  return (uint32_t)__shfl((int)v, (int)src, WAVE);
-}
 
 template <int TYPE>
 struct RowVal {  // per-lane value accumulator of the scalar types (unused for the others)
@@ -115,39 +45,10 @@ struct RowVal<AM_LWW> {
   using T = LwwVal;
 };
 
-// births / kills appended to the row's LDS lists; overflow -> workgroup tier
-struct RowSink {
-  RowSmem *s;
-  __device__ void births(uint64_t e, const uint64_t *tok, uint32_t n, int32_t pos) {
-    const uint32_t bi = atomicAdd(&s->ctr[1], n);
-    if (bi + n > RB) {
-      s->ctr[3] = 1;
-      return;
-    }
-    for (uint32_t i = 0; i < n; ++i) s->ba[bi + i] = e, s->bb[bi + i] = tok[i], s->bp[bi + i] = pos;
-  }
-  __device__ void birth(uint64_t a, uint64_t b, int32_t pos) {
-    const uint32_t bi = atomicAdd(&s->ctr[1], 1u);
-    if (bi >= RB) {
-      s->ctr[3] = 1;
-      return;
-    }
-    s->ba[bi] = a, s->bb[bi] = b, s->bp[bi] = pos;
-  }
-  __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
-    const uint32_t ki = atomicAdd(&s->ctr[0], n);
-    if (ki + n > RK) {
-      s->ctr[3] = 1;
-      return;
-    }
-    for (uint32_t i = 0; i < n; ++i) s->ka[ki + i] = tok[i], s->kb[ki + i] = e, s->kp[ki + i] = pos;
-  }
-};
-
 template <int DMAX>
 struct ROut {  // per-lane buffered outputs of read (batch base + lane)
   int32_t status;
-  uint32_t flags, pres, count, ign, newss, vflag, setlen, store;
+  uint32_t flags, pres, count, ign, newss, vflag, store;
   int64_t nlo;
   uint64_t ct[DMAX];
   uint64_t v0, v1;
@@ -156,10 +57,8 @@ struct ROut {  // per-lane buffered outputs of read (batch base + lane)
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                 am_rows_cfg C) {
-  constexpr bool SETS = TYPE == AM_AWSET || TYPE == AM_MVREG;
   constexpr bool BC = TYPE == AM_BCOUNTER;
-  constexpr bool LDS = SETS || BC;
-  constexpr bool REC = SETS && PACKED;  // effects from the record view (am_pack.hip)
+  constexpr bool LDS = BC;
   using V = typename RowVal<TYPE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   RowSmem *rs = LDS ? ((RowSmem *)smem_raw) + (threadIdx.x / G) : nullptr;
@@ -219,7 +118,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
     }
     const uint64_t len = off1 - off0;
     const bool mine = lane < nb && ((bmask >> lane) & 1u) && len <= C.short_max;  // error reads have len 0
-    // set types: long reads go to the workgroup tier through the ordered list
+    // bounded counter: long reads go to the workgroup tier through the hand-off list
     if (C.list) {
       const bool hand = lane < nb && !mine;
       const uint64_t hm = __ballot(hand);
@@ -234,7 +133,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
     // ---- per-lane buffered result, initialised to materialize/4 of an empty log ----
     ROut<DMAX> o;
     o.status = st, o.store = mine ? 1u : 0u;
-    o.flags = 0, o.pres = 0, o.count = 0, o.ign = 1, o.newss = 0, o.nlo = 0, o.setlen = 0;
+    o.flags = 0, o.pres = 0, o.count = 0, o.ign = 1, o.newss = 0, o.nlo = 0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) o.ct[d] = 0;
     o.v0 = 0, o.v1 = 0, o.vflag = TYPE == AM_LWW ? 1 : 0;
@@ -254,9 +153,9 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         }
       }
     }
-    // An empty log still returns the base value: sets copy the base CSR, bcounters the
-    // base slots (materialize/4 on [] applies no effect).  Done by the row below as a
-    // read with zero ops, so the value paths stay in one place.
+    // An empty log still returns the base value: bcounters copy the base slots
+    // (materialize/4 on [] applies no effect).  Done by the row below as a read with zero
+    // ops, so the value paths stay in one place.
     const bool work = mine && st == AM_OK && (len > 0 || LDS);
     const uint64_t wmask = __ballot(work);
     if (wmask) {
@@ -264,7 +163,6 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
       uint32_t s = rowbits ? (uint32_t)__builtin_ctz(rowbits) : 16u;
       // current read of the row (row-uniform values)
       uint64_t o0 = 0, o1 = 0, rj = 0, keyj = 0, t = 0;
-      uint64_t imask = 0, rk0 = 0, rk1 = 0;  // REC: included ops of the read, its record range
       Acc<DMAX> a;
       V v;
       a.reset();
@@ -277,9 +175,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         if (!upd) return;
         o0 = n0, o1 = n1, rj = nr, keyj = nk;
         t = 0;
-        imask = 0;
         if (s >= 16) return;
-        if (REC) rk0 = L.rec_key_off[keyj], rk1 = L.rec_key_off[keyj + 1];
         if (GENERAL) {
           if (B.per_read_clock) {
             u.spres = B.read_pres[rj] & allmask;
@@ -298,21 +194,6 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         if (LDS) {
           if (sl == 0) rs->ctr[0] = 0, rs->ctr[1] = 0, rs->ctr[2] = 0, rs->ctr[3] = 0;
           wave_sync();
-          if (SETS && GENERAL && B.base.set_off) {  // base snapshot pairs: births at -1
-            const uint64_t bo = B.base.set_off[rj];
-            const uint32_t bl = B.base.set_len[rj];
-            if (bl > RB) {
-              if (sl == 0) rs->ctr[3] = 1;
-            } else {
-              for (uint32_t i = sl; i < bl; i += G) {
-                rs->ba[i] = B.base.set_a[bo + i];
-                rs->bb[i] = B.base.set_b[bo + i];
-                rs->bp[i] = -1;
-              }
-              if (sl == 0) rs->ctr[1] = bl;
-            }
-            wave_sync();
-          }
         }
       };
       begin(true);
@@ -338,8 +219,8 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         }
         q.sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : allmask;
         q.tx = (GENERAL && u.has_txid) ? L.op_txid[p] : 0;
-        if (TYPE != AM_AWSET) q.p0 = L.p0[p];
-        if (TYPE != AM_AWSET && TYPE != AM_PN) q.p1 = L.p1[p];
+        q.p0 = L.p0[p];
+        if (TYPE != AM_PN) q.p1 = L.p1[p];
       };
       ROp cur, nxt;
       load_op(cur, o0 + sl, s < 16 && o0 + sl < o1);
@@ -355,7 +236,6 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
           if (fin_next) load_op(nxt, n0 + sl, s2 < 16 && n0 + sl < n1);
           else load_op(nxt, p + G, act && p + G < o1);
         }
-        bool inc = false;  // REC: the op is included (its records apply)
         if (act && p < o1) {
           // ---- one op: is_op_in_snapshot/7 + the type's effect ----
           uint32_t meta;
@@ -393,15 +273,9 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
               } else {
                 a.flags |= FLAG_BAD;
               }
-            } else if constexpr (REC) {
-              inc = true;
-            } else {
-              RowSink sink{rs};
-              if (!set_effects<TYPE>(L, p, meta, (int32_t)(p - o0), sink)) a.flags |= FLAG_BAD;
             }
           }
         }
-        if (REC) imask |= ((__ballot(inc) >> (row * G)) & 0xFFFFull) << t;
         t += G;
         const bool fin = act && o0 + t >= o1;
         if (__ballot(fin)) {
@@ -422,7 +296,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
             int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
             bool defer = false;
             uint64_t v0 = 0, v1 = 0;
-            uint32_t vflag = 0, setlen = 0;
+            uint32_t vflag = 0;
             if constexpr (TYPE == AM_PN) {
               int64_t hi = vr.hi;
               uint64_t lo = vr.lo;
@@ -517,83 +391,6 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                   }
                 }
               }
-            } else {  // add-wins set / MV register
-              if (REC && status == AM_OK) {  // the included ops' records -> births / kills
-                for (uint64_t q = rk0 + sl; q < rk1; q += G) {
-                  const uint32_t m = L.rec_meta[q];
-                  if (!((imask >> AM_REC_OP(m)) & 1u)) continue;
-                  const uint64_t ra = L.rec_a[q], rb = L.rec_b[q];
-                  if (m & AM_REC_KILL) {
-                    const uint32_t ki = atomicAdd(&rs->ctr[0], 1u);
-                    if (ki < RK) rs->ka[ki] = rb, rs->kb[ki] = ra, rs->kp[ki] = (int32_t)AM_REC_OP(m);
-                    else rs->ctr[3] = 1;
-                  } else {
-                    const uint32_t bi = atomicAdd(&rs->ctr[1], 1u);
-                    if (bi < RB) rs->ba[bi] = ra, rs->bb[bi] = rb, rs->bp[bi] = (int32_t)AM_REC_OP(m);
-                    else rs->ctr[3] = 1;
-                  }
-                }
-                wave_sync();
-              }
-              if (status == AM_OK && rs->ctr[3]) defer = true;
-              if (status == AM_OK && !defer) {
-                const uint32_t nk = rs->ctr[0], nbth = rs->ctr[1];
-                // 1. a birth survives iff no kill of its kill key at a later position
-                uint32_t alive = 0;
-                for (uint32_t m = 0; m * G < nbth; ++m) {
-                  const uint32_t i = sl + m * G;
-                  if (i < nbth) {
-                    const uint64_t qa = rs->bb[i], qb = TYPE == AM_AWSET ? rs->ba[i] : 0ull;
-                    const int32_t bpos = rs->bp[i];
-                    bool al = true;
-                    for (uint32_t k = 0; k < nk; ++k)
-                      if (rs->ka[k] == qa && rs->kb[k] == qb && rs->kp[k] > bpos) al = false;
-                    if (al) alive |= 1u << m;
-                  }
-                }
-                wave_sync();
-                // 2. compact the survivors in place (row ballots keep birth order)
-                uint32_t ns = 0;
-                for (uint32_t m = 0; m * G < nbth; ++m) {
-                  const uint32_t i = sl + m * G;
-                  const bool al = i < nbth && ((alive >> m) & 1u);
-                  uint64_t xa = 0, xb = 0;
-                  if (al) xa = rs->ba[i], xb = rs->bb[i];
-                  const uint32_t rm = (uint32_t)((__ballot(al) >> (row * G)) & 0xFFFFu);
-                  wave_sync();
-                  if (al) {
-                    const uint32_t o_ = ns + (uint32_t)__popc(rm & ((1u << sl) - 1u));
-                    rs->ba[o_] = xa, rs->bb[o_] = xb;
-                  }
-                  ns += (uint32_t)__popc(rm);
-                  wave_sync();
-                }
-                // 3. duplicate flags (the state is a set: keep first occurrences)
-                for (uint32_t i = sl; i < ns; i += G) {
-                  const uint64_t xa = rs->ba[i], xb = rs->bb[i];
-                  int32_t dup = 0;
-                  for (uint32_t k = 0; k < i; ++k)
-                    if (rs->ba[k] == xa && rs->bb[k] == xb) dup = 1;
-                  rs->bp[i] = dup;
-                  if (!dup) atomicAdd(&rs->ctr[2], 1u);
-                }
-                wave_sync();
-                // 4. rank among distinct pairs = output slot (sorted by (a, b))
-                const uint32_t ndist = rs->ctr[2];
-                const uint64_t ooff = R.value.set_off[rj], ocap = R.value.set_off[rj + 1] - ooff;
-                for (uint32_t i = sl; i < ns; i += G) {
-                  if (rs->bp[i]) continue;
-                  const uint64_t xa = rs->ba[i], xb = rs->bb[i];
-                  uint32_t rank = 0;
-                  for (uint32_t k = 0; k < ns; ++k) {
-                    const uint64_t ya = rs->ba[k], yb = rs->bb[k];
-                    if (!rs->bp[k] && (ya < xa || (ya == xa && yb < xb))) ++rank;
-                  }
-                  if (rank < ocap) R.value.set_a[ooff + rank] = xa, R.value.set_b[ooff + rank] = xb;
-                }
-                if (ndist > ocap) status = AM_ERR_CAPACITY;
-                setlen = ndist;
-              }
             }
             // NewLastOp: id of the oldest excluded candidate - 1, else get_first_id/1
             const uint64_t nops = o1 - o0;
@@ -622,7 +419,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                 const uint64_t m = mx[d] > u.C0[d] ? mx[d] : u.C0[d];
                 o.ct[d] = ((opres >> d) & 1u) ? m : 0;
               }
-              o.v0 = v0, o.v1 = v1, o.vflag = vflag, o.setlen = setlen;
+              o.v0 = v0, o.v1 = v1, o.vflag = vflag;
             }
             a.reset();
             v.reset();
@@ -653,7 +450,6 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
           R.value.v1[r] = o.v1;
           R.value.vflag[r] = (uint8_t)o.vflag;
         }
-        if (SETS) R.value.set_len[r] = o.setlen;
       }
     }
   }
@@ -662,7 +458,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
 template <int D, int TYPE, bool GENERAL, bool PACKED>
 int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
              const am_rows_cfg &C) {
-  constexpr bool LDS = TYPE == AM_AWSET || TYPE == AM_MVREG || TYPE == AM_BCOUNTER;
+  constexpr bool LDS = TYPE == AM_BCOUNTER;
   const size_t smem = LDS ? sizeof(RowSmem) * (BLOCK / G) : 0;
   static int occ = 0;
   if (occ == 0) {
@@ -700,8 +496,7 @@ template <int TYPE>
 int launch_t(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
              const am_rows_cfg &C) {
   const bool general = am_batch_general(L, B);
-  // set types take the packed view only together with the record view
-  const bool packed = am_log_packed(L) && ((TYPE != AM_AWSET && TYPE != AM_MVREG) || L->rec_key_off);
+  const bool packed = am_log_packed(L);
   if (general) return packed ? launch<TYPE, true, true>(ctx, L, B, R, S, C) : launch<TYPE, true, false>(ctx, L, B, R, S, C);
   return packed ? launch<TYPE, false, true>(ctx, L, B, R, S, C) : launch<TYPE, false, false>(ctx, L, B, R, S, C);
 }
@@ -713,8 +508,6 @@ int am_launch_rows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
   switch (type) {
     case AM_PN: return launch_t<AM_PN>(ctx, L, B, R, S, C);
     case AM_LWW: return launch_t<AM_LWW>(ctx, L, B, R, S, C);
-    case AM_AWSET: return launch_t<AM_AWSET>(ctx, L, B, R, S, C);
-    case AM_MVREG: return launch_t<AM_MVREG>(ctx, L, B, R, S, C);
     case AM_BCOUNTER: return launch_t<AM_BCOUNTER>(ctx, L, B, R, S, C);
     default: return AM_ERR_UNSUPPORTED;
   }

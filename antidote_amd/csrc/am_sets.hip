@@ -16,8 +16,14 @@
 //      effects' births / kills to LDS lists (LDS atomics for the slots);
 //   2. bitonic-sorts the kills by (token, elem, pos) in LDS;
 //   3. keeps each birth whose upper-bound lookup finds no later kill;
-//   4. bitonic-sorts the survivors by (a, b), drops duplicates (the reference
-//      state is compared as a canonical sorted rendering) and writes the CSR.
+//   4. bitonic-sorts the survivors into the reference's order and writes the CSR:
+//      AW (elem, newest birth first, the effect's token order; base tokens last, in
+//      base order) -- the orddict's token lists are ToAdd ++ (Current -- ToRemove);
+//      MV (value, token) with duplicates dropped (insert_sorted).
+// This tier serves the keys the token-group tier (am_group.hip) does not: base-snapshot
+// reads, logs outside the group view's limits, and logs that re-add a live token (where
+// it emits every surviving birth, as the list semantics do unless a later remove takes
+// only one of the copies).
 // The bounded counter (orddict:update_counter on P[{From,To}] and D[Id]) is a
 // keyed sum: exact 128-bit LDS accumulators (64-bit atomics + carry).
 // Capacity: KCAP kills / BCAP births per read live in LDS (78 KB per group);
@@ -40,7 +46,7 @@ struct Smem {
   uint64_t *ka, *kb;  // kills: token, elem (MV: 0)
   int32_t *kp;        // kill position
   uint64_t *ba, *bb;  // births: AW (elem, tok), MV (value, tok)
-  int32_t *bp;        // birth position (-1: base snapshot)
+  int32_t *bp;        // birth: (position + 1) << 16 | index in the effect's ToAdd / base list
   uint64_t *oa, *ob;  // survivors
   uint32_t *ctr;      // [0] kills [1] births [2] survivors [3] overflow [4..7] wave sums
   uint64_t *red;      // block reduction scratch [NW][8]
@@ -51,6 +57,17 @@ struct Smem {
 };
 
 // births / kills appended to the LDS lists; overflow sets ctr[3] (-> big-read tier)
+// packed birth position: op position (-1 = base snapshot) and the index within the
+// effect's token list (base: within the base list), for the AW output order
+__device__ __forceinline__ int32_t bpack(int32_t pos, uint32_t sub) {
+  return (int32_t)(((uint32_t)(pos + 1) << 16) | (sub < 0xFFFFu ? sub : 0xFFFFu));
+}
+__device__ __forceinline__ int32_t bpos(int32_t bp) { return (int32_t)((uint32_t)bp >> 16) - 1; }
+// AW output order within one elem: newest birth first, then the effect's token order
+__device__ __forceinline__ uint64_t bord(int32_t bp) {
+  return ((uint64_t)(uint32_t)(0x7FFFFFFF - bpos(bp)) << 32) | ((uint32_t)bp & 0xFFFFu);
+}
+
 struct LdsSink {
   Smem *s;
   __device__ void births(uint64_t e, const uint64_t *tok, uint32_t n, int32_t pos) {
@@ -59,7 +76,7 @@ struct LdsSink {
       s->ctr[3] = 1;
       return;
     }
-    for (uint32_t i = 0; i < n; ++i) s->ba[bi + i] = e, s->bb[bi + i] = tok[i], s->bp[bi + i] = pos;
+    for (uint32_t i = 0; i < n; ++i) s->ba[bi + i] = e, s->bb[bi + i] = tok[i], s->bp[bi + i] = bpack(pos, i);
   }
   __device__ void birth(uint64_t a, uint64_t b, int32_t pos) {
     const uint32_t bi = atomicAdd(&s->ctr[1], 1u);
@@ -67,7 +84,7 @@ struct LdsSink {
       s->ctr[3] = 1;
       return;
     }
-    s->ba[bi] = a, s->bb[bi] = b, s->bp[bi] = pos;
+    s->ba[bi] = a, s->bb[bi] = b, s->bp[bi] = bpack(pos, 0);
   }
   __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
     const uint32_t ki = atomicAdd(&s->ctr[0], n);
@@ -179,7 +196,7 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
         for (uint32_t i = tid; i < bl; i += BLOCK) {
           s.ba[i] = B.base.set_a[bo + i];
           s.bb[i] = B.base.set_b[bo + i];
-          s.bp[i] = -1;
+          s.bp[i] = bpack(-1, i);
         }
         if (tid == 0) s.ctr[1] = bl;
       }
@@ -295,20 +312,39 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
           else hi = mid;
         }
         bool alive = true;
-        if (lo > 0 && s.ka[lo - 1] == qa && s.kb[lo - 1] == qb) alive = s.kp[lo - 1] <= s.bp[i];
-        if (alive) {
-          const uint32_t o = atomicAdd(&s.ctr[2], 1u);
-          s.oa[o] = s.ba[i];
+        if (lo > 0 && s.ka[lo - 1] == qa && s.kb[lo - 1] == qb) alive = s.kp[lo - 1] <= bpos(s.bp[i]);
+        if (!alive) s.bp[i] = -1;  // dead (packed positions are >= 0)
+      }
+      __syncthreads();
+      // survivors: AW keyed (elem, output order) with the token in the (free) kill arrays,
+      // MV keyed (value, token)
+      for (uint32_t i = tid; i < nb; i += BLOCK) {
+        if (s.bp[i] < 0) continue;
+        const uint32_t o = atomicAdd(&s.ctr[2], 1u);
+        s.oa[o] = s.ba[i];
+        if (TYPE == AM_AWSET) {
+          s.ob[o] = bord(s.bp[i]);
+          s.ka[o] = s.bb[i];
+          s.kp[o] = (int32_t)o;
+        } else {
           s.ob[o] = s.bb[i];
         }
       }
       __syncthreads();
       const uint32_t no = s.ctr[2];
-      block_sort(s.oa, s.ob, nullptr, no, BCAP);
-      // drop duplicates and write the CSR (compaction by wave ballots)
       const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
-      const uint32_t base =
-          block_write_unique(s.oa, s.ob, no, R.value.set_a + ooff, R.value.set_b + ooff, ocap, &s.ctr[4]);
+      uint32_t base;
+      if (TYPE == AM_AWSET) {
+        block_sort(s.oa, s.ob, s.kp, no, BCAP);
+        for (uint32_t j = tid; j < no && j < ocap; j += BLOCK) {
+          R.value.set_a[ooff + j] = s.oa[j];
+          R.value.set_b[ooff + j] = s.ka[s.kp[j]];
+        }
+        base = no;
+      } else {
+        block_sort(s.oa, s.ob, nullptr, no, BCAP);
+        base = block_write_unique(s.oa, s.ob, no, R.value.set_a + ooff, R.value.set_b + ooff, ocap, &s.ctr[4]);
+      }
       if (base > ocap) status = AM_ERR_CAPACITY;
       else if (tid == 0) R.value.set_len[r] = base;
     }

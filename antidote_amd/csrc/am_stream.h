@@ -1,5 +1,4 @@
-// am_stream.h -- the streaming materialize kernel (PN counter, LWW register; and the
-// inclusion pass of the add-wins-set / MV-register token-table tier, am_hash.hip).
+// am_stream.h -- the streaming materialize kernel of the PN counter and the LWW register.
 //
 // Work split.  Reads are cut into batches of 64 consecutive reads; wavefront gw
 // of W takes batches gw, gw+W, gw+2W, ...  For a batch, lane i loads read i's
@@ -26,24 +25,8 @@
 #pragma once
 #include "am_wave.h"
 
-// Set mode (TYPE = AM_AWSET / AM_MVREG, packed view): k_stream runs the inclusion test
-// and the scalar outputs of materialize/4 and hands the effects to am_hash.hip's k_hrec.
-// Per selection slot it writes the read's included-op bitmap (HB_WORDS words: bit
-// op_pos + (off0 & 3), tile-aligned) and a task word set:
-//   task_r[slot]   = r | flag << 32 | (off0 & 3) << 40   flag 0: effects to resolve,
-//                    1: done (error status written), 2: log longer than max_ops (the
-//                    read is left to the next tier untouched)
-//   task_rk[2 slot], task_rk[2 slot + 1] = the read's record range
-struct am_setincl {
-  uint32_t *bitmap = nullptr;
-  uint64_t *task_r = nullptr;
-  uint64_t *task_rk = nullptr;
-  uint32_t max_ops = 0;
-};
-
 namespace amk_stream {
 using namespace amk;
-constexpr uint32_t HB_WORDS = 72;  // (2048 + 3 ops, whole 256-op tiles) / 32
 
 constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;
@@ -97,31 +80,16 @@ struct Out {
   uint32_t fin;       // the read was finalized (wide clocks: LastOpCt already stored)
 };
 
-struct NoVal {  // set mode: the effects are resolved by k_hrec (am_hash.hip)
-  __device__ void reset() {}
-  __device__ void add(uint64_t, uint64_t) {}
-};
 template <int TYPE>
 struct SOf {
   using T = typename ValOf<TYPE>::T;
-  static constexpr bool SETM = false, NEED_P0 = true, NEED_P1 = ValOf<TYPE>::NEED_P1;
-};
-template <>
-struct SOf<AM_AWSET> {
-  using T = NoVal;
-  static constexpr bool SETM = true, NEED_P0 = false, NEED_P1 = false;
-};
-template <>
-struct SOf<AM_MVREG> {
-  using T = NoVal;
-  static constexpr bool SETM = true, NEED_P0 = false, NEED_P1 = false;
+  static constexpr bool NEED_P0 = true, NEED_P1 = ValOf<TYPE>::NEED_P1;
 };
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
-                                                  am_rows_cfg H, am_setincl X) {
+                                                  am_rows_cfg H) {
   using V = typename SOf<TYPE>::T;
-  constexpr bool SETM = SOf<TYPE>::SETM;
   constexpr int OPL = opl_of<DMAX>();
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
   constexpr bool BUF_CT = DMAX < 8;  // wide clocks: LastOpCt leaves at finalize (fewer VGPRs)
@@ -159,14 +127,11 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
     uint64_t key, off0, off1, rb, r;  // rb: first slot of the batch; r: lane's read index
     int32_t st;
     uint32_t nb, skip;  // skip: the row tier (am_rows.hip) owns this read
-    uint32_t sh, big;   // set mode: off0 & 3; the log is longer than X.max_ops
-    uint64_t rk0, rk1;  // set mode: the read's record range
   };
   auto load_meta = [&](uint64_t bid, Meta &M) {
     M.rb = bid * WAVE;
     M.nb = bid < n_batches ? (uint32_t)(nsel - M.rb < (uint64_t)WAVE ? nsel - M.rb : (uint64_t)WAVE) : 0u;
     M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK, M.r = 0, M.skip = 0;
-    M.sh = 0, M.big = 0, M.rk0 = 0, M.rk1 = 0;
     if (lane < M.nb) {
       const uint64_t r = sbase ? (uint64_t)sbase[M.rb + lane] : M.rb + lane;
       M.r = r;
@@ -185,13 +150,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
         else if (rtype != (uint32_t)TYPE)
           M.st = AM_ERR_INVALID;              // batch type_hint violated
       }
-      if (SETM && M.st == AM_OK) {
-        M.rk0 = L.rec_key_off[key];
-        M.rk1 = L.rec_key_off[key + 1];
-        M.sh = (uint32_t)(M.off0 & (OPL - 1));
-        if (M.off1 - M.off0 > (uint64_t)X.max_ops) M.big = 1, M.skip = 1;
-      }
-      if (M.st != AM_OK || M.big) M.off1 = M.off0;  // no tiles to stream
+      if (M.st != AM_OK) M.off1 = M.off0;  // no tiles to stream
       if (H.mask && M.off1 - M.off0 <= (uint64_t)H.short_max) M.skip = 1, M.off1 = M.off0;
     }
     if (H.mask && bid < n_batches) {  // hand short (and error) reads to the row tier
@@ -238,13 +197,6 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   };
   // the batch's results: one coalesced store per column
   auto store_out = [&](const Meta &M) {
-    if (SETM && lane < M.nb) {
-      const uint64_t slot = M.rb + lane;
-      const uint64_t flag = M.big ? 2u : (o.status != AM_OK ? 1u : 0u);
-      X.task_r[slot] = M.r | (flag << 32) | ((uint64_t)M.sh << 40);
-      X.task_rk[2 * slot] = M.rk0;
-      X.task_rk[2 * slot + 1] = M.rk1;
-    }
     if (lane < M.nb && !M.skip) {
       const uint64_t r = M.r;
       R.status[r] = o.status;
@@ -262,7 +214,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
         }
         R.is_new_ss[r] = (uint8_t)o.newss;
         R.count[r] = o.count;
-        if (!SETM) R.value.v0[r] = (int64_t)o.v0;
+        R.value.v0[r] = (int64_t)o.v0;
         if (TYPE == AM_LWW) {
           R.value.v1[r] = o.v1;
           R.value.vflag[r] = (uint8_t)o.vflag;
@@ -339,7 +291,6 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   auto process = [&](const Tile<DMAX> &T, uint32_t j, uint64_t t) {
     const uint64_t o0 = lane_u64(M0.off0, j), o1 = lane_u64(M0.off1, j);
     const uint64_t g = t + (uint64_t)lane * OPL;
-    uint32_t ib = 0;  // set mode: included ops of this lane's 4 (bit k: op g + k)
 #pragma unroll
     for (int k = 0; k < OPL; ++k) {
       const uint64_t p = g + k;
@@ -358,21 +309,10 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
           for (int d = 0; d < DMAX; ++d) sv[d] = ct - (uint64_t)(int64_t)T.sd[k][d];
         }
         const uint32_t meta = (uint32_t)(w >> 56);
-        if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, T.sp[k], txm, p, a)) {
-          v.add(T.p0[k], T.p1[k]);
-          if (SETM && !(meta & AM_META_BAD)) ib |= 1u << k;
-        }
+        if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, T.sp[k], txm, p, a)) v.add(T.p0[k], T.p1[k]);
       } else if (eval_op<DMAX, GENERAL>(u, (T.meta4 >> (8 * k)) & 0xFFu, T.ct[k], T.sv[k], T.sp[k], txm, p, a)) {
         v.add(T.p0[k], T.p1[k]);
       }
-    }
-    if constexpr (SETM) {  // the tile's 256 inclusion bits -> 8 words of the slot's bitmap
-      constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
-      uint32_t wv = ib << (OPL * (lane % LPW));
-#pragma unroll
-      for (uint32_t m = 1; m < LPW; m <<= 1) wv |= (uint32_t)__shfl_xor((int)wv, (int)m);
-      const uint64_t wi = (t - (o0 & ~(uint64_t)(OPL - 1))) / 32 + lane / LPW;
-      if (lane % LPW == 0 && wi < HB_WORDS) X.bitmap[(M0.rb + j) * HB_WORDS + wi] = wv;
     }
   };
   // Reduce read j of batch M0 across the wave and park its results in lane j.

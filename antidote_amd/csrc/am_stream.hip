@@ -1,6 +1,5 @@
 // am_stream.hip -- launchers of the streaming materialize kernel (am_stream.h) for the
-// PN counter and the LWW register, and of its set mode (the inclusion pass of the
-// add-wins-set / MV-register token-table tier, am_hash.hip).
+// PN counter and the LWW register.
 #include "am_stream.h"
 
 using namespace amk;
@@ -25,7 +24,7 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
   hipLaunchKernelGGL((k_stream<D, TYPE, GENERAL, PACKED>), dim3((unsigned)blocks), dim3(BLOCK), 0, ctx->stream, *L, *B,
-                     *R, S, H, am_setincl{});
+                     *R, S, H);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }
@@ -40,29 +39,6 @@ int launch(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_resu
   if (nd <= 8) return launch_d<8, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
   if (nd <= 16) return launch_d<16, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
   return launch_d<32, TYPE, GENERAL, PACKED>(ctx, L, B, R, S, H);
-}
-
-template <int D, int TYPE, bool GENERAL>
-int launch_incl(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                const am_setincl &X) {
-  static int occ = 0;
-  if (occ == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_stream<D, TYPE, GENERAL, true>, amk_stream::BLOCK, 0) !=
-            hipSuccess ||
-        nb <= 0)
-      nb = 2;
-    occ = nb;
-  }
-  const uint64_t batches = (B->n_reads + WAVE - 1) / WAVE;
-  uint64_t blocks = (batches + WPB - 1) / WPB;
-  const uint64_t cap = (uint64_t)ctx->n_cu * (uint64_t)occ;
-  if (blocks > cap) blocks = cap;
-  if (blocks == 0) return AM_OK;
-  hipLaunchKernelGGL((k_stream<D, TYPE, GENERAL, true>), dim3((unsigned)blocks), dim3(amk_stream::BLOCK), 0, ctx->stream,
-                     *L, *B, *R, S, am_rows_cfg{}, X);
-  AM_HIP(hipGetLastError());
-  return AM_OK;
 }
 
 }  // namespace
@@ -99,23 +75,3 @@ int am_launch_stream(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am
   return am_launch_stream_skip(ctx, L, B, R, S, type, am_rows_cfg{});
 }
 
-int am_launch_stream_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                          uint32_t type, const am_setincl &X) {
-  const bool general = am_batch_general(L, B);
-  const uint32_t nd = L->n_dc;
-  if (type != AM_AWSET && type != AM_MVREG) return AM_ERR_UNSUPPORTED;
-#define AM_I(D)                                                                                  \
-  if (type == AM_AWSET)                                                                          \
-    return general ? launch_incl<D, AM_AWSET, true>(ctx, L, B, R, S, X)                          \
-                   : launch_incl<D, AM_AWSET, false>(ctx, L, B, R, S, X);                        \
-  return general ? launch_incl<D, AM_MVREG, true>(ctx, L, B, R, S, X)                            \
-                 : launch_incl<D, AM_MVREG, false>(ctx, L, B, R, S, X);
-  if (nd <= 1) { AM_I(1) }
-  if (nd <= 2) { AM_I(2) }
-  if (nd <= 3) { AM_I(3) }
-  if (nd <= 4) { AM_I(4) }
-  if (nd <= 8) { AM_I(8) }
-  if (nd <= 16) { AM_I(16) }
-  AM_I(32)
-#undef AM_I
-}

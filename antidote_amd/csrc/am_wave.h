@@ -65,6 +65,41 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #undef S_
   return umin64(umin64(lane_u64(v, 0), lane_u64(v, 16)), umin64(lane_u64(v, 32), lane_u64(v, 48)));
 }
+// The same reductions with the result left in every lane's VGPRs (no readlane to scalar
+// registers): for kernels whose scalar register file is already full.
+__device__ __forceinline__ uint64_t xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, WAVE);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, WAVE);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32_v(uint32_t v) {
+#define S_(C) v += dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  v += (uint32_t)__shfl_xor((int)v, 16, WAVE);
+  return v + (uint32_t)__shfl_xor((int)v, 32, WAVE);
+}
+__device__ __forceinline__ uint32_t wave_or_u32_v(uint32_t v) {
+#define S_(C) v |= dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  v |= (uint32_t)__shfl_xor((int)v, 16, WAVE);
+  return v | (uint32_t)__shfl_xor((int)v, 32, WAVE);
+}
+__device__ __forceinline__ uint64_t wave_max_u64_v(uint64_t v) {
+#define S_(C) v = umax64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  v = umax64(v, xor_u64(v, 16));
+  return umax64(v, xor_u64(v, 32));
+}
+__device__ __forceinline__ uint64_t wave_min_u64_v(uint64_t v) {
+#define S_(C) v = umin64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  v = umin64(v, xor_u64(v, 16));
+  return umin64(v, xor_u64(v, 32));
+}
 // exact 128-bit sum of per-lane (hi, lo) pairs
 __device__ __forceinline__ void add128(int64_t &hi, uint64_t &lo, int64_t whi, uint64_t wlo) {
   const uint64_t s = lo + wlo;
@@ -86,6 +121,57 @@ __device__ __forceinline__ void wave_sum_i128(int64_t &hi, uint64_t &lo) {
   for (int r = 16; r < 64; r += 16) add128(h, l, (int64_t)lane_u64((uint64_t)hi, r), lane_u64(lo, r));
   hi = h;
   lo = l;
+}
+
+// ---- 16-lane row helpers (the row tier, am_rows.hip, and the group tier's row kernel) ----
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---- 16-lane row all-reductions: every lane of a row ends with the row's value.
+// Full EXEC required (DPP reads inactive lanes as 0).
+__device__ __forceinline__ uint32_t row_sum_u32(uint32_t v) {
+#define S_(C) v += dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ uint32_t row_or_u32(uint32_t v) {
+#define S_(C) v |= dpp32<C>(v);
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ uint64_t row_max_u64(uint64_t v) {
+#define S_(C) v = umax64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ uint64_t row_min_u64(uint64_t v) {
+#define S_(C) v = umin64(v, dpp64<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  return v;
+}
+__device__ __forceinline__ void row_sum_i128(int64_t &hi, uint64_t &lo) {
+#define S_(C)                                            \
+  {                                                      \
+    const uint64_t wlo = dpp64<C>(lo);                   \
+    const int64_t whi = (int64_t)dpp64<C>((uint64_t)hi); \
+    add128(hi, lo, whi, wlo);                            \
+  }
+  AMK_ROW_STEPS(S_)
+#undef S_
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, WAVE);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, WAVE);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, uint32_t src) {
+  return (uint32_t)__shfl((int)v, (int)src, WAVE);
 }
 
 // ---- per-read uniform inputs and per-lane accumulators ----
@@ -217,6 +303,20 @@ __device__ __forceinline__ void wave_max_lww(LwwVal &v) {
     r.has |= whas;
   }
   v = r;
+}
+
+__device__ __forceinline__ void row_max_lww(LwwVal &v) {
+#define S_(C)                                                                        \
+  {                                                                                  \
+    const uint64_t wts = dpp64<C>(v.ts), wval = dpp64<C>(v.val);                     \
+    const uint32_t whas = dpp32<C>(v.has);                                           \
+    const bool gt = whas && (!v.has || wts > v.ts || (wts == v.ts && wval > v.val)); \
+    v.ts = gt ? wts : v.ts;                                                          \
+    v.val = gt ? wval : v.val;                                                       \
+    v.has |= whas;                                                                   \
+  }
+  AMK_ROW_STEPS(S_)
+#undef S_
 }
 
 }  // namespace amk

@@ -219,7 +219,9 @@ class HostBatch:
                     self.b_v0[i] = np.array([ts], np.uint64).view(np.int64)[0]
                     self.b_v1[i] = val
                     self.b_vflag[i] = 1 if isbin else 0
-                elif r.type in (abi.AM_AWSET, abi.AM_MVREG):
+                elif r.type == abi.AM_AWSET:  # the orddict in state order (elems ascending)
+                    pairs = [(int(a), int(b)) for a, b in bv]
+                elif r.type == abi.AM_MVREG:  # a sorted list of {Value, Token}
                     pairs = sorted((int(a), int(b)) for a, b in bv)
                 elif r.type == abi.AM_BCOUNTER:
                     pdict, ddict = bv

@@ -72,13 +72,14 @@ def bytes_per_op(type_: int, n_dc: int, packed: bool = True) -> int:
     return 1 + 8 + 8 * n_dc + payload
 
 
-REC_BYTES = 20  # one set-effect record: rec_a 8 + rec_b 8 + rec_meta 4 (am_pack.hip)
+REC_BYTES = 4  # one birth/kill record of the token-group view: rec_g u32 (am_group.hip)
 
 
 def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
     """Per read: key index 8 + type 1 + key_off 8 + key_type 1 (inputs) + outputs status 4,
     new_last_op 8, last_ct 8*D, last_ct_pres 4, last_ct_ignore 1, is_new_ss 1, count 4,
-    flags 1, value (PN 8; LWW 8+8+1; sets set_off 8 + set_len 4 + 16 per pair written;
+    flags 1, value (PN 8; LWW 8+8+1; sets: rec_key_off 8 + key_ngrp 4 + set_off 8 +
+    set_len 4 + per surviving pair 16 gathered from the group table and 16 written;
     bcounter (D*D + D) slots x 9)."""
     if type_ == abi.AM_PN:
         val = 8
@@ -87,7 +88,7 @@ def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
     elif type_ == abi.AM_BCOUNTER:
         val = 9 * (n_dc * n_dc + n_dc)
     else:
-        val = 12 + 16 * set_len
+        val = 24 + 32 * set_len
     return 8 + 1 + 8 + 1 + 4 + 8 + 8 * n_dc + 4 + 1 + 1 + 4 + 1 + val
 
 
@@ -191,7 +192,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
@@ -303,7 +304,7 @@ def main():
     ms = ctypes.c_float()
     abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
     kern_ms = ms.value / kern_iters
-    packed = bool(dlog.ct_meta) and os.environ.get("AM_PACKED", "1") != "0"
+    packed = bool(dlog.ct_meta)
     alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
@@ -329,10 +330,10 @@ def main():
                    "step": "GST min all-reduce (RCCL) + materialize all keys"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config, workload),
-                     "kernel": "k_stream" if single else "am_materialize (all tiers: k_stream, k_rows, k_hrec, k_sets, k_big_*)",
+                     "kernel": "k_stream" if single else "am_materialize (all tiers: k_stream, k_rows, k_grp_*, k_sets, k_big_*)",
                      "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "layout": "packed (ct_meta + int32 snapshot deltas); set effects as (a, tok, op) records"
+                     "layout": "packed (ct_meta + int32 snapshot deltas); set effects as u32 token-group records"
                      if packed else "full"},
         "cpu_baseline": None,
     }

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 1
+#define AM_ABI_VERSION 2
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -148,23 +148,37 @@ typedef struct am_op_log {
    * read that op from the full columns above.  Cuts C2 from 49 to 36 B/op. */
   const uint64_t *ct_meta;     /* [n_ops]                                            */
   const int32_t *snap_delta;   /* [n_dc][snap_stride]                                */
-  /* Set-effect record view (add-wins set and MV register keys), built on the device with
-   * the packed view.  Every effect is flattened to records (a, b, meta), a key's records
-   * contiguous and in op order: [rec_key_off[k], rec_key_off[k+1]).
-   *   AW  add token t of elem e -> birth (e, t);  remove token t of elem e -> kill (e, t)
-   *   MV  overridden token t   -> kill (0, t);   {Value, Token, _}      -> birth (Value, Token)
-   * rec_meta = op index within the key (bits 0-30) | kill << 31.  Ops carrying
-   * AM_META_BAD produce no record; an op whose variable payload is malformed (Type:update/2
-   * would raise) gets AM_META_BAD in its ct_meta meta byte instead of records.  A read
-   * then streams its ops (inclusion) and its records (effects) with no dependent loads. */
+  /* Token-group view (add-wins set and MV register keys), built on the device with the
+   * packed view (am_store_create / am_store_update / am_synth_store).  Every effect is
+   * flattened to births and kills of tokens:
+   *   AW  add token t of elem e -> birth of (e, t);  remove token t of elem e -> kill of (e, t)
+   *   MV  {Value, Token, _}      -> birth of (Value, Token); overridden token t -> kill of t
+   * A key's distinct kill keys (AW (elem, token), MV token) are its GROUPS, numbered in the
+   * reference's output order: AW by elem, then newest birth first (ToAdd ++ Current), MV by
+   * (Value, Token) (insert_sorted); groups without a birth last.  One u32 record per
+   * birth/kill, a key's records contiguous and in op order, [rec_key_off[k], rec_key_off[k+1]):
+   *   rec_g = op index within the key (bits 0-15) | kill << 16 | group << 17
+   * and group g of key k is (grp_a, grp_b)[rec_key_off[k] + g] (AW (elem, token), MV
+   * (Value, Token); kill-only MV groups (0, token)).  key_ngrp[k] = number of groups, or
+   * AM_NGRP_NONE when the key is materialized from var_data instead (more than
+   * AM_GRP_MAX_REC records or 2^16 ops, or a log outside the closed form: a token born
+   * twice (AW) / under two values (MV)).  A materialization then streams the ops
+   * (inclusion), the records (max birth / kill op per group) and only the surviving
+   * groups' pairs, with no sort.  Ops carrying AM_META_BAD produce no record; an op whose
+   * variable payload is malformed (Type:update/2 would raise) gets AM_META_BAD set in
+   * op_meta and ct_meta. */
   uint64_t n_rec;
   const uint64_t *rec_key_off; /* [n_keys+1]                                         */
-  const uint64_t *rec_a;       /* [n_rec]                                            */
-  const uint64_t *rec_b;       /* [n_rec]                                            */
-  const uint32_t *rec_meta;    /* [n_rec]                                            */
+  const uint32_t *rec_g;       /* [n_rec]                                            */
+  const uint64_t *grp_a;       /* [n_rec]                                            */
+  const uint64_t *grp_b;       /* [n_rec]                                            */
+  const uint32_t *key_ngrp;    /* [n_keys]                                           */
 } am_op_log;
-#define AM_REC_KILL (1u << 31)
-#define AM_REC_OP(m) ((m) & 0x7FFFFFFFu)
+#define AM_REC_KILL (1u << 16)
+#define AM_REC_OP(m) ((m) & 0xFFFFu)
+#define AM_REC_GRP(m) ((m) >> 17)
+#define AM_NGRP_NONE 0xFFFFFFFFu
+#define AM_GRP_MAX_REC 2048u
 #define AM_CT_ESC (1ull << 55)
 
 /*
@@ -172,8 +186,10 @@ typedef struct am_op_log {
  *   PN        v0
  *   LWW       v0 = ts (as u64 bits), v1 = value, vflag = 1 for the initial
  *             {0, <<>>} value (a binary sorts above every integer)
- *   AWSET     CSR of (elem, token) pairs sorted by (elem, token) -- one pair per
- *   MVREG     live token; MV: (value, token) pairs sorted.  set_off[n+1] gives
+ *   AWSET     CSR of (elem, token) pairs: the orddict [{Elem, Tokens}] flattened in
+ *             the reference's order (elems ascending, each token list in list order,
+ *             the newest add first)
+ *   MVREG     CSR of (value, token) pairs sorted (insert_sorted).  set_off[n+1] gives
  *             each read's capacity, set_len[n] the used length.
  *   BCOUNTER  bc_p[n][n_dc*n_dc] + bc_p_pres, bc_d[n][n_dc] + bc_d_pres
  *             (P key {From,To} at From*n_dc+To; an orddict entry is present iff

@@ -119,6 +119,21 @@ static int contains(const uint64_t *a, uint64_t n, uint64_t x) {
   return 0;
 }
 
+/* Current -- ToRemove (lists:subtract/2): each token of rm removes the first occurrence
+ * of that token from cur; the order of cur is kept.  Appends the result to ne. */
+static void aw_push_subtract(aw_ent *ne, const uint64_t *cur, uint32_t ncur, const uint64_t *rm, uint64_t nr) {
+  uint8_t *gone = (uint8_t *)calloc(ncur ? ncur : 1, 1);
+  for (uint64_t j = 0; j < nr; ++j)
+    for (uint32_t i = 0; i < ncur; ++i)
+      if (!gone[i] && cur[i] == rm[j]) {
+        gone[i] = 1;
+        break;
+      }
+  for (uint32_t i = 0; i < ncur; ++i)
+    if (!gone[i]) aw_push_tok(ne, cur[i]);
+  free(gone);
+}
+
 /* antidote_crdt_set_aw:update/2 -- apply_downstreams merge.  Returns 0, or -1 on a malformed effect. */
 static int aw_apply(aw_state *s, const uint64_t *eff, uint64_t len) {
   aw_state out = {0};
@@ -148,9 +163,8 @@ static int aw_apply(aw_state *s, const uint64_t *eff, uint64_t len) {
       q += 3 + na + nr;
     } else if (have_op && e1 == s->e[si].elem) {
       ne.elem = e1;
-      for (uint64_t i = 0; i < na; ++i) aw_push_tok(&ne, add[i]);
-      for (uint32_t i = 0; i < s->e[si].n; ++i)
-        if (!contains(rm, nr, s->e[si].tok[i])) aw_push_tok(&ne, s->e[si].tok[i]);
+      for (uint64_t i = 0; i < na; ++i) aw_push_tok(&ne, add[i]);  /* ToAdd ++ (Current -- ToRemove) */
+      aw_push_subtract(&ne, s->e[si].tok, s->e[si].n, rm, nr);
       q += 3 + na + nr;
       ++si;
     } else {
@@ -200,11 +214,6 @@ static void mv_apply(mv_state *s, int reset, uint64_t val, uint64_t tok, const u
   memmove(s->p + pos + 1, s->p + pos, (s->n - pos) * sizeof(mv_pair));
   s->p[pos] = a;
   s->n++;
-}
-
-static int cmp_u64(const void *a, const void *b) {
-  uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
-  return x < y ? -1 : x > y;
 }
 
 static int add_ovf(__int128 *acc, __int128 v) {
@@ -341,7 +350,7 @@ int amo_materialize_one(const am_op_log *L, const am_read_batch *B, uint64_t r, 
       }
     } else if (type == AM_AWSET) {
       aw_state st = {0};
-      if (bv->set_off) { /* base pairs (elem, token) sorted */
+      if (bv->set_off) { /* base pairs (elem, token): the orddict in state order */
         for (uint64_t i = bv->set_off[r]; i < bv->set_off[r] + bv->set_len[r]; ++i) {
           if (st.n == 0 || st.e[st.n - 1].elem != bv->set_a[i]) {
             if (st.n == st.cap) {
@@ -367,9 +376,7 @@ int amo_materialize_one(const am_op_log *L, const am_read_batch *B, uint64_t r, 
       if (status == AM_OK) {
         uint64_t o = ov->set_off[r], cap = ov->set_off[r + 1] - o, w = 0;
         for (uint32_t i = 0; i < st.n && status == AM_OK; ++i) {
-          qsort(st.e[i].tok, st.e[i].n, sizeof(uint64_t), cmp_u64);
-          for (uint32_t t = 0; t < st.e[i].n; ++t) {
-            if (t > 0 && st.e[i].tok[t] == st.e[i].tok[t - 1]) continue; /* rendered as a set */
+          for (uint32_t t = 0; t < st.e[i].n; ++t) { /* the token list in state order */
             if (w >= cap) {
               status = AM_ERR_CAPACITY;
               break;

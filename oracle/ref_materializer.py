@@ -204,9 +204,23 @@ def _orddict_update_counter(d: list, key, incr: int) -> list:
     return out
 
 
+def erl_subtract(a: list, b: list) -> list:
+    """Erlang's A -- B (lists:subtract/2): for each element of B, the first
+    occurrence in A (if any) is removed; order of A is kept."""
+    out = list(a)
+    for x in b:
+        for i, y in enumerate(out):
+            if erl_cmp(x, y) == 0:
+                del out[i]
+                break
+    return out
+
+
 def _aw_apply_downstreams(ops: list, set_: list) -> list:
     # antidote_crdt_set_aw: merge of the (Elem-sorted) effect entries into the
     # Elem-sorted orddict; an element whose token list becomes empty is dropped.
+    # Token lists keep the reference's list order: ToAdd ++ (Current -- ToRemove),
+    # i.e. the newest add first.
     if not ops:
         return list(set_)
     if not set_:
@@ -215,7 +229,7 @@ def _aw_apply_downstreams(ops: list, set_: list) -> list:
     (e2, cur), set_rest = set_[0], set_[1:]
     c = erl_cmp(e1, e2)
     if c == 0:
-        toks = list(add) + [t for t in cur if t not in rm]
+        toks = list(add) + erl_subtract(cur, rm)
         tail = _aw_apply_downstreams(ops_rest, set_rest)
         return ([(e1, toks)] if toks else []) + tail
     if c > 0:

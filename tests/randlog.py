@@ -19,14 +19,21 @@ def rand_effect(rng, t, n_dc, state):
         return (rng.choice([0, rng.randint(1, 60)]) if rng.random() < 0.1 else rng.randint(1, 60),
                 rng.randint(0, 5))
     if t == abi.AM_AWSET:
+        # adds observe-and-replace the live tokens (antidote_crdt's add), or -- as a
+        # concurrent add would -- leave some live, so an element can hold several tokens
+        # (token-list order is part of the state); some effects add two tokens at once
         ents = []
         for e in sorted(rng.sample(range(6), rng.randint(1, 2))):
             live = state.setdefault(e, [])
             if rng.random() < 0.65:
-                tok = state["next"] = state.get("next", 100) + 1
-                rm = list(live)
-                state[e] = [tok]
-                ents.append((e, [tok], rm))
+                toks = []
+                for _ in range(1 if rng.random() < 0.85 else 2):
+                    toks.append(state.get("next", 100) + 1)
+                    state["next"] = toks[-1]
+                r = rng.random()
+                rm = list(live) if r < 0.6 else (live[: len(live) // 2] if r < 0.8 else [])
+                state[e] = toks + [x for x in live if x not in rm]
+                ents.append((e, toks, rm))
             else:
                 rm = list(live) if rng.random() < 0.8 else [rng.randint(100, 130)]
                 state[e] = []
@@ -112,11 +119,11 @@ def base_state_term(t, v):
     if t == abi.AM_LWW:
         ts, val, isbin = v
         return (ts, R.Bin(b"") if isbin else val)
-    if t == abi.AM_AWSET:
+    if t == abi.AM_AWSET:  # ordered (elem, token) pairs: elems ascending, token lists in state order
         d = {}
-        for e, tok in sorted(v):
+        for e, tok in v:
             d.setdefault(e, []).append(tok)
-        return sorted(d.items())
+        return sorted(d.items(), key=lambda kv: kv[0])
     if t == abi.AM_MVREG:
         return sorted(v)
     if t == abi.AM_BCOUNTER:
@@ -132,8 +139,8 @@ def canon_state(t, s):
     if t == abi.AM_LWW:
         ts, val = s
         return (ts, 0, True) if isinstance(val, bytes) else (ts, val, False)
-    if t == abi.AM_AWSET:
-        return sorted({(e, tok) for e, toks in s for tok in toks})
+    if t == abi.AM_AWSET:  # the orddict flattened in order: token lists are compared as ordered lists
+        return [(e, tok) for e, toks in s for tok in toks]
     if t == abi.AM_MVREG:
         return sorted(set(s))
     if t == abi.AM_BCOUNTER:

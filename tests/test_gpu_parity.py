@@ -402,17 +402,17 @@ def _seq_ops(t, effects, n_dc=2):
     return [Op(t, i % n_dc, 10 + 2 * i, {d: 10 + 2 * i - 1 for d in range(n_dc)}, eff) for i, eff in enumerate(effects)]
 
 
-def test_gpu_hash_tier_guards(mat):
-    """The token-table tier (am_hash.hip: k_stream set mode + k_hrec) hands a read to the
-    LDS-sort tier whenever its table cannot decide it exactly; every case must still
-    match the oracle.  Logs of 60 .. 2000 ops (between the row tier and the tier's limit):
-      0  AW: one token under two elems (the kill key is (tok, elem))
-      1  AW: 600 live elems (more survivors than the table's survivor list)
-      2  MV: one token with two values
-      3  MV: 1500 concurrent values (more distinct tokens than table slots)
+def test_gpu_group_tier_guards(mat):
+    """The token-group tier (am_group.hip) serves keys whose log the group builder could
+    number; the others go to the var_data tiers.  Every case must match the oracle.
+    Logs of 60 .. 2100 ops:
+      0  AW: one token under two elems (two kill keys (elem, tok): two groups)
+      1  AW: 600 live elems (600 survivors)
+      2  MV: one token with two values (outside the closed form: ungrouped, LDS-sort tier)
+      3  MV: 1500 concurrent values (1500 groups)
       4  AW / 5 MV: the sentinel 2^64-1 as a token / value
-      6  AW: plain 300-op log (stays in the tier), 7  MV: plain 2000-op chain
-      8  AW: 2100 ops (beyond the tier: the LDS-sort tier takes it whole)"""
+      6  AW: plain 300-op log, 7  MV: plain 2000-op chain
+      8  AW: 2100 ops, ~4200 births/kills (beyond the group view: the LDS-sort tier)"""
     M = (1 << 64) - 1
     aw, mv = abi.AM_AWSET, abi.AM_MVREG
     keys, types = [], []
@@ -448,9 +448,9 @@ def test_gpu_hash_tier_guards(mat):
         _batch_compare(log, [r for r in reads if r.type == t], mat, 2, cap=4096)
 
 
-def test_gpu_hash_tier_mixed_batch(mat):
-    """The same tier inside a mixed batch (planner selection + row-tier hand-off list),
-    with cached bases (base pairs are births at -1) on the second read."""
+def test_gpu_group_tier_mixed_batch(mat):
+    """The group tier inside a mixed batch (planner selection + row-kernel hand-off list),
+    then cached bases (base pairs: the LDS-sort tier) on the second read."""
     rng = random.Random(4242)
     keys, types = [], []
     for k in range(60):
