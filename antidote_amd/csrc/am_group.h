@@ -1,0 +1,825 @@
+// am_group.h -- the token-group tier of the add-wins set and the MV register
+// (antidote_crdt_set_aw / antidote_crdt_register_mv update/2, folded by
+// clocksi_materializer:apply_operations/4, src/clocksi_materializer.erl:113-121), and the
+// ingestion-side builder of the token-group view it reads (include/antidote_mat.h).
+//
+// Closed form.  Both types apply their effects sequentially, oldest -> newest, but the
+// final state has a closed form.  Call every token an effect inserts a BIRTH at the op's
+// position p (AW {Elem, [Token], _} -> (elem, token); MV {Value, Token, _} -> (value,
+// token)) and every token it drops a KILL at p (AW remove tokens, MV overridden tokens).
+// The AW update is ToAdd ++ (Current -- ToRemove) and the MV update drops the overridden
+// tokens before insert_sorted, so a kill never hits a birth of its own op, and
+//     a token survives  <=>  its newest included birth is at or after its newest included kill
+// per kill key (AW (elem, token), MV token).  Tokens are unique() binaries in antidote_crdt,
+// so a kill key has one birth; keys whose log breaks that (a token born twice, or under two
+// MV values) are left ungrouped by the builder and go to the var_data tiers (am_sets.hip).
+//
+// Builder (k_grp_build, one workgroup per key, at store creation / update): the key's
+// births and kills are sorted by kill key in LDS; every distinct kill key is a GROUP; the
+// groups are numbered in the reference's output order -- AW: elem ascending, then newest
+// birth first and, within one op, the effect's token order (ToAdd ++ Current); MV: (value,
+// token) ascending (insert_sorted) -- and each birth/kill becomes one u32 record
+// op | kill << 16 | group << 17.
+//
+// Read (k_grp_row: one 16-lane row per short read; k_grp_wave: one wave per read, up to
+// 1024 groups; k_grp_wg: one 512-thread workgroup per read, up to 2048 groups):
+//   1. the read's ops stream in 1024-op tiles (packed view, 16-byte loads): is_op_in_snapshot/7
+//      per op (am_wave.h eval_op) -> an LDS inclusion bitmap + the scalar outputs;
+//   2. the read's records (4 B each) stream in: an included birth / kill does one LDS
+//      atomicMax of its op index into the group's max-birth / max-kill slot;
+//   3. the groups are scanned in order: survivors (max birth >= max kill) are compacted by
+//      wave ballots and their (a, b) pairs gathered into the output CSR -- already in the
+//      reference's order, no sort.
+// Reads with base-snapshot pairs, longer logs or ungrouped keys are handed to the next tier.
+#pragma once
+#include "am_block.h"
+
+namespace amk_grp {
+using namespace amk;
+
+constexpr int BLOCK = 256;
+constexpr int NW = BLOCK / WAVE;
+constexpr uint32_t RCAP = AM_GRP_MAX_REC;
+constexpr int32_t PNONE = (int32_t)0x80000000;
+constexpr uint32_t KILL31 = 0x80000000u;
+
+// ================================================================ reads
+// per-read metadata shared by both read kernels
+struct GMeta {
+  uint64_t r, key, off0, off1, rk0, rk1;
+  uint32_t G;
+  int32_t st;
+};
+
+__device__ __forceinline__ void read_meta(const am_op_log &L, const am_read_batch &B, uint64_t r, uint32_t type,
+                                          GMeta &m) {
+  m.r = r;
+  m.key = B.key[r];
+  m.st = AM_OK;
+  m.off0 = m.off1 = m.rk0 = m.rk1 = 0;
+  m.G = AM_NGRP_NONE;
+  const uint32_t rtype = B.type[r];
+  if (m.key >= L.n_keys) {
+    m.st = AM_ERR_INVALID;
+    return;
+  }
+  m.off0 = L.key_off[m.key];
+  m.off1 = L.key_off[m.key + 1];
+  const uint32_t ktype = L.key_type[m.key];
+  const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[m.key] : 0u;
+  if (m.off1 > m.off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES))) m.st = AM_ERR_CORRUPTED_OPS_CACHE;
+  else if (rtype != type) m.st = AM_ERR_INVALID;
+  if (m.st != AM_OK) return;
+  m.rk0 = L.rec_key_off[m.key];
+  m.rk1 = L.rec_key_off[m.key + 1];
+  m.G = L.key_ngrp[m.key];
+}
+
+__device__ __forceinline__ bool has_base_pairs(const am_read_batch &B, uint64_t r) {
+  return B.base.set_off && B.base.set_len && B.base.set_len[r] != 0;
+}
+
+// per-read inputs (clock, base clock, TxId) of read r; UNIF: the whole workgroup reads one
+// read, so the values are made wave-uniform (scalar registers)
+template <int DMAX, bool GENERAL, bool UNIF>
+__device__ __forceinline__ void read_inputs(const am_op_log &L, uint32_t nd, const am_read_batch &B, uint64_t r,
+                                            ReadU<DMAX> &u) {
+  auto u32 = [](uint32_t x) { return UNIF ? uniform_u32(x) : x; };
+  auto u64 = [](uint64_t x) { return UNIF ? uniform_u64(x) : x; };
+  const uint64_t n = B.n_reads;
+  u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+  const uint64_t rstride = (GENERAL && B.per_read_clock) ? n : 1, ridx = (GENERAL && B.per_read_clock) ? r : 0;
+  u.spres = u32(B.read_pres[ridx]) & u.allmask;
+  u.base_ignore = !GENERAL || !B.base_ignore || B.base_ignore[r];
+  u.cpres = u.base_ignore ? 0u : (u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+    u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+  }
+  u.has_txid = GENERAL && B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+  u.txid = u.has_txid ? u64(B.txid[r]) : 0;
+}
+
+// one op of the log: inclusion (is_op_in_snapshot/7) from the packed or the full view
+template <int DMAX, bool GENERAL, bool PACKED>
+__device__ __forceinline__ bool eval_at(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t p, uint64_t stride,
+                                        uint64_t w /* ct_meta | commit_time */, const int32_t *sd,
+                                        const uint64_t *svf, uint32_t meta_full, uint32_t sp, uint64_t tx,
+                                        Acc<DMAX> &a) {
+  uint32_t meta;
+  uint64_t ct, sv[DMAX];
+  if (PACKED) {
+    meta = (uint32_t)(w >> 56);
+    if (w & AM_CT_ESC) {  // rare: the op does not fit the packed view
+      ct = L.commit_time[p];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+    } else {
+      ct = w & (AM_CT_ESC - 1);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) sv[d] = ct - (uint64_t)(int64_t)sd[d];
+    }
+  } else {
+    meta = meta_full;
+    ct = w;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sv[d] = svf[d];
+  }
+  const bool txm = GENERAL && u.has_txid && tx == u.txid;
+  return eval_op<DMAX, GENERAL>(u, meta, ct, sv, sp, txm, p, a) && !(meta & AM_META_BAD);
+}
+
+// NewLastOp: id of the oldest excluded candidate - 1, else get_first_id/1 (the newest op's id)
+__device__ __forceinline__ int64_t new_last_op(const am_op_log &L, uint64_t key, uint64_t off0, uint64_t off1,
+                                               uint64_t min_excl) {
+  const uint64_t idb = L.key_id_base ? L.key_id_base[key] : 1;
+  if (min_excl != NONE) return (L.op_id ? (int64_t)L.op_id[min_excl] : (int64_t)(idb + (min_excl - off0))) - 1;
+  if (off1 == off0) return 0;
+  return L.op_id ? (int64_t)L.op_id[off1 - 1] : (int64_t)(idb + (off1 - off0) - 1);
+}
+
+template <int DMAX>
+__device__ __forceinline__ void write_scalars(const am_op_log &L, uint32_t nd, const am_read_batch &B, am_read_result &R,
+                                              const GMeta &m, const ReadU<DMAX> &u, int32_t status, uint32_t count,
+                                              uint32_t flags, uint32_t pres, uint64_t min_excl, const uint64_t *mx,
+                                              uint32_t setlen) {
+  const uint64_t r = m.r, n = B.n_reads;
+  R.status[r] = status;
+  R.flags[r] = (uint8_t)(flags & 0xFFu);
+  if (status != AM_OK) return;
+  R.new_last_op[r] = new_last_op(L, m.key, m.off0, m.off1, min_excl);
+  const bool ign = u.base_ignore && count == 0;
+  const uint32_t opres = ign ? 0u : (pres | u.cpres);
+  R.last_ct_ignore[r] = ign ? 1 : 0;
+  R.last_ct_pres[r] = opres;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    if (d >= (int)nd) continue;
+    const uint64_t v = mx[d] > u.C0[d] ? mx[d] : u.C0[d];
+    R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? v : 0;
+  }
+  R.is_new_ss[r] = count > 0;
+  R.count[r] = count;
+  R.value.set_len[r] = setlen;
+}
+
+// ---------------------------------------------------------------- workgroup per read
+// 512 threads: one 1024-op tile (2 ops per thread at D >= 8, 2048 ops / 4 per thread below)
+// and 2048 records are in flight per read, with no register double-buffering; several
+// workgroups per CU overlap one read's LDS phases with another's loads.
+constexpr int WBLOCK = 512;
+constexpr int WNW = WBLOCK / WAVE;
+constexpr uint32_t OPMAX = 8192;                  // longest log of the workgroup kernel
+constexpr uint32_t IWORDS = OPMAX / 32 + 64;      // + tile alignment slack
+constexpr int RPT = 4;                            // records per thread per pass
+constexpr uint64_t RPASS = (uint64_t)WBLOCK * RPT;
+template <int DMAX>
+constexpr int wopl() { return DMAX >= 8 ? 2 : 4; }
+
+template <int DMAX>
+struct WgSmem {
+  int32_t mb[RCAP], mk[RCAP];   // per group: newest included birth / kill op (PNONE: none)
+  uint32_t incl[IWORDS];        // included ops, bit = op - (off0 & ~(OPL-1))
+  uint64_t red[WNW][4 + DMAX];  // per-wave partials: count, flags, pres, min_excl, mx[]
+  uint32_t wsum[WNW];
+};
+
+template <int N>
+__device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
+  const u64x2 a = *(const u64x2 *)p;
+  o[0] = a.x, o[1] = a.y;
+  if constexpr (N == 4) {
+    const u64x2 b = *(const u64x2 *)(p + 2);
+    o[2] = b.x, o[3] = b.y;
+  }
+}
+template <int N>
+__device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
+  if constexpr (N == 4) {
+    const u32x4 a = *(const u32x4 *)p;
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w;
+  } else {
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    const u32x2_t a = *(const u32x2_t *)p;
+    o[0] = a.x, o[1] = a.y;
+  }
+}
+
+template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
+__global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                      am_retry next) {
+  constexpr int OPL = wopl<DMAX>();
+  constexpr uint64_t TILE = (uint64_t)WBLOCK * OPL;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  WgSmem<DMAX> &s = *reinterpret_cast<WgSmem<DMAX> *>(smem_raw);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t nd = EXACT ? (uint32_t)DMAX : L.n_dc;  // EXACT: n_dc == DMAX, no per-DC guards
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+
+  for (uint64_t i = blockIdx.x; i < nsel; i += gridDim.x) {
+    GMeta m;
+    read_meta(L, B, S.idx ? (uint64_t)uniform_u32(S.idx[sel0 + i]) : i, TYPE, m);
+    m.st = (int32_t)uniform_u32((uint32_t)m.st);
+    m.off0 = uniform_u64(m.off0), m.off1 = uniform_u64(m.off1);
+    m.rk0 = uniform_u64(m.rk0), m.rk1 = uniform_u64(m.rk1), m.G = uniform_u32(m.G);
+    const uint64_t r = m.r;
+    if (m.st != AM_OK) {
+      if (tid == 0) R.status[r] = m.st, R.flags[r] = 0;
+      continue;
+    }
+    const uint32_t G = m.G;
+    if (G == AM_NGRP_NONE || G > RCAP || m.off1 - m.off0 > OPMAX || has_base_pairs(B, r)) {
+      if (tid == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
+      continue;
+    }
+    ReadU<DMAX> u;
+    read_inputs<DMAX, GENERAL, true>(L, nd, B, r, u);
+    const uint64_t t0 = m.off0 & ~(uint64_t)(OPL - 1);
+    const uint32_t sh = (uint32_t)(m.off0 & (OPL - 1));
+
+    // the first record pass is in flight while the ops are evaluated
+    uint32_t rec[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const uint64_t q = m.rk0 + (uint64_t)j * WBLOCK + tid;
+      rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+    }
+    for (uint32_t g = tid; g < G; g += WBLOCK) s.mb[g] = PNONE, s.mk[g] = PNONE;
+
+    // ---- 1. inclusion per op -> bitmap + scalar partials ----
+    Acc<DMAX> a;
+    a.reset();
+    for (uint64_t t = t0; t < m.off1; t += TILE) {
+      const uint64_t g = t + (uint64_t)tid * OPL;
+      uint32_t ib = 0;
+      if (g < m.off1) {
+        uint64_t wv[OPL];
+        uint32_t sp[OPL], mf[OPL] = {};
+        uint64_t tx[OPL] = {};
+#pragma unroll
+        for (int k = 0; k < OPL; ++k) sp[k] = u.allmask;
+        if (GENERAL && L.snap_pres) ld_n32<OPL>(L.snap_pres + g, sp);
+        if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
+        if (PACKED) {
+          int32_t sd[OPL][DMAX];
+          ld_n64<OPL>(L.ct_meta + g, wv);
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint32_t q[OPL] = {};
+            if (d < (int)nd) ld_n32<OPL>((const uint32_t *)L.snap_delta + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) sd[k][d] = (int32_t)q[k];
+          }
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) {
+            const uint64_t p = g + k;
+            if (p >= m.off0 && p < m.off1 &&
+                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a))
+              ib |= 1u << k;
+          }
+        } else {
+          uint64_t svf[OPL][DMAX];
+          ld_n64<OPL>(L.commit_time + g, wv);
+          const uint32_t m4 = OPL == 4 ? *(const uint32_t *)(L.op_meta + g) : (uint32_t)*(const uint16_t *)(L.op_meta + g);
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) mf[k] = (m4 >> (8 * k)) & 0xFFu;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint64_t q[OPL] = {};
+            if (d < (int)nd) ld_n64<OPL>(L.snap_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) svf[k][d] = q[k];
+          }
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) {
+            const uint64_t p = g + k;
+            if (p >= m.off0 && p < m.off1 &&
+                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a))
+              ib |= 1u << k;
+          }
+        }
+      }
+      // 32 / OPL lanes -> one bitmap word
+      constexpr uint32_t LPW = 32 / OPL;
+      uint32_t word = ib << (OPL * (lane % LPW));
+#pragma unroll
+      for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
+      if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + tid / LPW] = word;
+    }
+    {  // wave partials of the scalar outputs (VGPR reductions: the scalar file is full)
+      const uint32_t cnt = wave_sum_u32_v(a.count), fl = wave_or_u32_v(a.flags), pr = wave_or_u32_v(a.pres);
+      const uint64_t mn = wave_min_u64_v(a.min_excl);
+      if (lane == 0) s.red[w][0] = cnt, s.red[w][1] = fl, s.red[w][2] = pr, s.red[w][3] = mn;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d >= (int)nd) continue;
+        const uint64_t x = wave_max_u64_v(a.mx[d]);
+        if (lane == 0) s.red[w][4 + d] = x;
+      }
+    }
+    __syncthreads();
+
+    // ---- 2. records of included ops -> newest birth / kill per group ----
+    for (uint64_t q0 = m.rk0;;) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const uint32_t x = rec[j];
+        if (x == 0xFFFFFFFFu) continue;
+        const uint32_t op = AM_REC_OP(x), bit = op + sh;
+        if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
+        atomicMax((x & AM_REC_KILL) ? &s.mk[AM_REC_GRP(x)] : &s.mb[AM_REC_GRP(x)], (int32_t)op);
+      }
+      q0 += RPASS;
+      if (q0 >= m.rk1) break;
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const uint64_t q = q0 + (uint64_t)j * WBLOCK + tid;
+        rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+      }
+    }
+    // the block's scalar outputs (partials were published before the barrier above)
+    uint32_t count = 0, flags = 0, pres = 0;
+    uint64_t min_excl = NONE;
+#pragma unroll
+    for (int v = 0; v < WNW; ++v) {
+      count += (uint32_t)s.red[v][0];
+      flags |= (uint32_t)s.red[v][1];
+      pres |= (uint32_t)s.red[v][2];
+      min_excl = s.red[v][3] < min_excl ? s.red[v][3] : min_excl;
+    }
+    const int32_t st0 = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+    __syncthreads();
+
+    // ---- 3. survivors in group order -> the output CSR ----
+    uint32_t ns = 0;
+    if (st0 == AM_OK) {
+      const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
+      for (uint32_t g0 = 0; g0 < G; g0 += WBLOCK) {
+        const uint32_t g = g0 + tid;
+        bool alive = false;
+        if (g < G) {
+          const int32_t b = s.mb[g];
+          alive = b != PNONE && b >= s.mk[g];
+        }
+        const uint64_t bm = __ballot(alive);
+        if (lane == 0) s.wsum[w] = (uint32_t)__popcll(bm);
+        __syncthreads();
+        uint32_t woff = 0, total = 0;
+#pragma unroll
+        for (int v = 0; v < WNW; ++v) {
+          if (v < (int)w) woff += s.wsum[v];
+          total += s.wsum[v];
+        }
+        if (alive) {
+          const uint64_t o = ns + woff + (uint32_t)__popcll(bm & lt);
+          if (o < ocap) {
+            R.value.set_a[ooff + o] = L.grp_a[m.rk0 + g];
+            R.value.set_b[ooff + o] = L.grp_b[m.rk0 + g];
+          }
+        }
+        ns += total;
+        __syncthreads();
+      }
+    }
+    if (tid < 64) {  // wave 0: lane d owns LastOpCt entry d, lane 0 the rest
+      const uint64_t ocap = R.value.set_off[r + 1] - R.value.set_off[r];
+      const int32_t status = (st0 == AM_OK && ns > ocap) ? AM_ERR_CAPACITY : st0;
+      const bool ign = u.base_ignore && count == 0;
+      const uint32_t opres = ign ? 0u : (pres | u.cpres);
+      if (status == AM_OK && lane < nd) {
+        uint64_t mx = 0, c0 = 0;
+#pragma unroll
+        for (int v = 0; v < WNW; ++v) mx = s.red[v][4 + lane] > mx ? s.red[v][4 + lane] : mx;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          if ((uint32_t)d == lane) c0 = u.C0[d];
+        R.last_ct[(uint64_t)lane * B.n_reads + r] = ((opres >> lane) & 1u) ? (mx > c0 ? mx : c0) : 0;
+      }
+      if (lane == 0) {
+        R.status[r] = status;
+        R.flags[r] = (uint8_t)(flags & 0xFFu);
+        if (status == AM_OK) {
+          R.new_last_op[r] = new_last_op(L, m.key, m.off0, m.off1, min_excl);
+          R.last_ct_ignore[r] = ign ? 1 : 0;
+          R.last_ct_pres[r] = opres;
+          R.is_new_ss[r] = count > 0;
+          R.count[r] = count;
+          R.value.set_len[r] = ns;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- wave per read
+// The C3-class read (hundreds to thousands of ops, up to VG groups): each wave of a
+// 256-thread workgroup runs its own reads with no workgroup barrier -- LDS is carved per
+// wave (group slots + inclusion bitmap) -- so a CU keeps ~16 reads in flight and one read's
+// dependent steps (metadata -> ops + records -> survivors' pairs) hide behind the others.
+constexpr uint32_t VG = 1024;              // groups of a wave-kernel read
+constexpr uint32_t VOPS = 8192;            // ops of a wave-kernel read
+constexpr uint32_t VWORDS = VOPS / 32 + 8;
+constexpr int VRPT = 8;                    // records per lane per chunk (512 per wave)
+struct WaveSmem {
+  int32_t mb[VG], mk[VG];
+  uint32_t incl[VWORDS];
+};
+template <int DMAX>
+constexpr int vopl() { return DMAX >= 8 ? 2 : 4; }
+
+template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
+__global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                    am_retry next) {
+  constexpr int OPL = vopl<DMAX>();
+  constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
+  constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  WaveSmem &s = reinterpret_cast<WaveSmem *>(smem_raw)[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t nd = EXACT ? (uint32_t)DMAX : L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+  const uint64_t W = (uint64_t)gridDim.x * NW;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6);
+
+  for (uint64_t i = gw; i < nsel; i += W) {
+    GMeta m;
+    read_meta(L, B, S.idx ? (uint64_t)uniform_u32(S.idx[sel0 + i]) : i, TYPE, m);
+    m.st = (int32_t)uniform_u32((uint32_t)m.st);
+    m.off0 = uniform_u64(m.off0), m.off1 = uniform_u64(m.off1);
+    m.rk0 = uniform_u64(m.rk0), m.rk1 = uniform_u64(m.rk1), m.G = uniform_u32(m.G);
+    const uint64_t r = m.r;
+    if (m.st != AM_OK) {
+      if (lane == 0) R.status[r] = m.st, R.flags[r] = 0;
+      continue;
+    }
+    const uint32_t G = m.G;
+    if (G == AM_NGRP_NONE || G > VG || m.off1 - m.off0 > VOPS || has_base_pairs(B, r)) {
+      if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
+      continue;
+    }
+    ReadU<DMAX> u;
+    read_inputs<DMAX, GENERAL, true>(L, nd, B, r, u);
+    const uint64_t t0 = m.off0 & ~(uint64_t)(OPL - 1);
+    const uint32_t sh = (uint32_t)(m.off0 & (OPL - 1));
+
+    // the first record chunk is in flight while the ops are evaluated
+    uint32_t rec[VRPT];
+#pragma unroll
+    for (int j = 0; j < VRPT; ++j) {
+      const uint64_t q = m.rk0 + (uint64_t)j * WAVE + lane;
+      rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+    }
+    for (uint32_t g = lane; g < G; g += WAVE) s.mb[g] = PNONE, s.mk[g] = PNONE;
+
+    // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
+    Acc<DMAX> a;
+    a.reset();
+    for (uint64_t t = t0; t < m.off1; t += TILE) {
+      const uint64_t g = t + (uint64_t)lane * OPL;
+      uint32_t ib = 0;
+      if (g < m.off1) {
+        uint64_t wv[OPL];
+        uint32_t sp[OPL], mf[OPL] = {};
+        uint64_t tx[OPL] = {};
+#pragma unroll
+        for (int k = 0; k < OPL; ++k) sp[k] = u.allmask;
+        if (GENERAL && L.snap_pres) ld_n32<OPL>(L.snap_pres + g, sp);
+        if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
+        if (PACKED) {
+          int32_t sd[OPL][DMAX];
+          ld_n64<OPL>(L.ct_meta + g, wv);
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint32_t q[OPL] = {};
+            if (d < (int)nd) ld_n32<OPL>((const uint32_t *)L.snap_delta + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) sd[k][d] = (int32_t)q[k];
+          }
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) {
+            const uint64_t p = g + k;
+            if (p >= m.off0 && p < m.off1 &&
+                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a))
+              ib |= 1u << k;
+          }
+        } else {
+          uint64_t svf[OPL][DMAX];
+          ld_n64<OPL>(L.commit_time + g, wv);
+          const uint32_t m4 = OPL == 4 ? *(const uint32_t *)(L.op_meta + g) : (uint32_t)*(const uint16_t *)(L.op_meta + g);
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) mf[k] = (m4 >> (8 * k)) & 0xFFu;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint64_t q[OPL] = {};
+            if (d < (int)nd) ld_n64<OPL>(L.snap_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) svf[k][d] = q[k];
+          }
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) {
+            const uint64_t p = g + k;
+            if (p >= m.off0 && p < m.off1 &&
+                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a))
+              ib |= 1u << k;
+          }
+        }
+      }
+      uint32_t word = ib << (OPL * (lane % LPW));
+#pragma unroll
+      for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
+      if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
+    }
+    wave_sync();
+
+    // ---- 2. records of included ops -> newest birth / kill per group ----
+    for (uint64_t q0 = m.rk0;;) {
+#pragma unroll
+      for (int j = 0; j < VRPT; ++j) {
+        const uint32_t x = rec[j];
+        if (x == 0xFFFFFFFFu) continue;
+        const uint32_t op = AM_REC_OP(x), bit = op + sh;
+        if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
+        atomicMax((x & AM_REC_KILL) ? &s.mk[AM_REC_GRP(x)] : &s.mb[AM_REC_GRP(x)], (int32_t)op);
+      }
+      q0 += (uint64_t)VRPT * WAVE;
+      if (q0 >= m.rk1) break;
+#pragma unroll
+      for (int j = 0; j < VRPT; ++j) {
+        const uint64_t q = q0 + (uint64_t)j * WAVE + lane;
+        rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+      }
+    }
+    wave_sync();
+
+    // ---- 3. scalar outputs (VGPR wave reductions) ----
+    const uint32_t count = wave_sum_u32_v(a.count), flags = wave_or_u32_v(a.flags), pres = wave_or_u32_v(a.pres);
+    const uint64_t min_excl = wave_min_u64_v(a.min_excl);
+    int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+    const bool ign = u.base_ignore && count == 0;
+    const uint32_t opres = ign ? 0u : (pres | u.cpres);
+    uint64_t myct = 0;  // lane d: LastOpCt entry d
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d >= (int)nd) continue;
+      const uint64_t x = wave_max_u64_v(a.mx[d]);
+      const uint64_t v = x > u.C0[d] ? x : u.C0[d];
+      if ((uint32_t)d == lane) myct = ((opres >> d) & 1u) ? v : 0;
+    }
+
+    // ---- 4. survivors in group order -> the output CSR ----
+    uint32_t ns = 0;
+    if (status == AM_OK) {
+      const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
+      for (uint32_t g0 = 0; g0 < G; g0 += WAVE) {
+        const uint32_t g = g0 + lane;
+        bool alive = false;
+        if (g < G) {
+          const int32_t b = s.mb[g];
+          alive = b != PNONE && b >= s.mk[g];
+        }
+        const uint64_t bm = __ballot(alive);
+        if (alive) {
+          const uint64_t o = ns + (uint32_t)__popcll(bm & lt);
+          if (o < ocap) {
+            R.value.set_a[ooff + o] = L.grp_a[m.rk0 + g];
+            R.value.set_b[ooff + o] = L.grp_b[m.rk0 + g];
+          }
+        }
+        ns += (uint32_t)__popcll(bm);
+      }
+      if (ns > ocap) status = AM_ERR_CAPACITY;
+    }
+    if (status == AM_OK && lane < nd) R.last_ct[(uint64_t)lane * B.n_reads + r] = myct;
+    if (lane == 0) {
+      R.status[r] = status;
+      R.flags[r] = (uint8_t)(flags & 0xFFu);
+      if (status == AM_OK) {
+        R.new_last_op[r] = new_last_op(L, m.key, m.off0, m.off1, min_excl);
+        R.last_ct_ignore[r] = ign ? 1 : 0;
+        R.last_ct_pres[r] = opres;
+        R.is_new_ss[r] = count > 0;
+        R.count[r] = count;
+        R.value.set_len[r] = ns;
+      }
+    }
+    wave_sync();
+  }
+}
+
+// ---------------------------------------------------------------- 16-lane row per short read
+// A wave takes 64 reads at a time: lane i checks read i against the row limits (the others
+// leave through one hand-off atomic per wave), then the four 16-lane rows walk the
+// eligible reads, one read per row per step: op sl + 16k, records sl + 16j, groups sl + 16j.
+constexpr uint32_t ROW_OPS = 64, ROW_REC = 128, ROW_G = 64;
+constexpr int RG = 16;
+
+struct RowGSmem {
+  int32_t mb[ROW_G], mk[ROW_G];
+};
+
+template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
+__global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                   am_retry next) {
+  __shared__ RowGSmem rsm[BLOCK / RG];
+  RowGSmem &s = rsm[threadIdx.x / RG];
+  const uint32_t lane = threadIdx.x & (WAVE - 1), row = lane / RG, sl = lane % RG;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t nd = EXACT ? (uint32_t)DMAX : L.n_dc;  // EXACT: n_dc == DMAX, no per-DC guards
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+  const uint64_t W = (uint64_t)gridDim.x * (BLOCK / WAVE);
+  const uint64_t gw = (uint64_t)blockIdx.x * (BLOCK / WAVE) + uniform_u32(threadIdx.x >> 6);
+  const uint64_t n_batches = (nsel + WAVE - 1) / WAVE;
+
+  for (uint64_t bid = gw; bid < n_batches; bid += W) {
+    // ---- lane i: read rb + i, checked against the row limits ----
+    const uint64_t rb = bid * WAVE;
+    const uint32_t nb = (uint32_t)(nsel - rb < (uint64_t)WAVE ? nsel - rb : (uint64_t)WAVE);
+    GMeta mi;
+    mi.st = AM_OK, mi.G = AM_NGRP_NONE, mi.off0 = mi.off1 = mi.rk0 = mi.rk1 = 0, mi.key = 0, mi.r = 0;
+    if (lane < nb) read_meta(L, B, S.idx ? (uint64_t)S.idx[sel0 + rb + lane] : rb + lane, TYPE, mi);
+    const bool ok_i = lane < nb && mi.st == AM_OK && mi.G != AM_NGRP_NONE && mi.off1 - mi.off0 <= ROW_OPS &&
+                      mi.rk1 - mi.rk0 <= ROW_REC && mi.G <= ROW_G && !has_base_pairs(B, mi.r);
+    if (lane < nb && mi.st != AM_OK) R.status[mi.r] = mi.st, R.flags[mi.r] = 0;
+    const uint64_t hm = __ballot(lane < nb && mi.st == AM_OK && !ok_i);
+    if (hm) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(next.count, (uint32_t)__popcll(hm));
+      base = uniform_u32(base);
+      if ((hm >> lane) & 1ull) next.list[base + (uint32_t)__popcll(hm & lt)] = (uint32_t)mi.r;
+    }
+    uint64_t emask = __ballot(ok_i);
+    while (emask) {
+      // row q takes the q-th eligible read left in the batch
+      uint64_t mm = emask;
+      for (uint32_t q = 0; q < row && mm; ++q) mm &= mm - 1;
+      const bool ok = mm != 0;
+      const uint32_t j = ok ? (uint32_t)__builtin_ctzll(mm) : 0u;
+      for (uint32_t q = 0; q < 4 && emask; ++q) emask &= emask - 1;
+      GMeta m;
+      m.r = shfl_u64(mi.r, j), m.key = shfl_u64(mi.key, j);
+      m.off0 = shfl_u64(mi.off0, j), m.off1 = shfl_u64(mi.off1, j);
+      m.rk0 = shfl_u64(mi.rk0, j), m.rk1 = shfl_u64(mi.rk1, j);
+      m.G = shfl_u32(mi.G, j), m.st = AM_OK;
+      ReadU<DMAX> u;
+      if (ok) {
+        read_inputs<DMAX, GENERAL, false>(L, nd, B, m.r, u);
+      } else {
+        u.allmask = 0, u.spres = 0, u.cpres = 0, u.base_ignore = true, u.has_txid = false, u.txid = 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) u.S[d] = 0, u.C0[d] = 0;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < ROW_G / RG; ++k) s.mb[sl + RG * k] = PNONE, s.mk[sl + RG * k] = PNONE;
+      // the read's records (one per lane and step), in flight with the ops
+      uint32_t rec[ROW_REC / RG];
+#pragma unroll
+      for (uint32_t k = 0; k < ROW_REC / RG; ++k) {
+        const uint64_t q = m.rk0 + sl + RG * k;
+        rec[k] = (ok && q < m.rk1) ? L.rec_g[q] : 0xFFFFFFFFu;
+      }
+      // ---- ops: op sl + 16k of the read ----
+      Acc<DMAX> a;
+      a.reset();
+      uint64_t incl = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < ROW_OPS / RG; ++k) {
+        const uint64_t p = m.off0 + sl + RG * k;
+        bool in = false;
+        if (ok && p < m.off1) {
+          uint32_t sp = u.allmask;
+          uint64_t tx = 0;
+          if (GENERAL && L.snap_pres) sp = L.snap_pres[p];
+          if (GENERAL && u.has_txid) tx = L.op_txid[p];
+          if (PACKED) {
+            int32_t sd[DMAX];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) sd[d] = d < (int)nd ? L.snap_delta[(uint64_t)d * stride + p] : 0;
+            in = eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, L.ct_meta[p], sd, nullptr, 0, sp, tx, a);
+          } else {
+            uint64_t svf[DMAX];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+            in = eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, L.commit_time[p], nullptr, svf, L.op_meta[p], sp, tx, a);
+          }
+        }
+        incl |= ((__ballot(in) >> (row * RG)) & 0xFFFFull) << (RG * k);
+      }
+      wave_sync();
+      // ---- records of included ops -> newest birth / kill per group ----
+#pragma unroll
+      for (uint32_t k = 0; k < ROW_REC / RG; ++k) {
+        const uint32_t x = rec[k];
+        if (x == 0xFFFFFFFFu) continue;
+        const uint32_t op = AM_REC_OP(x);
+        if (!((incl >> op) & 1ull)) continue;
+        atomicMax((x & AM_REC_KILL) ? &s.mk[AM_REC_GRP(x)] : &s.mb[AM_REC_GRP(x)], (int32_t)op);
+      }
+      wave_sync();
+      // ---- scalar outputs: row reductions (full EXEC) ----
+      const uint32_t count = row_sum_u32(a.count), flags = row_or_u32(a.flags), pres = row_or_u32(a.pres);
+      const uint64_t min_excl = row_min_u64(a.min_excl);
+      uint64_t mx[DMAX];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? row_max_u64(a.mx[d]) : 0;
+      int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+      // ---- survivors in group order ----
+      uint32_t ns = 0;
+      const uint64_t ooff = ok ? R.value.set_off[m.r] : 0, ocap = ok ? R.value.set_off[m.r + 1] - ooff : 0;
+#pragma unroll
+      for (uint32_t k = 0; k < ROW_G / RG; ++k) {
+        const uint32_t g = sl + RG * k;
+        const int32_t b = s.mb[g];
+        const bool alive = ok && status == AM_OK && g < m.G && b != PNONE && b >= s.mk[g];
+        const uint32_t rm = (uint32_t)((__ballot(alive) >> (row * RG)) & 0xFFFFu);
+        if (alive) {
+          const uint64_t o = ns + (uint32_t)__popc(rm & ((1u << sl) - 1u));
+          if (o < ocap) {
+            R.value.set_a[ooff + o] = L.grp_a[m.rk0 + g];
+            R.value.set_b[ooff + o] = L.grp_b[m.rk0 + g];
+          }
+        }
+        ns += (uint32_t)__popc(rm);
+      }
+      if (ok && status == AM_OK && ns > ocap) status = AM_ERR_CAPACITY;
+      if (ok && sl == 0) write_scalars<DMAX>(L, nd, B, R, m, u, status, count, flags, pres, min_excl, mx, ns);
+      wave_sync();
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+template <int D, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
+             int tier) {
+  if (tier == AM_GRP_WAVE) {
+    constexpr size_t smem = sizeof(WaveSmem) * NW;
+    static int occ = 0;
+    if (!occ) {
+      AM_HIP(hipFuncSetAttribute((const void *)k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>, BLOCK,
+                                                       smem) != hipSuccess || occ < 1)
+        occ = 1;
+    }
+    uint64_t blocks = (B->n_reads + NW - 1) / NW, cap = (uint64_t)ctx->n_cu * occ;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return AM_OK;
+    hipLaunchKernelGGL((k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), smem,
+                       ctx->stream, *L, *B, *R, S, next);
+  } else if (tier == AM_GRP_ROW) {
+    static int occ = 0;
+    if (!occ) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_grp_row<D, TYPE, GENERAL, PACKED, EXACT>, BLOCK, 0) !=
+              hipSuccess || occ < 1)
+        occ = 2;
+    }
+    const uint64_t waves = (B->n_reads + WAVE - 1) / WAVE;
+    uint64_t blocks = (waves + NW - 1) / NW, cap = (uint64_t)ctx->n_cu * occ;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return AM_OK;
+    hipLaunchKernelGGL((k_grp_row<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), 0,
+                       ctx->stream, *L, *B, *R, S, next);
+  } else {
+    constexpr size_t smem = sizeof(WgSmem<D>);
+    static int occ = 0;
+    if (!occ) {
+      AM_HIP(hipFuncSetAttribute((const void *)k_grp_wg<D, TYPE, GENERAL, PACKED, EXACT>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_grp_wg<D, TYPE, GENERAL, PACKED, EXACT>, WBLOCK, smem) !=
+              hipSuccess || occ < 1)
+        occ = 1;
+    }
+    uint64_t blocks = B->n_reads, cap = (uint64_t)ctx->n_cu * occ;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return AM_OK;
+    hipLaunchKernelGGL((k_grp_wg<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(WBLOCK), smem,
+                       ctx->stream, *L, *B, *R, S, next);
+  }
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
+// kernel variants: the fast path (full clocks, no TxIds / bases / op ids: GENERAL false)
+// over the packed view, with the n_dc == D case specialised; everything else runs GENERAL
+template <int D, int TYPE>
+int launch_v(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
+             int tier) {
+  const bool general = am_batch_general(L, B), packed = am_log_packed(L);
+  if (!general && packed)
+    return L->n_dc == (uint32_t)D ? launch_d<D, TYPE, false, true, true>(ctx, L, B, R, S, next, tier)
+                                  : launch_d<D, TYPE, false, true, false>(ctx, L, B, R, S, next, tier);
+  return packed ? launch_d<D, TYPE, true, true, false>(ctx, L, B, R, S, next, tier)
+                : launch_d<D, TYPE, true, false, false>(ctx, L, B, R, S, next, tier);
+}
+
+}  // namespace amk_grp

@@ -80,12 +80,14 @@ int am_launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
 int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, uint32_t type,
                   am_retry retry);  // am_big.hip: reads beyond the LDS tier
 // Token-group tier (am_group.hip) for add-wins-set / MV-register reads over the packed view
-// and the token-group view: rows = true is the 16-lane-row kernel for short logs, false the
-// workgroup-per-read kernel.  Reads it does not take (ungrouped keys, base-snapshot pairs,
-// longer logs; for the row kernel also anything beyond its row limits) go to `next`.
+// and the token-group view, three kernels by read size: AM_GRP_ROW (16-lane row per short
+// log), AM_GRP_WAVE (wave per read), AM_GRP_WG (512-thread workgroup per read).  Reads a
+// kernel does not take (ungrouped keys, base-snapshot pairs, logs beyond its limits) go to
+// `next`.
+enum { AM_GRP_ROW = 0, AM_GRP_WAVE = 1, AM_GRP_WG = 2 };
 bool am_group_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
 int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
-                    uint32_t type, am_retry next, bool rows);
+                    uint32_t type, am_retry next, int tier);
 // the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp_a,
                           uint64_t *grp_b, uint32_t *key_ngrp);

@@ -139,10 +139,10 @@ int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
 }
 
 // Set types over selection S.
-//   add-wins set / MV register: token-group tier, row kernel (short logs) -> (hand-off list)
-//     workgroup kernel -> (hand-off list) LDS-sort tier k_sets -> (retry list) big-read tier
+//   add-wins set / MV register: token-group tier, row kernel (short logs) -> wave kernel ->
+//     workgroup kernel -> (hand-off lists) LDS-sort tier k_sets -> (retry list) big-read tier
 //   bounded counter: row tier -> (hand-off list) k_sets -> (retry list) big-read tier
-// rows_buf / grp_buf: [0] = 0, [1] = hand-off count, list at +64.
+// rows_buf / grp_buf (two lists): [0] = 0, [1] = hand-off count, list at +64.
 int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
              uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf) {
   am_retry retry;
@@ -162,21 +162,19 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     cur.idx = C.list;
     cur.range = rows_buf;
   } else if (grp_buf && am_group_applies(L, R, type)) {
-    AM_HIP(hipMemsetAsync(rows_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
-    AM_HIP(hipMemsetAsync(grp_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
-    am_retry n1, n2;
-    n1.count = rows_buf + 1;
-    n1.list = rows_buf + 64;
-    n2.count = grp_buf + 1;
-    n2.list = grp_buf + 64;
-    rc = am_launch_group(ctx, L, B, R, S, type, n1, true);
-    if (rc) return rc;
-    cur.idx = n1.list;
-    cur.range = rows_buf;
-    rc = am_launch_group(ctx, L, B, R, cur, type, n2, false);
-    if (rc) return rc;
-    cur.idx = n2.list;
-    cur.range = grp_buf;
+    // row -> wave -> workgroup kernels; each hands what it does not take to the next
+    uint32_t *bufs[3] = {rows_buf, grp_buf, grp_buf + (B->n_reads + 64)};
+    for (int k = 0; k < 3; ++k) AM_HIP(hipMemsetAsync(bufs[k], 0, 2 * sizeof(uint32_t), ctx->stream));
+    const int tiers[3] = {AM_GRP_ROW, AM_GRP_WAVE, AM_GRP_WG};
+    for (int k = 0; k < 3; ++k) {
+      am_retry nx;
+      nx.count = bufs[k] + 1;
+      nx.list = bufs[k] + 64;
+      rc = am_launch_group(ctx, L, B, R, cur, type, nx, tiers[k]);
+      if (rc) return rc;
+      cur.idx = nx.list;
+      cur.range = bufs[k];
+    }
   }
   rc = am_launch_sets(ctx, L, B, R, cur, type, retry);
   if (rc) return rc;
@@ -209,7 +207,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   {
     int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
     if (!rc && B->type_hint != AM_PN && B->type_hint != AM_LWW && B->type_hint != AM_BCOUNTER)
-      rc = am_ctx_scratch(ctx, AM_SCR_GRP, (n + 64) * sizeof(uint32_t), &grp_scr);
+      rc = am_ctx_scratch(ctx, AM_SCR_GRP, 2 * (n + 64) * sizeof(uint32_t), &grp_scr);
     if (rc) return rc;
   }
   if (B->type_hint == AM_PN || B->type_hint == AM_LWW)
