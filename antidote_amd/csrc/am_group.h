@@ -25,9 +25,11 @@
 // 1024 groups; k_grp_wg: one 512-thread workgroup per read, up to 2048 groups):
 //   1. the read's ops stream in 1024-op tiles (packed view, 16-byte loads): is_op_in_snapshot/7
 //      per op (am_wave.h eval_op) -> an LDS inclusion bitmap + the scalar outputs;
-//   2. the read's records (4 B each) stream in: an included birth / kill does one LDS
-//      atomicMax of its op index into the group's max-birth / max-kill slot;
-//   3. the groups are scanned in order: survivors (max birth >= max kill) are compacted by
+//   2. the read's records (4 B each) stream in: an included birth sets its group's BORN bit,
+//      an included kill its KILLED bit (LDS atomicOr; the builder keeps only EFFECTIVE kills,
+//      those after the group's birth -- a kill in the birth's own op or earlier never
+//      removes it: ToAdd ++ (Current -- ToRemove), MV drops before inserting);
+//   3. the groups are scanned in order: survivors (born and not killed) are compacted by
 //      wave ballots and their (a, b) pairs gathered into the output CSR -- already in the
 //      reference's order, no sort.
 // Reads with base-snapshot pairs, longer logs or ungrouped keys are handed to the next tier.
@@ -40,7 +42,6 @@ using namespace amk;
 constexpr int BLOCK = 256;
 constexpr int NW = BLOCK / WAVE;
 constexpr uint32_t RCAP = AM_GRP_MAX_REC;
-constexpr int32_t PNONE = (int32_t)0x80000000;
 constexpr uint32_t KILL31 = 0x80000000u;
 
 // ================================================================ reads
@@ -101,25 +102,27 @@ __device__ __forceinline__ void read_inputs(const am_op_log &L, uint32_t nd, con
   u.txid = u.has_txid ? u64(B.txid[r]) : 0;
 }
 
-// one op of the log: inclusion (is_op_in_snapshot/7) from the packed or the full view
+// one op of the log: inclusion (is_op_in_snapshot/7) from the packed or the full view.
+// An op the packed view could not hold (AM_CT_ESC) is not evaluated here: esc is set and
+// the caller's escape pass (esc_pass) evaluates it from the full columns, off the hot loop
+// (loads and addresses for the full columns in the streaming loop cost registers and
+// break the loop's counted load waits).
 template <int DMAX, bool GENERAL, bool PACKED>
 __device__ __forceinline__ bool eval_at(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t p, uint64_t stride,
                                         uint64_t w /* ct_meta | commit_time */, const int32_t *sd,
                                         const uint64_t *svf, uint32_t meta_full, uint32_t sp, uint64_t tx,
-                                        Acc<DMAX> &a) {
+                                        Acc<DMAX> &a, bool &esc) {
   uint32_t meta;
   uint64_t ct, sv[DMAX];
   if (PACKED) {
-    meta = (uint32_t)(w >> 56);
-    if (w & AM_CT_ESC) {  // rare: the op does not fit the packed view
-      ct = L.commit_time[p];
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-    } else {
-      ct = w & (AM_CT_ESC - 1);
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) sv[d] = ct - (uint64_t)(int64_t)sd[d];
+    if (w & AM_CT_ESC) {
+      esc = true;
+      return false;
     }
+    meta = (uint32_t)(w >> 56);
+    ct = w & (AM_CT_ESC - 1);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sv[d] = ct - (uint64_t)(int64_t)sd[d];
   } else {
     meta = meta_full;
     ct = w;
@@ -128,6 +131,26 @@ __device__ __forceinline__ bool eval_at(const am_op_log &L, uint32_t nd, const R
   }
   const bool txm = GENERAL && u.has_txid && tx == u.txid;
   return eval_op<DMAX, GENERAL>(u, meta, ct, sv, sp, txm, p, a) && !(meta & AM_META_BAD);
+}
+
+// the escaped ops of ops [off0, off1) handled by this lane (p = off0 + lane0, step nl), from
+// the full columns; included ones are OR-ed into the LDS bitmap (bit = p - t0)
+template <int DMAX, bool GENERAL>
+__device__ __forceinline__ void esc_pass(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t off0,
+                                      uint64_t off1, uint64_t t0, uint64_t stride, uint32_t lane0, uint32_t nl,
+                                      uint32_t *incl, Acc<DMAX> &a) {
+  for (uint64_t p = off0 + lane0; p < off1; p += nl) {
+    const uint64_t w = L.ct_meta[p];
+    if (!(w & AM_CT_ESC)) continue;
+    uint64_t sv[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+    const uint32_t meta = (uint32_t)(w >> 56);
+    const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
+    const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
+    if (eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], sv, sp, txm, p, a) && !(meta & AM_META_BAD))
+      atomicOr(&incl[(uint32_t)((p - t0) >> 5)], 1u << ((p - t0) & 31));
+  }
 }
 
 // NewLastOp: id of the oldest excluded candidate - 1, else get_first_id/1 (the newest op's id)
@@ -179,7 +202,7 @@ constexpr int wopl() { return DMAX >= 8 ? 2 : 4; }
 
 template <int DMAX>
 struct WgSmem {
-  int32_t mb[RCAP], mk[RCAP];   // per group: newest included birth / kill op (PNONE: none)
+  uint32_t born[RCAP / 32], killed[RCAP / 32];  // per group: birth included / an effective kill included
   uint32_t incl[IWORDS];        // included ops, bit = op - (off0 & ~(OPL-1))
   uint64_t red[WNW][4 + DMAX];  // per-wave partials: count, flags, pres, min_excl, mx[]
   uint32_t wsum[WNW];
@@ -248,11 +271,12 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
       const uint64_t q = m.rk0 + (uint64_t)j * WBLOCK + tid;
       rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
     }
-    for (uint32_t g = tid; g < G; g += WBLOCK) s.mb[g] = PNONE, s.mk[g] = PNONE;
+    for (uint32_t g = tid; g < (G + 31) / 32; g += WBLOCK) s.born[g] = 0, s.killed[g] = 0;
 
     // ---- 1. inclusion per op -> bitmap + scalar partials ----
     Acc<DMAX> a;
     a.reset();
+    bool esc = false;  // some op of this lane did not fit the packed view
     for (uint64_t t = t0; t < m.off1; t += TILE) {
       const uint64_t g = t + (uint64_t)tid * OPL;
       uint32_t ib = 0;
@@ -278,7 +302,7 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
           for (int k = 0; k < OPL; ++k) {
             const uint64_t p = g + k;
             if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a))
+                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a, esc))
               ib |= 1u << k;
           }
         } else {
@@ -298,7 +322,7 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
           for (int k = 0; k < OPL; ++k) {
             const uint64_t p = g + k;
             if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a))
+                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a, esc))
               ib |= 1u << k;
           }
         }
@@ -310,6 +334,8 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
       for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
       if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + tid / LPW] = word;
     }
+    if (PACKED && __syncthreads_or(esc))  // rare: ops outside the packed view, from the full columns
+      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, tid, WBLOCK, s.incl, a);
     {  // wave partials of the scalar outputs (VGPR reductions: the scalar file is full)
       const uint32_t cnt = wave_sum_u32_v(a.count), fl = wave_or_u32_v(a.flags), pr = wave_or_u32_v(a.pres);
       const uint64_t mn = wave_min_u64_v(a.min_excl);
@@ -331,7 +357,7 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
         if (x == 0xFFFFFFFFu) continue;
         const uint32_t op = AM_REC_OP(x), bit = op + sh;
         if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
-        atomicMax((x & AM_REC_KILL) ? &s.mk[AM_REC_GRP(x)] : &s.mb[AM_REC_GRP(x)], (int32_t)op);
+        atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
       }
       q0 += RPASS;
       if (q0 >= m.rk1) break;
@@ -361,10 +387,7 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
       for (uint32_t g0 = 0; g0 < G; g0 += WBLOCK) {
         const uint32_t g = g0 + tid;
         bool alive = false;
-        if (g < G) {
-          const int32_t b = s.mb[g];
-          alive = b != PNONE && b >= s.mk[g];
-        }
+        if (g < G) alive = ((s.born[g >> 5] & ~s.killed[g >> 5]) >> (g & 31)) & 1u;
         const uint64_t bm = __ballot(alive);
         if (lane == 0) s.wsum[w] = (uint32_t)__popcll(bm);
         __syncthreads();
@@ -421,12 +444,12 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
 // 256-thread workgroup runs its own reads with no workgroup barrier -- LDS is carved per
 // wave (group slots + inclusion bitmap) -- so a CU keeps ~16 reads in flight and one read's
 // dependent steps (metadata -> ops + records -> survivors' pairs) hide behind the others.
-constexpr uint32_t VG = 1024;              // groups of a wave-kernel read
+constexpr uint32_t VG = AM_GRP_MAX_REC;    // groups of a wave-kernel read
 constexpr uint32_t VOPS = 8192;            // ops of a wave-kernel read
 constexpr uint32_t VWORDS = VOPS / 32 + 8;
 constexpr int VRPT = 8;                    // records per lane per chunk (512 per wave)
 struct WaveSmem {
-  int32_t mb[VG], mk[VG];
+  uint32_t born[VG / 32], killed[VG / 32];
   uint32_t incl[VWORDS];
 };
 template <int DMAX>
@@ -477,11 +500,12 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
       const uint64_t q = m.rk0 + (uint64_t)j * WAVE + lane;
       rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
     }
-    for (uint32_t g = lane; g < G; g += WAVE) s.mb[g] = PNONE, s.mk[g] = PNONE;
+    for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
 
     // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
     Acc<DMAX> a;
     a.reset();
+    bool esc = false;  // some op of this lane did not fit the packed view
     for (uint64_t t = t0; t < m.off1; t += TILE) {
       const uint64_t g = t + (uint64_t)lane * OPL;
       uint32_t ib = 0;
@@ -507,7 +531,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
           for (int k = 0; k < OPL; ++k) {
             const uint64_t p = g + k;
             if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a))
+                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a, esc))
               ib |= 1u << k;
           }
         } else {
@@ -527,7 +551,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
           for (int k = 0; k < OPL; ++k) {
             const uint64_t p = g + k;
             if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a))
+                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a, esc))
               ib |= 1u << k;
           }
         }
@@ -538,6 +562,10 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
       if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
     }
     wave_sync();
+    if (PACKED && __ballot(esc)) {  // rare: ops outside the packed view, from the full columns
+      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, lane, WAVE, s.incl, a);
+      wave_sync();
+    }
 
     // ---- 2. records of included ops -> newest birth / kill per group ----
     for (uint64_t q0 = m.rk0;;) {
@@ -547,7 +575,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
         if (x == 0xFFFFFFFFu) continue;
         const uint32_t op = AM_REC_OP(x), bit = op + sh;
         if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
-        atomicMax((x & AM_REC_KILL) ? &s.mk[AM_REC_GRP(x)] : &s.mb[AM_REC_GRP(x)], (int32_t)op);
+        atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
       }
       q0 += (uint64_t)VRPT * WAVE;
       if (q0 >= m.rk1) break;
@@ -581,10 +609,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
       for (uint32_t g0 = 0; g0 < G; g0 += WAVE) {
         const uint32_t g = g0 + lane;
         bool alive = false;
-        if (g < G) {
-          const int32_t b = s.mb[g];
-          alive = b != PNONE && b >= s.mk[g];
-        }
+        if (g < G) alive = ((s.born[g >> 5] & ~s.killed[g >> 5]) >> (g & 31)) & 1u;
         const uint64_t bm = __ballot(alive);
         if (alive) {
           const uint64_t o = ns + (uint32_t)__popcll(bm & lt);
@@ -622,7 +647,7 @@ constexpr uint32_t ROW_OPS = 64, ROW_REC = 128, ROW_G = 64;
 constexpr int RG = 16;
 
 struct RowGSmem {
-  int32_t mb[ROW_G], mk[ROW_G];
+  uint32_t born[ROW_G / 32], killed[ROW_G / 32];
 };
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
@@ -678,8 +703,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) u.S[d] = 0, u.C0[d] = 0;
       }
-#pragma unroll
-      for (uint32_t k = 0; k < ROW_G / RG; ++k) s.mb[sl + RG * k] = PNONE, s.mk[sl + RG * k] = PNONE;
+      if (sl < ROW_G / 32) s.born[sl] = 0, s.killed[sl] = 0;
       // the read's records (one per lane and step), in flight with the ops
       uint32_t rec[ROW_REC / RG];
 #pragma unroll
@@ -690,6 +714,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
       // ---- ops: op sl + 16k of the read ----
       Acc<DMAX> a;
       a.reset();
+      bool esc = false;
       uint64_t incl = 0;
 #pragma unroll
       for (uint32_t k = 0; k < ROW_OPS / RG; ++k) {
@@ -704,15 +729,33 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
             int32_t sd[DMAX];
 #pragma unroll
             for (int d = 0; d < DMAX; ++d) sd[d] = d < (int)nd ? L.snap_delta[(uint64_t)d * stride + p] : 0;
-            in = eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, L.ct_meta[p], sd, nullptr, 0, sp, tx, a);
+            in = eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, L.ct_meta[p], sd, nullptr, 0, sp, tx, a, esc);
           } else {
             uint64_t svf[DMAX];
 #pragma unroll
             for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-            in = eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, L.commit_time[p], nullptr, svf, L.op_meta[p], sp, tx, a);
+            in = eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, L.commit_time[p], nullptr, svf, L.op_meta[p], sp, tx, a, esc);
           }
         }
         incl |= ((__ballot(in) >> (row * RG)) & 0xFFFFull) << (RG * k);
+      }
+      if (PACKED && __ballot(esc)) {  // rare: ops outside the packed view, from the full columns
+#pragma unroll
+        for (uint32_t k = 0; k < ROW_OPS / RG; ++k) {
+          const uint64_t p = m.off0 + sl + RG * k;
+          bool in = false;
+          if (ok && p < m.off1 && (L.ct_meta[p] & AM_CT_ESC)) {
+            uint64_t svf[DMAX];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+            const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
+            const uint64_t tx = (GENERAL && u.has_txid) ? L.op_txid[p] : 0;
+            bool e2 = false;
+            in = eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, L.commit_time[p], nullptr, svf,
+                                                (uint32_t)(L.ct_meta[p] >> 56), sp, tx, a, e2);
+          }
+          incl |= ((__ballot(in) >> (row * RG)) & 0xFFFFull) << (RG * k);
+        }
       }
       wave_sync();
       // ---- records of included ops -> newest birth / kill per group ----
@@ -722,7 +765,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
         if (x == 0xFFFFFFFFu) continue;
         const uint32_t op = AM_REC_OP(x);
         if (!((incl >> op) & 1ull)) continue;
-        atomicMax((x & AM_REC_KILL) ? &s.mk[AM_REC_GRP(x)] : &s.mb[AM_REC_GRP(x)], (int32_t)op);
+        atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
       }
       wave_sync();
       // ---- scalar outputs: row reductions (full EXEC) ----
@@ -738,8 +781,8 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
 #pragma unroll
       for (uint32_t k = 0; k < ROW_G / RG; ++k) {
         const uint32_t g = sl + RG * k;
-        const int32_t b = s.mb[g];
-        const bool alive = ok && status == AM_OK && g < m.G && b != PNONE && b >= s.mk[g];
+        const bool alive =
+            ok && status == AM_OK && g < m.G && (((s.born[g >> 5] & ~s.killed[g >> 5]) >> (g & 31)) & 1u);
         const uint32_t rm = (uint32_t)((__ballot(alive) >> (row * RG)) & 0xFFFFu);
         if (alive) {
           const uint64_t o = ns + (uint32_t)__popc(rm & ((1u << sl) - 1u));

@@ -126,7 +126,7 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
   __syncthreads();
   block_sort(s.ka, s.kb, s.kp, n, RCAP);
   const uint32_t G = raw_groups(s, n);
-  // 3. births per group; the closed form needs one birth per kill key (MV: one value)
+  // 3. births per group; the closed form needs one birth per kill key
   for (uint32_t g = tid; g < G; g += BLOCK) s.bc[g] = 0, s.bfirst[g] = 0xFFFFFFFFu;
   __syncthreads();
   for (uint32_t r = tid; r < n; r += BLOCK)
@@ -138,7 +138,7 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
   for (uint32_t r = tid; r < n; r += BLOCK)
     if (!(s.info[r] & KILL31)) {
       const uint32_t g = s.grpof[r];
-      if (TYPE == AM_AWSET ? s.bc[g] > 1 : s.val[r] != s.val[s.bfirst[g]]) s.ctr[1] = 1;
+      if (s.bc[g] > 1) s.ctr[1] = 1;  // a token born twice (AW) / twice or under two values (MV)
     }
   __syncthreads();
   if (s.ctr[1]) {
@@ -169,8 +169,16 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
     grp_b[r0 + j] = TYPE == AM_AWSET ? s.tok[s.rep[rg]] : s.kb[j];
   }
   __syncthreads();
-  for (uint32_t r = tid; r < n; r += BLOCK)
-    rec_g[r0 + r] = (s.info[r] & 0xFFFFu) | ((s.info[r] >> 31) << 16) | (s.fin[s.grpof[r]] << 17);
+  // records; a kill is EFFECTIVE only after its group's birth (a kill in the birth's own op
+  // or before it never removes the token, and a group without a birth is never output):
+  // the others become empty slots (0xFFFFFFFF)
+  for (uint32_t r = tid; r < n; r += BLOCK) {
+    const uint32_t g = s.grpof[r], b = s.bfirst[g];
+    const uint32_t op = s.info[r] & 0xFFFFu;
+    const bool kill = (s.info[r] & KILL31) != 0;
+    const bool keep = !kill || (b != 0xFFFFFFFFu && op > (s.info[b] & 0xFFFFu));
+    rec_g[r0 + r] = keep ? (op | ((kill ? 1u : 0u) << 16) | (s.fin[g] << 17)) : 0xFFFFFFFFu;
+  }
   if (tid == 0) ngrp[k] = G;
   __syncthreads();
 }

@@ -156,17 +156,19 @@ typedef struct am_op_log {
    * A key's distinct kill keys (AW (elem, token), MV token) are its GROUPS, numbered in the
    * reference's output order: AW by elem, then newest birth first (ToAdd ++ Current), MV by
    * (Value, Token) (insert_sorted); groups without a birth last.  One u32 record per
-   * birth/kill, a key's records contiguous and in op order, [rec_key_off[k], rec_key_off[k+1]):
-   *   rec_g = op index within the key (bits 0-15) | kill << 16 | group << 17
+   * birth / EFFECTIVE kill (one that follows its group's birth: a kill in the birth's own op
+   * or earlier never removes the token), a key's records contiguous and in op order,
+   * [rec_key_off[k], rec_key_off[k+1]):
+   *   rec_g = op index within the key (bits 0-15) | kill << 16 | group << 17, or 0xFFFFFFFF
+   *           for a kill slot that is not effective
    * and group g of key k is (grp_a, grp_b)[rec_key_off[k] + g] (AW (elem, token), MV
-   * (Value, Token); kill-only MV groups (0, token)).  key_ngrp[k] = number of groups, or
-   * AM_NGRP_NONE when the key is materialized from var_data instead (more than
+   * (Value, Token); MV groups without a birth (~0, token)).  key_ngrp[k] = number of groups,
+   * or AM_NGRP_NONE when the key is materialized from var_data instead (more than
    * AM_GRP_MAX_REC records or 2^16 ops, or a log outside the closed form: a token born
-   * twice (AW) / under two values (MV)).  A materialization then streams the ops
-   * (inclusion), the records (max birth / kill op per group) and only the surviving
-   * groups' pairs, with no sort.  Ops carrying AM_META_BAD produce no record; an op whose
-   * variable payload is malformed (Type:update/2 would raise) gets AM_META_BAD set in
-   * op_meta and ct_meta. */
+   * twice).  A materialization then streams the ops (inclusion), the records (born / killed
+   * bits per group) and only the surviving groups' pairs, with no sort.  Ops carrying
+   * AM_META_BAD produce no record; an op whose variable payload is malformed (Type:update/2
+   * would raise) gets AM_META_BAD set in op_meta and ct_meta. */
   uint64_t n_rec;
   const uint64_t *rec_key_off; /* [n_keys+1]                                         */
   const uint32_t *rec_g;       /* [n_rec]                                            */
