@@ -53,7 +53,7 @@ class am_op_log(ctypes.Structure):
         ("op_meta", c_void_p), ("commit_time", c_void_p), ("snap_vc", c_void_p), ("snap_pres", c_void_p),
         ("op_txid", c_void_p), ("op_id", c_void_p), ("p0", c_void_p), ("p1", c_void_p),
         ("var_off", c_void_p), ("var_data", c_void_p),
-        ("ct_meta", c_void_p), ("snap_delta", c_void_p),
+        ("key_tbase", c_void_p), ("pk_vc", c_void_p),
         ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp_a", c_void_p),
         ("grp_b", c_void_p), ("key_ngrp", c_void_p),
     ]
@@ -165,7 +165,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 2:
+        if L.am_abi_version() != 3:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

@@ -13,7 +13,8 @@
 //   exclusive scans (hipcub) -> new key_off / var_off bases
 //   k_upd_scatter  one wave per key: survivors, then the key's new ops, copied column by
 //                  column with coalesced stores (positions from ballot prefix counts)
-// with the packed view (am_packop.h) written from the same registers, then the record view
+// with the packed view (am_packop.h; the key's time base re-derived from its first output
+// op) written from the same registers, then the record view
 // (am_store_pack_records) of the new store.  Each column is
 // read once and written once: HBM-bound stream compaction, no atomics.
 //
@@ -119,6 +120,33 @@ __global__ void k_upd_count(UpdArgs A, uint64_t *cnt, uint64_t *vcnt) {
   }
 }
 
+// survivor bits of the pruned chunk [b, min(b + 64, o1)) from the count pass's bitmap
+__device__ __forceinline__ uint64_t chunk_bits(const UpdArgs &A, uint64_t b, uint64_t o1) {
+  const uint32_t sh = (uint32_t)(b & 63);
+  uint64_t mb = A.keep_bits[b >> 6] >> sh;
+  if (sh) mb |= A.keep_bits[(b >> 6) + 1] << (64 - sh);
+  if (o1 - b < WAVE_SZ) mb &= (1ull << (o1 - b)) - 1ull;
+  return mb;
+}
+
+// the packed-view time base of key k in the new log: from its first output op (the first
+// survivor, else the first new op)
+__device__ __forceinline__ uint64_t out_base(const UpdArgs &A, uint64_t k, uint64_t o0, uint64_t o1, bool prune) {
+  const am_op_log *S = &A.L;
+  uint64_t p = ~0ull;
+  if (o1 > o0 && !prune) p = o0;
+  for (uint64_t b = o0; prune && b < o1 && p == ~0ull; b += WAVE_SZ) {
+    const uint64_t mb = chunk_bits(A, b, o1);
+    if (mb) p = b + (uint64_t)__builtin_ctzll(mb);
+  }
+  if (p == ~0ull && A.N.key_off && A.N.key_off[k + 1] > A.N.key_off[k]) S = &A.N, p = A.N.key_off[k];
+  if (p == ~0ull) return 0;
+  const uint64_t ss = S->snap_stride ? S->snap_stride : S->n_ops;
+  uint64_t s[AM_MAX_DC];
+  for (uint32_t d = 0; d < S->n_dc; ++d) s[d] = S->snap_vc[(uint64_t)d * ss + p];
+  return am_pk_base(S->commit_time[p], s, S->n_dc, 0xFFFFFFFFu, AM_META_DC(S->op_meta[p]));
+}
+
 struct OutCols {
   uint64_t *key_id_base, *counter;
   uint8_t *key_type, *key_flags, *gc_flags, *gap;
@@ -126,13 +154,13 @@ struct OutCols {
   uint64_t *commit_time, *snap_vc;
   uint32_t *snap_pres;
   uint64_t *op_txid, *op_id, *p0, *p1, *var_off, *var_data;
-  uint64_t *ct_meta;            // packed view of the new log (am_packop.h)
-  int32_t *snap_delta;
+  uint64_t *key_tbase;          // packed view of the new log (am_packop.h), or null
+  uint32_t *pk_vc;
   uint64_t stride;
 };
 
 __device__ __forceinline__ void put_op(const am_op_log &S, uint64_t p, const OutCols &O, uint64_t q, uint64_t id,
-                                       uint64_t vq) {
+                                       uint64_t vq, uint64_t base) {
   const uint64_t ss = S.snap_stride ? S.snap_stride : S.n_ops;
   const uint32_t all = all_mask(S.n_dc);
   const uint32_t meta = S.op_meta[p];
@@ -140,13 +168,10 @@ __device__ __forceinline__ void put_op(const am_op_log &S, uint64_t p, const Out
   const uint32_t pres = S.snap_pres ? S.snap_pres[p] : all;
   O.op_meta[q] = (uint8_t)meta;
   O.commit_time[q] = ct;
-  bool esc = false;
-  for (uint32_t d = 0; d < S.n_dc; ++d) {
-    const uint64_t v = S.snap_vc[(uint64_t)d * ss + p];
-    O.snap_vc[(uint64_t)d * O.stride + q] = v;
-    O.snap_delta[(uint64_t)d * O.stride + q] = am_pack_delta(ct, v, ((pres & all) >> d) & 1u, esc);
-  }
-  O.ct_meta[q] = am_pack_ct_meta(ct, meta, esc);
+  for (uint32_t d = 0; d < S.n_dc; ++d) O.snap_vc[(uint64_t)d * O.stride + q] = S.snap_vc[(uint64_t)d * ss + p];
+  if (O.pk_vc)
+    am_pk_write(O.pk_vc, O.stride, q, S.n_dc, base, ct, meta,
+                [&](uint32_t d) { return S.snap_vc[(uint64_t)d * ss + p]; });
   if (O.snap_pres) O.snap_pres[q] = pres;
   if (O.op_txid) O.op_txid[q] = S.op_txid ? S.op_txid[p] : ~0ull;
   O.op_id[q] = id;
@@ -176,6 +201,8 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
     uint64_t q = cnt[k], vq = vcnt[k];
     uint64_t kept = 0, first_id = 0, last_id = 0;
     constexpr int DR = DK > 0 ? DK : 1;
+    const uint64_t base = O.pk_vc ? out_base(A, k, o0, o1, prune) : 0;
+    if (O.key_tbase && lane() == 0) O.key_tbase[k] = base;
     const uint64_t sstride = A.L.snap_stride ? A.L.snap_stride : A.L.n_ops;
     const uint32_t all = all_mask(A.L.n_dc);
     for (uint64_t b = o0; b < o1; b += WAVE_SZ) {
@@ -183,15 +210,8 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
       const bool in = p < o1;
       // survivors of a pruned key come from the count pass's bitmap: a chunk with none is
       // skipped without touching its columns, and the predicate is not evaluated again
-      uint64_t mb = 0;
-      if (prune) {
-        const uint32_t sh = (uint32_t)(b & 63);
-        const uint64_t w0 = A.keep_bits[b >> 6];
-        mb = w0 >> sh;
-        if (sh) mb |= A.keep_bits[(b >> 6) + 1] << (64 - sh);
-        if (o1 - b < WAVE_SZ) mb &= (1ull << (o1 - b)) - 1ull;
-        if (!mb) continue;
-      }
+      const uint64_t mb = prune ? chunk_bits(A, b, o1) : 0;
+      if (prune && !mb) continue;
       const bool keep = prune ? ((mb >> lane()) & 1ull) != 0 : in;
       uint64_t x[DR], ct = 0, v0 = 0, v1 = 0;
       uint32_t meta = 0, spres = all;
@@ -215,12 +235,8 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
         if constexpr (DK > 0) {
           O.op_meta[qq] = (uint8_t)meta;
           O.commit_time[qq] = ct;
-          bool esc = false;
-          for (int d = 0; d < DK; ++d) {
-            O.snap_vc[(uint64_t)d * O.stride + qq] = x[d];
-            O.snap_delta[(uint64_t)d * O.stride + qq] = am_pack_delta(ct, x[d], ((spres & all) >> d) & 1u, esc);
-          }
-          O.ct_meta[qq] = am_pack_ct_meta(ct, meta, esc);
+          for (int d = 0; d < DK; ++d) O.snap_vc[(uint64_t)d * O.stride + qq] = x[d];
+          if (O.pk_vc) am_pk_write(O.pk_vc, O.stride, qq, DK, base, ct, meta, [&](uint32_t d) { return x[d]; });
           if (O.snap_pres) O.snap_pres[qq] = spres;
           if (O.op_txid) O.op_txid[qq] = A.L.op_txid ? A.L.op_txid[p] : ~0ull;
           O.op_id[qq] = id;
@@ -233,7 +249,7 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
               for (uint64_t i = A.L.var_off[p], e = A.L.var_off[p + 1]; i < e; ++i) O.var_data[w++] = A.L.var_data[i];
           }
         } else {
-          put_op(A.L, p, O, qq, id, vq + vincl - vl);
+          put_op(A.L, p, O, qq, id, vq + vincl - vl, base);
         }
       }
       const uint32_t lo = __ffsll((unsigned long long)m) - 1, hi = 63 - __clzll((long long)m);
@@ -257,7 +273,7 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
         const uint64_t vl = in ? var_len(A.N, p) : 0;
         const uint64_t vincl = A.N.var_off ? wave_incl_scan(vl) : 0;
         // op_insert_gc: NewId = ets:update_counter(OpsCache, Key, {3, 1})
-        if (in) put_op(A.N, p, O, q + lane(), counter + 1 + (p - n0), vq + vincl - vl);
+        if (in) put_op(A.N, p, O, q + lane(), counter + 1 + (p - n0), vq + vincl - vl, base);
         const uint64_t w = (n1 - b) < WAVE_SZ ? (n1 - b) : WAVE_SZ;
         q += w;
         vq += wave_bcast(vincl, 63);
@@ -404,12 +420,14 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   O.p1 = (uint64_t *)alloc(na * 8, n_out * 8);
   O.var_off = has_var ? (uint64_t *)alloc((n_out + 1) * 8, (n_out + 1) * 8) : nullptr;
   O.var_data = has_var ? (uint64_t *)alloc(v_out * 8 + 32, v_out * 8) : nullptr;
-  O.ct_meta = (uint64_t *)alloc(na * 8, n_out * 8);
-  O.snap_delta = (int32_t *)alloc((size_t)L.n_dc * na * 4, (size_t)L.n_dc * na * 4);  // DC tails zeroed below
+  if (!has_pres) {  // the packed view needs full clocks (am_pack.hip)
+    O.key_tbase = (uint64_t *)alloc(nk * 8 + 8, nk * 8);
+    O.pk_vc = (uint32_t *)alloc((size_t)L.n_dc * na * 4, (size_t)L.n_dc * na * 4);  // DC tails zeroed below
+  }
   uint64_t *key_off = (uint64_t *)alloc((nk + 1) * 8, (nk + 1) * 8);
   for (uint32_t dd = 0; !rc && dd < L.n_dc && na > n_out; ++dd)
     if (hipMemsetAsync(O.snap_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 8, c->stream) != hipSuccess ||
-        hipMemsetAsync(O.snap_delta + (uint64_t)dd * na + n_out, 0, (na - n_out) * 4, c->stream) != hipSuccess)
+        (O.pk_vc && hipMemsetAsync(O.pk_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 4, c->stream) != hipSuccess))
       rc = AM_ERR_HIP;
   if (rc) {
     cleanup();
@@ -453,8 +471,8 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   d.p1 = O.p1;
   d.var_off = O.var_off;
   d.var_data = O.var_data;
-  d.ct_meta = O.ct_meta;
-  d.snap_delta = O.snap_delta;
+  d.key_tbase = O.key_tbase;
+  d.pk_vc = O.pk_vc;
   ns->counter = O.counter;
   rc = am_store_pack_records(ns);  // the packed view was written by k_upd_scatter
   if (rc) {

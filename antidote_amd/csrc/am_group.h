@@ -102,35 +102,91 @@ __device__ __forceinline__ void read_inputs(const am_op_log &L, uint32_t nd, con
   u.txid = u.has_txid ? u64(B.txid[r]) : 0;
 }
 
-// one op of the log: inclusion (is_op_in_snapshot/7) from the packed or the full view.
-// An op the packed view could not hold (AM_CT_ESC) is not evaluated here: esc is set and
-// the caller's escape pass (esc_pass) evaluates it from the full columns, off the hot loop
-// (loads and addresses for the full columns in the streaming loop cost registers and
-// break the loop's counted load waits).
-template <int DMAX, bool GENERAL, bool PACKED>
-__device__ __forceinline__ bool eval_at(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t p, uint64_t stride,
-                                        uint64_t w /* ct_meta | commit_time */, const int32_t *sd,
-                                        const uint64_t *svf, uint32_t meta_full, uint32_t sp, uint64_t tx,
-                                        Acc<DMAX> &a, bool &esc) {
-  uint32_t meta;
-  uint64_t ct, sv[DMAX];
-  if (PACKED) {
-    if (w & AM_CT_ESC) {
-      esc = true;
-      return false;
-    }
-    meta = (uint32_t)(w >> 56);
-    ct = w & (AM_CT_ESC - 1);
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) sv[d] = ct - (uint64_t)(int64_t)sd[d];
+// N consecutive elements per lane (N = 1, 2, 4; 16-byte loads at most)
+template <int N>
+__device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
+  if constexpr (N == 1) {
+    o[0] = *p;
   } else {
-    meta = meta_full;
-    ct = w;
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) sv[d] = svf[d];
+    const u64x2 a = *(const u64x2 *)p;
+    o[0] = a.x, o[1] = a.y;
+    if constexpr (N == 4) {
+      const u64x2 b = *(const u64x2 *)(p + 2);
+      o[2] = b.x, o[3] = b.y;
+    }
   }
-  const bool txm = GENERAL && u.has_txid && tx == u.txid;
-  return eval_op<DMAX, GENERAL>(u, meta, ct, sv, sp, txm, p, a) && !(meta & AM_META_BAD);
+}
+template <int N>
+__device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
+  if constexpr (N == 4) {
+    const u32x4 a = *(const u32x4 *)p;
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w;
+  } else if constexpr (N == 2) {
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    const u32x2_t a = *(const u32x2_t *)p;
+    o[0] = a.x, o[1] = a.y;
+  } else {
+    o[0] = *p;
+  }
+}
+
+// the OPL ops [g, g + OPL) of a read's [off0, off1): inclusion bits (is_op_in_snapshot/7).
+// Packed view: u32 entries relative to the key's time base (am_wave.h pk_eval), partials in
+// ap; an escaped op (pk_vc[0] == AM_PK_ESC) is not evaluated here: esc is set and the
+// caller's escape pass (esc_pass) evaluates it from the full columns, off the hot loop.
+// Full view: eval_op on the u64 columns, partials in a.
+template <int DMAX, int OPL, bool GENERAL, bool PACKED>
+__device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u,
+                                              const PkRead<DMAX> &pk, uint64_t g, uint64_t off0, uint64_t off1,
+                                              uint64_t stride, AccP<DMAX> &ap, Acc<DMAX> &a, bool &esc) {
+  uint32_t ib = 0;
+  uint64_t tx[OPL] = {};
+  if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
+  if (PACKED) {
+    uint32_t x[OPL][DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      uint32_t q[OPL] = {};
+      if (d < (int)nd) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+      for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
+    }
+#pragma unroll
+    for (int k = 0; k < OPL; ++k) {
+      const uint64_t p = g + k;
+      if (p < off0 || p >= off1) continue;
+      if (x[k][0] == AM_PK_ESC) {
+        esc = true;
+        continue;
+      }
+      if (pk_eval<DMAX, GENERAL>(pk, u, x[k], GENERAL && u.has_txid && tx[k] == u.txid, p, ap)) ib |= 1u << k;
+    }
+  } else {
+    uint64_t ct[OPL], sv[OPL][DMAX];
+    uint32_t sp[OPL];
+#pragma unroll
+    for (int k = 0; k < OPL; ++k) sp[k] = u.allmask;
+    if (GENERAL && L.snap_pres) ld_n32<OPL>(L.snap_pres + g, sp);
+    ld_n64<OPL>(L.commit_time + g, ct);
+    const uint32_t m4 = OPL == 4 ? *(const uint32_t *)(L.op_meta + g)
+                        : OPL == 2 ? (uint32_t)*(const uint16_t *)(L.op_meta + g) : (uint32_t)L.op_meta[g];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      uint64_t q[OPL] = {};
+      if (d < (int)nd) ld_n64<OPL>(L.snap_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+      for (int k = 0; k < OPL; ++k) sv[k][d] = q[k];
+    }
+#pragma unroll
+    for (int k = 0; k < OPL; ++k) {
+      const uint64_t p = g + k;
+      if (p < off0 || p >= off1) continue;
+      const uint32_t meta = (m4 >> (8 * k)) & 0xFFu;
+      const bool txm = GENERAL && u.has_txid && tx[k] == u.txid;
+      if (eval_op<DMAX, GENERAL>(u, meta, ct[k], sv[k], sp[k], txm, p, a) && !(meta & AM_META_BAD)) ib |= 1u << k;
+    }
+  }
+  return ib;
 }
 
 // the escaped ops of ops [off0, off1) handled by this lane (p = off0 + lane0, step nl), from
@@ -140,16 +196,45 @@ __device__ __forceinline__ void esc_pass(const am_op_log &L, uint32_t nd, const 
                                       uint64_t off1, uint64_t t0, uint64_t stride, uint32_t lane0, uint32_t nl,
                                       uint32_t *incl, Acc<DMAX> &a) {
   for (uint64_t p = off0 + lane0; p < off1; p += nl) {
-    const uint64_t w = L.ct_meta[p];
-    if (!(w & AM_CT_ESC)) continue;
+    if (L.pk_vc[p] != AM_PK_ESC) continue;
     uint64_t sv[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-    const uint32_t meta = (uint32_t)(w >> 56);
+    const uint32_t meta = L.op_meta[p];
     const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
     const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
     if (eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], sv, sp, txm, p, a) && !(meta & AM_META_BAD))
       atomicOr(&incl[(uint32_t)((p - t0) >> 5)], 1u << ((p - t0) & 31));
+  }
+}
+
+// a wave's scalar outputs (in every lane): packed partials (u32, relative to K) and, when
+// `full` (wave-uniform: the full view, or escaped ops), full-width partials.  mxl: lane d's
+// max X[d] over the included ops (0 when none)
+template <int DMAX, bool PACKED>
+__device__ __forceinline__ void wave_scalars(const AccP<DMAX> &ap, const Acc<DMAX> &a, bool full, uint64_t K,
+                                             uint32_t allmask, uint32_t nd, uint32_t lane, uint32_t &count,
+                                             uint32_t &flags, uint32_t &pres, uint64_t &min_excl, uint64_t &mxl) {
+  count = 0, flags = 0, pres = 0, mxl = 0;
+  min_excl = wave_min_u64_v(umin64(ap.min_excl, a.min_excl));
+  if (PACKED) {
+    const uint32_t cp = wave_sum_u32_v(ap.count);
+    count = cp, flags = wave_or_u32_v(ap.flags), pres = cp ? allmask : 0u;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d >= (int)nd) continue;
+      const uint32_t m = wave_max_u32_v(ap.mx[d]);
+      if ((uint32_t)d == lane) mxl = cp ? K + m : 0;
+    }
+  }
+  if (full) {
+    count += wave_sum_u32_v(a.count), flags |= wave_or_u32_v(a.flags), pres |= wave_or_u32_v(a.pres);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d >= (int)nd) continue;
+      const uint64_t m = wave_max_u64_v(a.mx[d]);
+      if ((uint32_t)d == lane) mxl = umax64(mxl, m);
+    }
   }
 }
 
@@ -208,27 +293,6 @@ struct WgSmem {
   uint32_t wsum[WNW];
 };
 
-template <int N>
-__device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
-  const u64x2 a = *(const u64x2 *)p;
-  o[0] = a.x, o[1] = a.y;
-  if constexpr (N == 4) {
-    const u64x2 b = *(const u64x2 *)(p + 2);
-    o[2] = b.x, o[3] = b.y;
-  }
-}
-template <int N>
-__device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
-  if constexpr (N == 4) {
-    const u32x4 a = *(const u32x4 *)p;
-    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w;
-  } else {
-    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-    const u32x2_t a = *(const u32x2_t *)p;
-    o[0] = a.x, o[1] = a.y;
-  }
-}
-
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
 __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                       am_retry next) {
@@ -274,59 +338,17 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
     for (uint32_t g = tid; g < (G + 31) / 32; g += WBLOCK) s.born[g] = 0, s.killed[g] = 0;
 
     // ---- 1. inclusion per op -> bitmap + scalar partials ----
+    PkRead<DMAX> pk;
+    if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[m.key]), pk);
+    AccP<DMAX> ap;
     Acc<DMAX> a;
+    ap.reset();
     a.reset();
     bool esc = false;  // some op of this lane did not fit the packed view
     for (uint64_t t = t0; t < m.off1; t += TILE) {
       const uint64_t g = t + (uint64_t)tid * OPL;
-      uint32_t ib = 0;
-      if (g < m.off1) {
-        uint64_t wv[OPL];
-        uint32_t sp[OPL], mf[OPL] = {};
-        uint64_t tx[OPL] = {};
-#pragma unroll
-        for (int k = 0; k < OPL; ++k) sp[k] = u.allmask;
-        if (GENERAL && L.snap_pres) ld_n32<OPL>(L.snap_pres + g, sp);
-        if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
-        if (PACKED) {
-          int32_t sd[OPL][DMAX];
-          ld_n64<OPL>(L.ct_meta + g, wv);
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            uint32_t q[OPL] = {};
-            if (d < (int)nd) ld_n32<OPL>((const uint32_t *)L.snap_delta + (uint64_t)d * stride + g, q);
-#pragma unroll
-            for (int k = 0; k < OPL; ++k) sd[k][d] = (int32_t)q[k];
-          }
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) {
-            const uint64_t p = g + k;
-            if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a, esc))
-              ib |= 1u << k;
-          }
-        } else {
-          uint64_t svf[OPL][DMAX];
-          ld_n64<OPL>(L.commit_time + g, wv);
-          const uint32_t m4 = OPL == 4 ? *(const uint32_t *)(L.op_meta + g) : (uint32_t)*(const uint16_t *)(L.op_meta + g);
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) mf[k] = (m4 >> (8 * k)) & 0xFFu;
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            uint64_t q[OPL] = {};
-            if (d < (int)nd) ld_n64<OPL>(L.snap_vc + (uint64_t)d * stride + g, q);
-#pragma unroll
-            for (int k = 0; k < OPL; ++k) svf[k][d] = q[k];
-          }
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) {
-            const uint64_t p = g + k;
-            if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a, esc))
-              ib |= 1u << k;
-          }
-        }
-      }
+      const uint32_t ib =
+          g < m.off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, m.off0, m.off1, stride, ap, a, esc) : 0u;
       // 32 / OPL lanes -> one bitmap word
       constexpr uint32_t LPW = 32 / OPL;
       uint32_t word = ib << (OPL * (lane % LPW));
@@ -334,18 +356,15 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
       for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
       if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + tid / LPW] = word;
     }
-    if (PACKED && __syncthreads_or(esc))  // rare: ops outside the packed view, from the full columns
+    const bool full = !PACKED || __syncthreads_or(esc);
+    if (PACKED && full)  // rare: ops outside the packed view, from the full columns
       esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, tid, WBLOCK, s.incl, a);
     {  // wave partials of the scalar outputs (VGPR reductions: the scalar file is full)
-      const uint32_t cnt = wave_sum_u32_v(a.count), fl = wave_or_u32_v(a.flags), pr = wave_or_u32_v(a.pres);
-      const uint64_t mn = wave_min_u64_v(a.min_excl);
+      uint32_t cnt, fl, pr;
+      uint64_t mn, mxl;
+      wave_scalars<DMAX, PACKED>(ap, a, full, PACKED ? pk.K : 0, u.allmask, nd, lane, cnt, fl, pr, mn, mxl);
       if (lane == 0) s.red[w][0] = cnt, s.red[w][1] = fl, s.red[w][2] = pr, s.red[w][3] = mn;
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        if (d >= (int)nd) continue;
-        const uint64_t x = wave_max_u64_v(a.mx[d]);
-        if (lane == 0) s.red[w][4 + d] = x;
-      }
+      if (lane < nd) s.red[w][4 + lane] = mxl;
     }
     __syncthreads();
 
@@ -451,9 +470,10 @@ constexpr int VRPT = 8;                    // records per lane per chunk (512 pe
 struct WaveSmem {
   uint32_t born[VG / 32], killed[VG / 32];
   uint32_t incl[VWORDS];
+  uint16_t list[VG];  // surviving groups in order
 };
 template <int DMAX>
-constexpr int vopl() { return DMAX >= 8 ? 2 : 4; }
+constexpr int vopl() { return DMAX <= 8 ? 4 : DMAX <= 16 ? 2 : 1; }  // 32 VGPRs of u32 entries per tile
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
 __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
@@ -492,6 +512,8 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
     read_inputs<DMAX, GENERAL, true>(L, nd, B, r, u);
     const uint64_t t0 = m.off0 & ~(uint64_t)(OPL - 1);
     const uint32_t sh = (uint32_t)(m.off0 & (OPL - 1));
+    // loaded now, used at the end: the output range (lane 0: also the op-id base)
+    const uint64_t ooff = R.value.set_off[r], oend = R.value.set_off[r + 1];
 
     // the first record chunk is in flight while the ops are evaluated
     uint32_t rec[VRPT];
@@ -503,72 +525,39 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
     for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
 
     // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
+    PkRead<DMAX> pk;
+    if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[m.key]), pk);
+    AccP<DMAX> ap;
     Acc<DMAX> a;
+    ap.reset();
     a.reset();
     bool esc = false;  // some op of this lane did not fit the packed view
     for (uint64_t t = t0; t < m.off1; t += TILE) {
       const uint64_t g = t + (uint64_t)lane * OPL;
-      uint32_t ib = 0;
-      if (g < m.off1) {
-        uint64_t wv[OPL];
-        uint32_t sp[OPL], mf[OPL] = {};
-        uint64_t tx[OPL] = {};
-#pragma unroll
-        for (int k = 0; k < OPL; ++k) sp[k] = u.allmask;
-        if (GENERAL && L.snap_pres) ld_n32<OPL>(L.snap_pres + g, sp);
-        if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
-        if (PACKED) {
-          int32_t sd[OPL][DMAX];
-          ld_n64<OPL>(L.ct_meta + g, wv);
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            uint32_t q[OPL] = {};
-            if (d < (int)nd) ld_n32<OPL>((const uint32_t *)L.snap_delta + (uint64_t)d * stride + g, q);
-#pragma unroll
-            for (int k = 0; k < OPL; ++k) sd[k][d] = (int32_t)q[k];
-          }
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) {
-            const uint64_t p = g + k;
-            if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, wv[k], sd[k], nullptr, 0, sp[k], tx[k], a, esc))
-              ib |= 1u << k;
-          }
-        } else {
-          uint64_t svf[OPL][DMAX];
-          ld_n64<OPL>(L.commit_time + g, wv);
-          const uint32_t m4 = OPL == 4 ? *(const uint32_t *)(L.op_meta + g) : (uint32_t)*(const uint16_t *)(L.op_meta + g);
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) mf[k] = (m4 >> (8 * k)) & 0xFFu;
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            uint64_t q[OPL] = {};
-            if (d < (int)nd) ld_n64<OPL>(L.snap_vc + (uint64_t)d * stride + g, q);
-#pragma unroll
-            for (int k = 0; k < OPL; ++k) svf[k][d] = q[k];
-          }
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) {
-            const uint64_t p = g + k;
-            if (p >= m.off0 && p < m.off1 &&
-                eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, wv[k], nullptr, svf[k], mf[k], sp[k], tx[k], a, esc))
-              ib |= 1u << k;
-          }
-        }
-      }
+      const uint32_t ib =
+          g < m.off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, m.off0, m.off1, stride, ap, a, esc) : 0u;
       uint32_t word = ib << (OPL * (lane % LPW));
 #pragma unroll
       for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
       if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
     }
     wave_sync();
-    if (PACKED && __ballot(esc)) {  // rare: ops outside the packed view, from the full columns
+    const bool full = !PACKED || __ballot(esc);
+    if (PACKED && full) {  // rare: ops outside the packed view, from the full columns
       esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, lane, WAVE, s.incl, a);
       wave_sync();
     }
 
-    // ---- 2. records of included ops -> newest birth / kill per group ----
+    // ---- 2. records of included ops -> newest birth / kill per group (the next chunk's
+    //      loads in flight while one chunk is applied) ----
     for (uint64_t q0 = m.rk0;;) {
+      const uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
+      uint32_t nxt[VRPT];
+#pragma unroll
+      for (int j = 0; j < VRPT; ++j) {
+        const uint64_t q = q1 + (uint64_t)j * WAVE + lane;
+        nxt[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+      }
 #pragma unroll
       for (int j = 0; j < VRPT; ++j) {
         const uint32_t x = rec[j];
@@ -577,50 +566,50 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
         if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
         atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
       }
-      q0 += (uint64_t)VRPT * WAVE;
-      if (q0 >= m.rk1) break;
+      if (q1 >= m.rk1) break;
 #pragma unroll
-      for (int j = 0; j < VRPT; ++j) {
-        const uint64_t q = q0 + (uint64_t)j * WAVE + lane;
-        rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
-      }
+      for (int j = 0; j < VRPT; ++j) rec[j] = nxt[j];
+      q0 = q1;
     }
     wave_sync();
 
     // ---- 3. scalar outputs (VGPR wave reductions) ----
-    const uint32_t count = wave_sum_u32_v(a.count), flags = wave_or_u32_v(a.flags), pres = wave_or_u32_v(a.pres);
-    const uint64_t min_excl = wave_min_u64_v(a.min_excl);
+    uint32_t count, flags, pres;
+    uint64_t min_excl, mxl;
+    wave_scalars<DMAX, PACKED>(ap, a, full, PACKED ? pk.K : 0, u.allmask, nd, lane, count, flags, pres, min_excl, mxl);
     int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
     const bool ign = u.base_ignore && count == 0;
     const uint32_t opres = ign ? 0u : (pres | u.cpres);
-    uint64_t myct = 0;  // lane d: LastOpCt entry d
+    uint64_t c0 = 0;  // lane d: LastOpCt entry d
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) {
-      if (d >= (int)nd) continue;
-      const uint64_t x = wave_max_u64_v(a.mx[d]);
-      const uint64_t v = x > u.C0[d] ? x : u.C0[d];
-      if ((uint32_t)d == lane) myct = ((opres >> d) & 1u) ? v : 0;
-    }
+    for (int d = 0; d < DMAX; ++d)
+      if ((uint32_t)d == lane) c0 = u.C0[d];
+    const uint64_t myct = (lane < nd && ((opres >> lane) & 1u)) ? umax64(mxl, c0) : 0;
 
-    // ---- 4. survivors in group order -> the output CSR ----
+    // ---- 4. survivors in group order -> the output CSR.  Lane w owns alive word w (G <=
+    //      2048 = 64 words): a scan of the popcounts places every survivor, the group ids are
+    //      listed in LDS and the pairs gathered 64 at a time, all loads of a pass in flight ----
     uint32_t ns = 0;
     if (status == AM_OK) {
-      const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
-      for (uint32_t g0 = 0; g0 < G; g0 += WAVE) {
-        const uint32_t g = g0 + lane;
-        bool alive = false;
-        if (g < G) alive = ((s.born[g >> 5] & ~s.killed[g >> 5]) >> (g & 31)) & 1u;
-        const uint64_t bm = __ballot(alive);
-        if (alive) {
-          const uint64_t o = ns + (uint32_t)__popcll(bm & lt);
-          if (o < ocap) {
-            R.value.set_a[ooff + o] = L.grp_a[m.rk0 + g];
-            R.value.set_b[ooff + o] = L.grp_b[m.rk0 + g];
-          }
-        }
-        ns += (uint32_t)__popcll(bm);
+      const uint32_t nwd = (G + 31) / 32;
+      const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
+      const uint32_t c = (uint32_t)__popc(aw);
+      const uint32_t inc = wave_incl_scan_u32(c, lane);
+      ns = (uint32_t)__shfl((int)inc, 63, WAVE);
+      uint32_t o = inc - c;
+      for (uint32_t bits = aw; bits; bits &= bits - 1) s.list[o++] = (uint16_t)(lane * 32 + __builtin_ctz(bits));
+      wave_sync();
+      const uint64_t ocap = oend - ooff;
+      const uint32_t nput = (uint64_t)ns < ocap ? ns : (uint32_t)ocap;
+      for (uint32_t j0 = 0; j0 < nput; j0 += 2 * WAVE) {
+        const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
+        uint64_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+        if (j1 < nput) a1 = L.grp_a[m.rk0 + s.list[j1]], b1 = L.grp_b[m.rk0 + s.list[j1]];
+        if (j2 < nput) a2 = L.grp_a[m.rk0 + s.list[j2]], b2 = L.grp_b[m.rk0 + s.list[j2]];
+        if (j1 < nput) R.value.set_a[ooff + j1] = a1, R.value.set_b[ooff + j1] = b1;
+        if (j2 < nput) R.value.set_a[ooff + j2] = a2, R.value.set_b[ooff + j2] = b2;
       }
-      if (ns > ocap) status = AM_ERR_CAPACITY;
+      if ((uint64_t)ns > ocap) status = AM_ERR_CAPACITY;
     }
     if (status == AM_OK && lane < nd) R.last_ct[(uint64_t)lane * B.n_reads + r] = myct;
     if (lane == 0) {
@@ -712,29 +701,38 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
         rec[k] = (ok && q < m.rk1) ? L.rec_g[q] : 0xFFFFFFFFu;
       }
       // ---- ops: op sl + 16k of the read ----
+      PkRead<DMAX> pk;
+      if (PACKED) pk_setup(u, nd, ok ? L.key_tbase[m.key] : 0, pk);
       Acc<DMAX> a;
+      AccP<DMAX> ap;
       a.reset();
+      ap.reset();
       bool esc = false;
       uint64_t incl = 0;
+      // one op from the full columns (full view, or an op outside the packed view)
+      auto eval_full = [&](uint64_t p) -> bool {
+        uint64_t svf[DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+        const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
+        const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
+        const uint32_t meta = L.op_meta[p];
+        return eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], svf, sp, txm, p, a) && !(meta & AM_META_BAD);
+      };
 #pragma unroll
       for (uint32_t k = 0; k < ROW_OPS / RG; ++k) {
         const uint64_t p = m.off0 + sl + RG * k;
         bool in = false;
         if (ok && p < m.off1) {
-          uint32_t sp = u.allmask;
-          uint64_t tx = 0;
-          if (GENERAL && L.snap_pres) sp = L.snap_pres[p];
-          if (GENERAL && u.has_txid) tx = L.op_txid[p];
           if (PACKED) {
-            int32_t sd[DMAX];
+            uint32_t x[DMAX];
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) sd[d] = d < (int)nd ? L.snap_delta[(uint64_t)d * stride + p] : 0;
-            in = eval_at<DMAX, GENERAL, true>(L, nd, u, p, stride, L.ct_meta[p], sd, nullptr, 0, sp, tx, a, esc);
+            for (int d = 0; d < DMAX; ++d) x[d] = d < (int)nd ? L.pk_vc[(uint64_t)d * stride + p] : 0u;
+            const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
+            if (x[0] == AM_PK_ESC) esc = true;
+            else in = pk_eval<DMAX, GENERAL>(pk, u, x, txm, p, ap);
           } else {
-            uint64_t svf[DMAX];
-#pragma unroll
-            for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-            in = eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, L.commit_time[p], nullptr, svf, L.op_meta[p], sp, tx, a, esc);
+            in = eval_full(p);
           }
         }
         incl |= ((__ballot(in) >> (row * RG)) & 0xFFFFull) << (RG * k);
@@ -743,17 +741,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
 #pragma unroll
         for (uint32_t k = 0; k < ROW_OPS / RG; ++k) {
           const uint64_t p = m.off0 + sl + RG * k;
-          bool in = false;
-          if (ok && p < m.off1 && (L.ct_meta[p] & AM_CT_ESC)) {
-            uint64_t svf[DMAX];
-#pragma unroll
-            for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-            const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
-            const uint64_t tx = (GENERAL && u.has_txid) ? L.op_txid[p] : 0;
-            bool e2 = false;
-            in = eval_at<DMAX, GENERAL, false>(L, nd, u, p, stride, L.commit_time[p], nullptr, svf,
-                                                (uint32_t)(L.ct_meta[p] >> 56), sp, tx, a, e2);
-          }
+          const bool in = ok && p < m.off1 && L.pk_vc[p] == AM_PK_ESC && eval_full(p);
           incl |= ((__ballot(in) >> (row * RG)) & 0xFFFFull) << (RG * k);
         }
       }
@@ -769,6 +757,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
       }
       wave_sync();
       // ---- scalar outputs: row reductions (full EXEC) ----
+      if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
       const uint32_t count = row_sum_u32(a.count), flags = row_or_u32(a.flags), pres = row_or_u32(a.pres);
       const uint64_t min_excl = row_min_u64(a.min_excl);
       uint64_t mx[DMAX];

@@ -1,8 +1,10 @@
-// am_pack.hip -- the packed streaming view of a device op log (am_op_log.ct_meta,
-// .snap_delta).  The scan kernels are HBM-bound; the ClockSI inclusion test only
-// needs each snapshot entry relative to the op's own commit time, which fits in 32
-// bits for any realistic clock lag/skew (2^31 us = 35 min).  Ops that do not fit are
-// flagged (AM_CT_ESC) and read from the full columns, so results stay bit-exact.
+// am_pack.hip -- the packed streaming view of a device op log (am_op_log.key_tbase, .pk_vc).
+// The scan kernels are HBM-bound and their per-op work is the ClockSI inclusion test, a
+// compare of the op's commit vector against the read clock per DC.  Entries of one key's ops
+// lie within minutes of each other, so relative to a per-key time base they fit in u32: the
+// test and the LastOpCt max run on 32-bit lanes and each op streams 4 B per DC.  Ops that do
+// not fit (or carry AM_META_BAD) are flagged (pk_vc[0] = AM_PK_ESC) and read from the full
+// columns, so results stay bit-exact.
 //
 // The token-group view (am_op_log.rec_* / grp_* / key_ngrp, include/antidote_mat.h)
 // flattens the add-wins-set / MV-register effects of every op into u32 birth / kill records
@@ -10,7 +12,7 @@
 // stream effects like any other column instead of chasing var_off -> var_data:
 //   k_op_key_mark + inclusive max-scan   op -> key
 //   k_rec_count + exclusive scan         per-op record counts -> record offsets (malformed
-//                                        effects: AM_META_BAD in op_meta and ct_meta)
+//                                        effects: AM_META_BAD in op_meta, escaped in pk_vc)
 //   k_rec_key_off                        per-key record ranges
 //   k_grp_build (am_group.hip)           per key: token groups in output order + u32 records
 #include <hipcub/hipcub.hpp>
@@ -22,20 +24,23 @@ using namespace amk;
 
 namespace {
 
-__global__ void k_pack(am_op_log L, uint64_t *ct_meta, int32_t *snap_delta) {
+// one wave per key: the key's base from its first op, then its ops' entries
+__global__ void k_pack(am_op_log L, uint64_t *tbase, uint32_t *pk_vc) {
   const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
-  const uint32_t all = L.n_dc >= 32 ? 0xFFFFFFFFu : ((1u << L.n_dc) - 1u);
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < L.n_ops;
-       q += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t ct = L.commit_time[q];
-    const uint32_t meta = L.op_meta[q];
-    const uint32_t pres = L.snap_pres ? L.snap_pres[q] & all : all;
-    bool esc = false;
-    for (uint32_t d = 0; d < L.n_dc; ++d) {
-      const bool pr = (pres >> d) & 1u;
-      snap_delta[(uint64_t)d * stride + q] = am_pack_delta(ct, pr ? L.snap_vc[(uint64_t)d * stride + q] : 0, pr, esc);
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; k < L.n_keys; k += waves) {
+    const uint64_t o0 = L.key_off[k], o1 = L.key_off[k + 1];
+    uint64_t base = 0;
+    if (o1 > o0) {
+      uint64_t s[AM_MAX_DC];
+      for (uint32_t d = 0; d < L.n_dc; ++d) s[d] = L.snap_vc[(uint64_t)d * stride + o0];
+      base = am_pk_base(L.commit_time[o0], s, L.n_dc, 0xFFFFFFFFu, AM_META_DC(L.op_meta[o0]));
     }
-    ct_meta[q] = am_pack_ct_meta(ct, meta, esc);
+    if (lane == 0) tbase[k] = base;
+    for (uint64_t p = o0 + lane; p < o1; p += WAVE)
+      am_pk_write(pk_vc, stride, p, L.n_dc, base, L.commit_time[p], L.op_meta[p],
+                  [&](uint32_t d) { return L.snap_vc[(uint64_t)d * stride + p]; });
   }
 }
 
@@ -58,7 +63,7 @@ __device__ __forceinline__ bool op_effects(const am_op_log &L, uint64_t p, uint3
   return set_effects<AM_MVREG>(L, p, meta, 0, sk);
 }
 
-__global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, uint64_t *ct_meta, uint8_t *op_meta) {
+__global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, uint32_t *pk_vc, uint8_t *op_meta) {
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < L.n_ops; p += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t type = L.key_type[okey[p]];
     const uint32_t meta = L.op_meta[p];
@@ -67,8 +72,8 @@ __global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, ui
       CountSink cs;
       if (op_effects(L, p, type, meta, cs)) {
         c = cs.n;
-      } else {  // Type:update/2 raises on this effect: flagged in both views, no records
-        ct_meta[p] |= (uint64_t)AM_META_BAD << 56;
+      } else {  // Type:update/2 raises on this effect: flagged, escaped, no records
+        if (pk_vc) pk_vc[p] = AM_PK_ESC;
         op_meta[p] = (uint8_t)(meta | AM_META_BAD);
       }
     }
@@ -91,7 +96,7 @@ unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256 < 65536 ? (n + 
 int build_records(am_store *st) {
   am_ctx *c = st->ctx;
   am_op_log &d = st->dev;
-  if (!d.var_off || !d.ct_meta || d.n_ops == 0 || d.n_ops > 0xFFFFFFFFull) return AM_OK;
+  if (!d.var_off || d.n_ops == 0 || d.n_ops > 0xFFFFFFFFull) return AM_OK;
   const uint64_t n = d.n_ops;
   uint32_t *okey = nullptr;
   uint64_t *cnt = nullptr;
@@ -123,7 +128,7 @@ int build_records(am_store *st) {
     hipLaunchKernelGGL(k_op_key_mark, dim3(grid_of(d.n_keys)), dim3(256), 0, c->stream, d.key_off, d.n_keys, okey);
     if (hipcub::DeviceScan::InclusiveScan(tmp, tmp_b, okey, okey, MaxOp(), n, c->stream) != hipSuccess) break;
     hipLaunchKernelGGL(k_rec_count, dim3(grid_of(n)), dim3(256), 0, c->stream, d, okey, cnt,
-                       const_cast<uint64_t *>(d.ct_meta), const_cast<uint8_t *>(d.op_meta));
+                       const_cast<uint32_t *>(d.pk_vc), const_cast<uint8_t *>(d.op_meta));
     if (hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, cnt, cnt, n + 1, c->stream) != hipSuccess) break;
     if (hipMemcpyAsync(&n_rec, cnt + n, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) break;
     if (hipStreamSynchronize(c->stream) != hipSuccess) break;
@@ -173,23 +178,26 @@ int am_store_pack(am_store *st) {
   am_ctx *c = st->ctx;
   am_op_log &d = st->dev;
   const uint64_t stride = d.snap_stride ? d.snap_stride : d.n_ops;
-  if (stride % 4 || !d.commit_time || !d.op_meta || (d.n_ops && !d.snap_vc)) return AM_OK;  // not packable
-  void *ctm = nullptr, *sd = nullptr;
-  int rc = am_dev_alloc(c, stride * 8, &ctm);
+  // the packed view assumes full clocks (snap_pres NULL) and padded columns (16-byte loads);
+  // the token-group view is built either way
+  if (!d.commit_time || !d.op_meta || (d.n_ops && !d.snap_vc)) return AM_OK;
+  if (stride % 4 || d.snap_pres) return build_records(st);
+  void *tb = nullptr, *pk = nullptr;
+  int rc = am_dev_alloc(c, d.n_keys * 8 + 8, &tb);
   if (rc) return rc;
-  st->allocs.push_back(ctm);
-  rc = am_dev_alloc(c, (size_t)d.n_dc * stride * 4, &sd);
+  st->allocs.push_back(tb);
+  rc = am_dev_alloc(c, (size_t)d.n_dc * stride * 4, &pk);
   if (rc) return rc;
-  st->allocs.push_back(sd);
-  AM_HIP(hipMemsetAsync(ctm, 0, stride * 8, c->stream));
-  AM_HIP(hipMemsetAsync(sd, 0, (size_t)d.n_dc * stride * 4, c->stream));
-  if (d.n_ops) {
-    const uint64_t blocks = (d.n_ops + 255) / 256 < 65536 ? (d.n_ops + 255) / 256 : 65536;
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)ctm, (int32_t *)sd);
+  st->allocs.push_back(pk);
+  AM_HIP(hipMemsetAsync(pk, 0, (size_t)d.n_dc * stride * 4, c->stream));
+  AM_HIP(hipMemsetAsync(tb, 0, d.n_keys * 8 + 8, c->stream));
+  if (d.n_ops && d.n_keys) {
+    const uint64_t blocks = (d.n_keys + 3) / 4 < 65536 ? (d.n_keys + 3) / 4 : 65536;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)tb, (uint32_t *)pk);
     AM_HIP(hipGetLastError());
   }
   AM_HIP(hipStreamSynchronize(c->stream));
-  d.ct_meta = (const uint64_t *)ctm;
-  d.snap_delta = (const int32_t *)sd;
+  d.key_tbase = (const uint64_t *)tb;
+  d.pk_vc = (const uint32_t *)pk;
   return build_records(st);
 }

@@ -164,8 +164,11 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
       // current read of the row (row-uniform values)
       uint64_t o0 = 0, o1 = 0, rj = 0, keyj = 0, t = 0;
       Acc<DMAX> a;
+      AccP<DMAX> ap;
+      PkRead<DMAX> pk;
       V v;
       a.reset();
+      ap.reset();
       v.reset();
       // (re)start the row's current read; uniform call (the shuffles need every lane),
       // takes effect in rows with upd set; rows with s == 16 are idle
@@ -191,6 +194,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
           u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[rj]) && L.op_txid;
           u.txid = u.has_txid ? B.txid[rj] : 0;
         }
+        if (PACKED) pk_setup(u, nd, L.key_tbase[keyj], pk);
         if (LDS) {
           if (sl == 0) rs->ctr[0] = 0, rs->ctr[1] = 0, rs->ctr[2] = 0, rs->ctr[3] = 0;
           wave_sync();
@@ -199,18 +203,18 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
       begin(true);
       // one op's streamed columns, loaded one step ahead of their use
       struct ROp {
-        uint64_t w;         // packed: ct_meta; full: commit_time
-        uint32_t meta, sp;  // full: op_meta; snapshot presence
-        int32_t sd[DMAX];   // packed: commit_time - snapshot entry
+        uint64_t w;         // full: commit_time
+        uint32_t meta, sp;  // op_meta (full view, bounded counter); snapshot presence
+        uint32_t x[DMAX];   // packed: X[d] - key_tbase
         uint64_t sv[DMAX];  // full: snapshot entries
         uint64_t tx, p0, p1;
       };
       auto load_op = [&](ROp &q, uint64_t p, bool valid) {
         if (!valid) return;
         if (PACKED) {
-          q.w = L.ct_meta[p];
 #pragma unroll
-          for (int d = 0; d < DMAX; ++d) q.sd[d] = d < (int)nd ? L.snap_delta[(uint64_t)d * stride + p] : 0;
+          for (int d = 0; d < DMAX; ++d) q.x[d] = d < (int)nd ? L.pk_vc[(uint64_t)d * stride + p] : 0u;
+          if (BC) q.meta = L.op_meta[p];
         } else {
           q.meta = L.op_meta[p];
           q.w = L.commit_time[p];
@@ -238,27 +242,26 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         }
         if (act && p < o1) {
           // ---- one op: is_op_in_snapshot/7 + the type's effect ----
-          uint32_t meta;
-          uint64_t ct, sv[DMAX];
-          if (PACKED) {
-            meta = (uint32_t)(cur.w >> 56);
-            if (!(cur.w & AM_CT_ESC)) {
-              ct = cur.w & (AM_CT_ESC - 1);
-#pragma unroll
-              for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? ct - (uint64_t)(int64_t)cur.sd[d] : 0;
-            } else {  // rare: the op does not fit the packed view
+          uint32_t meta = PACKED && !BC ? 0u : cur.meta;
+          const bool txm = GENERAL && u.has_txid && cur.tx == u.txid;
+          bool in;
+          if (PACKED && cur.x[0] != AM_PK_ESC) {
+            in = pk_eval<DMAX, GENERAL>(pk, u, cur.x, txm, p, ap);
+          } else {
+            uint64_t ct, sv[DMAX];
+            if (PACKED) {  // rare: the op does not fit the packed view
+              meta = L.op_meta[p];
               ct = L.commit_time[p];
 #pragma unroll
               for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-            }
-          } else {
-            meta = cur.meta;
-            ct = cur.w;
+            } else {
+              ct = cur.w;
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) sv[d] = cur.sv[d];
+              for (int d = 0; d < DMAX; ++d) sv[d] = cur.sv[d];
+            }
+            in = eval_op<DMAX, GENERAL>(u, meta, ct, sv, cur.sp, txm, p, a);
           }
-          const bool txm = GENERAL && u.has_txid && cur.tx == u.txid;
-          if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, cur.sp, txm, p, a) && !(LDS && (meta & AM_META_BAD))) {
+          if (in && !(LDS && (meta & AM_META_BAD))) {
             if constexpr (TYPE == AM_PN || TYPE == AM_LWW) {
               v.add(cur.p0, TYPE == AM_LWW ? cur.p1 : 0);
             } else if constexpr (BC) {
@@ -280,6 +283,11 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         const bool fin = act && o0 + t >= o1;
         if (__ballot(fin)) {
           // ---- row reductions (full EXEC), then rows that finished a read emit it ----
+          if (PACKED) {  // rows still inside a read keep their partials until they finish
+            Acc<DMAX> af = a;
+            pk_fold(ap, pk.K, u.allmask, af);
+            if (fin) a = af, ap.reset();
+          }
           const uint32_t count = row_sum_u32(a.count);
           const uint32_t flags = row_or_u32(a.flags);
           const uint32_t pres = row_or_u32(a.pres);

@@ -17,8 +17,9 @@
 // 4 readlanes).  The next batch's metadata is prefetched one batch ahead, so the
 // stream does not drain at batch boundaries.
 //
-// Packed view (am_pack.hip): with ct_meta / snap_delta present the tile streams
-// 8 + 4*D + payload bytes per op instead of 9 + 8*D + payload.
+// Packed view (am_pack.hip): the tile streams the op's commit vector as u32 entries relative
+// to the key's time base (4*D + payload bytes per op instead of 9 + 8*D + payload) and the
+// inclusion test runs on u32 (am_wave.h pk_eval); escaped ops are read from the full columns.
 //
 // Per-op semantics: am_wave.h eval_op (is_op_in_snapshot/7, belongs_to_snapshot_op/3).
 // Per-read outputs: materialize/4's {ok, Value, NewLastOp, LastOpCt, IsNewSS, Count}.
@@ -61,12 +62,10 @@ struct Tile {
   uint32_t meta4;           // full view
   uint64_t ct[OPL];
   uint64_t sv[OPL][DMAX];
-  uint64_t ctm[OPL];        // packed view (am_pack.hip): ct | esc << 55 | meta << 56
-  int32_t sd[OPL][DMAX];    //   commit_time - snapshot entry
+  uint32_t x[OPL][DMAX];    // packed view (am_pack.hip): X[d] - key_tbase
   uint32_t sp[OPL];
   uint64_t p0[OPL], p1[OPL], tx[OPL];
 };
-constexpr uint64_t CT_MASK = AM_CT_ESC - 1;
 
 // per-lane buffered outputs of read (batch base + lane)
 template <int DMAX>
@@ -125,13 +124,14 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   // ---- batch metadata (lane i: read rb+i), double-buffered across batches ----
   struct Meta {
     uint64_t key, off0, off1, rb, r;  // rb: first slot of the batch; r: lane's read index
+    uint64_t K;                       // packed view: the key's time base
     int32_t st;
     uint32_t nb, skip;  // skip: the row tier (am_rows.hip) owns this read
   };
   auto load_meta = [&](uint64_t bid, Meta &M) {
     M.rb = bid * WAVE;
     M.nb = bid < n_batches ? (uint32_t)(nsel - M.rb < (uint64_t)WAVE ? nsel - M.rb : (uint64_t)WAVE) : 0u;
-    M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK, M.r = 0, M.skip = 0;
+    M.key = 0, M.off0 = 0, M.off1 = 0, M.st = AM_OK, M.r = 0, M.skip = 0, M.K = 0;
     if (lane < M.nb) {
       const uint64_t r = sbase ? (uint64_t)sbase[M.rb + lane] : M.rb + lane;
       M.r = r;
@@ -143,6 +143,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       } else {
         M.off0 = L.key_off[key];
         M.off1 = L.key_off[key + 1];
+        if (PACKED) M.K = L.key_tbase[key];
         const uint32_t ktype = L.key_type[key];
         const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;
         if (M.off1 > M.off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES)))
@@ -160,8 +161,11 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   };
 
   Acc<DMAX> a;
+  AccP<DMAX> ap;
+  PkRead<DMAX> pk;
   V v;
   a.reset();
+  ap.reset();
   v.reset();
   Tile<DMAX> TA, TB;
   Out<DMAX> o;
@@ -239,19 +243,18 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
     T.meta4 = 0;
 #pragma unroll
     for (int k = 0; k < OPL; ++k) {
-      T.ct[k] = 0, T.ctm[k] = 0, T.p0[k] = 0, T.p1[k] = 0, T.tx[k] = 0, T.sp[k] = u.allmask;
+      T.ct[k] = 0, T.p0[k] = 0, T.p1[k] = 0, T.tx[k] = 0, T.sp[k] = u.allmask;
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) T.sv[k][d] = 0, T.sd[k][d] = 0;
+      for (int d = 0; d < DMAX; ++d) T.sv[k][d] = 0, T.x[k][d] = 0;
     }
     if (g < o1 && PACKED) {
-      ld_u64<OPL>(L.ct_meta + g, T.ctm);
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d < (int)nd) {
-          uint32_t sdv[OPL];
-          ld_u32<OPL>((const uint32_t *)L.snap_delta + (uint64_t)d * stride + g, sdv);
+          uint32_t xv[OPL];
+          ld_u32<OPL>(L.pk_vc + (uint64_t)d * stride + g, xv);
 #pragma unroll
-          for (int k = 0; k < OPL; ++k) T.sd[k][d] = (int32_t)sdv[k];
+          for (int k = 0; k < OPL; ++k) T.x[k][d] = xv[k];
         }
       }
     } else if (g < o1) {
@@ -276,8 +279,11 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       if (GENERAL && L.op_txid && B.txid) ld_u64<OPL>(L.op_txid + g, T.tx);
     }
   };
-  auto setup_read = [&](uint32_t j) {  // per-read uniform inputs (GENERAL only)
-    if (!GENERAL) return;
+  auto setup_read = [&](uint32_t j) {  // per-read uniform inputs
+    if (!GENERAL) {
+      if (PACKED) pk_setup(u, nd, lane_u64(M0.K, j), pk);
+      return;
+    }
     const uint64_t r = lane_u64(M0.r, j);
     if (B.per_read_clock) load_clock(r, n);
     u.base_ignore = !B.base_ignore || B.base_ignore[r];
@@ -287,6 +293,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
     u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
     u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+    if (PACKED) pk_setup(u, nd, lane_u64(M0.K, j), pk);
   };
   auto process = [&](const Tile<DMAX> &T, uint32_t j, uint64_t t) {
     const uint64_t o0 = lane_u64(M0.off0, j), o1 = lane_u64(M0.off1, j);
@@ -297,19 +304,14 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       if (p < o0 || p >= o1) continue;
       const bool txm = GENERAL && u.has_txid && T.tx[k] == u.txid;
       if (PACKED) {
-        const uint64_t w = T.ctm[k];
-        uint64_t ct, sv[DMAX];
-        if (w & AM_CT_ESC) {  // rare: the op does not fit the packed view
-          ct = L.commit_time[p];
+        if (T.x[k][0] == AM_PK_ESC) {  // rare: the op does not fit the packed view
+          uint64_t sv[DMAX];
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-        } else {
-          ct = w & CT_MASK;
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) sv[d] = ct - (uint64_t)(int64_t)T.sd[k][d];
+          if (eval_op<DMAX, GENERAL>(u, L.op_meta[p], L.commit_time[p], sv, T.sp[k], txm, p, a)) v.add(T.p0[k], T.p1[k]);
+        } else if (pk_eval<DMAX, GENERAL>(pk, u, T.x[k], txm, p, ap)) {
+          v.add(T.p0[k], T.p1[k]);
         }
-        const uint32_t meta = (uint32_t)(w >> 56);
-        if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, T.sp[k], txm, p, a)) v.add(T.p0[k], T.p1[k]);
       } else if (eval_op<DMAX, GENERAL>(u, (T.meta4 >> (8 * k)) & 0xFFu, T.ct[k], T.sv[k], T.sp[k], txm, p, a)) {
         v.add(T.p0[k], T.p1[k]);
       }
@@ -319,6 +321,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
   auto finalize = [&](uint32_t j) {
     const uint64_t key = lane_u64(M0.key, j);
     const uint64_t o0 = lane_u64(M0.off0, j), o1 = lane_u64(M0.off1, j);
+    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
     const uint32_t count = wave_sum_u32(a.count);
     const uint32_t flags = wave_or_u32(a.flags);
     const uint32_t pres = wave_or_u32(a.pres);
@@ -387,6 +390,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       }
     }
     a.reset();
+    ap.reset();
     v.reset();
   };
   // batch switch: M0's results leave, M1 becomes current, the next batch's metadata

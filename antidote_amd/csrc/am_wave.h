@@ -86,6 +86,21 @@ __device__ __forceinline__ uint32_t wave_or_u32_v(uint32_t v) {
   v |= (uint32_t)__shfl_xor((int)v, 16, WAVE);
   return v | (uint32_t)__shfl_xor((int)v, 32, WAVE);
 }
+__device__ __forceinline__ uint32_t wave_max_u32_v(uint32_t v) {
+#define S_(C) v = max(v, dpp32<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  v = max(v, (uint32_t)__shfl_xor((int)v, 16, WAVE));
+  return max(v, (uint32_t)__shfl_xor((int)v, 32, WAVE));
+}
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, (unsigned)o, WAVE);
+    if (lane >= (uint32_t)o) v += t;
+  }
+  return v;
+}
 __device__ __forceinline__ uint64_t wave_max_u64_v(uint64_t v) {
 #define S_(C) v = umax64(v, dpp64<C>(v));
   AMK_ROW_STEPS(S_)
@@ -241,6 +256,93 @@ __device__ __forceinline__ bool eval_op(const ReadU<DMAX> &u, uint32_t meta, uin
     a.min_excl = pos < a.min_excl ? pos : a.min_excl;
   }
   return incl;
+}
+
+// ---- the same test on the packed view (am_pack.hip): the op's commit vector X as u32
+// entries x[d] = X[d] - K relative to the key's time base K (every DC present).  Per read the
+// clocks become u32 thresholds: X <= S iff S >= K and x <= min(S - K, 2^32 - 2), so the test
+// is one compare per DC and LastOpCt one u32 max per DC.
+template <int DMAX>
+struct PkRead {
+  uint64_t K;
+  uint32_t thr[DMAX];   // MinSnapshotTime
+  uint32_t cthr[DMAX];  // base snapshot_time (belongs_to_snapshot_op)
+  uint32_t miss;        // AM_FLAG_MISSING_DC_LOGGED: a DC of the ops is not in the clock
+  bool never;           // no op passes: a DC missing from the clock or below K
+  bool cnever;          // le(X, base) fails for every op: a base entry below K
+};
+__device__ __forceinline__ uint32_t pk_clamp(uint64_t s, uint64_t K) {
+  return s < K ? 0u : (s - K >= (uint64_t)AM_PK_ESC ? AM_PK_ESC - 1u : (uint32_t)(s - K));
+}
+// nd: DCs of the log; thresholds of pad lanes d >= nd pass (their entries are loaded as 0)
+template <int DMAX>
+__device__ __forceinline__ void pk_setup(const ReadU<DMAX> &u, uint32_t nd, uint64_t K, PkRead<DMAX> &t) {
+  t.K = K;
+  t.miss = (u.allmask & ~u.spres) ? AM_FLAG_MISSING_DC_LOGGED : 0u;
+  t.never = t.miss != 0;
+  t.cnever = false;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    if (d >= (int)nd) {
+      t.thr[d] = AM_PK_ESC, t.cthr[d] = AM_PK_ESC;
+      continue;
+    }
+    t.never |= u.S[d] < K;
+    t.cnever |= u.C0[d] < K;
+    t.thr[d] = pk_clamp(u.S[d], K);
+    t.cthr[d] = pk_clamp(u.C0[d], K);
+  }
+}
+template <int DMAX>
+struct AccP {
+  uint32_t mx[DMAX];
+  uint32_t count, flags;
+  uint64_t min_excl;
+  __device__ void reset() {
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = 0;
+    count = flags = 0;
+    min_excl = NONE;
+  }
+};
+// x[0] == AM_PK_ESC ops are the caller's (full columns)
+template <int DMAX, bool GENERAL>
+__device__ __forceinline__ bool pk_eval(const PkRead<DMAX> &t, const ReadU<DMAX> &u, const uint32_t (&x)[DMAX],
+                                        bool txmatch, uint64_t pos, AccP<DMAX> &a) {
+  if (GENERAL) {
+    bool cand = u.base_ignore | txmatch;
+    if (!cand) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
+      bool le = !t.cnever;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) le &= x[d] <= t.cthr[d];
+      cand = !le;
+    }
+    if (!cand) return false;
+  }
+  a.flags |= t.miss;
+  bool incl = !t.never;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) incl &= x[d] <= t.thr[d];
+  if (incl) {
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) a.mx[d] = max(a.mx[d], x[d]);
+    a.count += 1;
+  } else {
+    a.min_excl = pos < a.min_excl ? pos : a.min_excl;
+  }
+  return incl;
+}
+// folds a lane's packed partials into its full-width accumulator (every DC present)
+template <int DMAX>
+__device__ __forceinline__ void pk_fold(const AccP<DMAX> &p, uint64_t K, uint32_t allmask, Acc<DMAX> &a) {
+  if (p.count) {
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) a.mx[d] = umax64(a.mx[d], K + p.mx[d]);
+    a.pres |= allmask;
+  }
+  a.count += p.count;
+  a.flags |= p.flags;
+  a.min_excl = umin64(a.min_excl, p.min_excl);
 }
 
 // ---- per-type value reductions (apply_operations folds of commutative updates) ----

@@ -61,13 +61,13 @@ CONFIGS = {
 
 def bytes_per_op(type_: int, n_dc: int, packed: bool = True) -> int:
     """Algorithmic HBM bytes read per op by its materialize kernel.
-    Packed view: ct_meta 8 + snapshot deltas 4*D + payload (PN 8, LWW 16, bcounter 16;
-    add-wins-set / MV-register effects come from the record view, counted per record in
-    workload_bytes).  Full view (logs without the packed view): op_meta 1 + commit_time 8 +
+    Packed view: commit vector 4*D (u32 relative to the key's time base) + payload (PN 8,
+    LWW 16, bcounter 16 + op_meta 1; add-wins-set / MV-register effects come from the record
+    view, counted per record in workload_bytes; the key's time base 8 B per read).  Full view (logs without the packed view): op_meta 1 + commit_time 8 +
     snapshot_time 8*D + payload (PN 8, LWW 16; AW var_off 8; MV p0 p1 var_off 24; bcounter
     p0 p1 16), variable-length effect words counted separately, 8 B each."""
     if packed:
-        return 8 + 4 * n_dc + {abi.AM_PN: 8, abi.AM_LWW: 16, abi.AM_AWSET: 0, abi.AM_MVREG: 0, abi.AM_BCOUNTER: 16}[type_]
+        return 4 * n_dc + {abi.AM_PN: 8, abi.AM_LWW: 16, abi.AM_AWSET: 0, abi.AM_MVREG: 0, abi.AM_BCOUNTER: 17}[type_]
     payload = {abi.AM_PN: 8, abi.AM_LWW: 16, abi.AM_AWSET: 8, abi.AM_MVREG: 24, abi.AM_BCOUNTER: 16}[type_]
     return 1 + 8 + 8 * n_dc + payload
 
@@ -116,7 +116,7 @@ def workload_bytes(cfg, dlog, ko, kt, reads, packed):
         m = kt == t
         total += float(lens[m].sum()) * bytes_per_op(t, cfg["n_dc"], packed)
         sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG)) else 0.0
-        total += float(m.sum()) * bytes_per_key(t, cfg["n_dc"], sl)
+        total += float(m.sum()) * (bytes_per_key(t, cfg["n_dc"], sl) + (8 if packed else 0))
     return total
 
 
@@ -304,7 +304,7 @@ def main():
     ms = ctypes.c_float()
     abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
     kern_ms = ms.value / kern_iters
-    packed = bool(dlog.ct_meta)
+    packed = bool(dlog.pk_vc)
     alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
@@ -333,7 +333,7 @@ def main():
                      "kernel": "k_stream" if single else "am_materialize (all tiers: k_stream, k_rows, k_grp_*, k_sets, k_big_*)",
                      "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
-                     "layout": "packed (ct_meta + int32 snapshot deltas); set effects as u32 token-group records"
+                     "layout": "packed (u32 commit vectors relative to a per-key time base); set effects as u32 token-group records"
                      if packed else "full"},
         "cpu_baseline": None,
     }

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 2
+#define AM_ABI_VERSION 3
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -141,13 +141,18 @@ typedef struct am_op_log {
   const uint64_t *p1;          /* [n_ops]                                            */
   const uint64_t *var_off;     /* [n_ops+1] or NULL                                  */
   const uint64_t *var_data;    /* [n_var]                                            */
-  /* Packed streaming view, built on the device by am_store_create / am_synth_store
-   * (NULL in host logs).  ct_meta[p] = commit_time | esc << 55 | op_meta << 56 and
-   * snap_delta[d][p] = commit_time - snap_vc[d][p] as int32; esc = 1 when the op
-   * does not fit (commit_time >= 2^55 or a delta outside int32), and the kernels then
-   * read that op from the full columns above.  Cuts C2 from 49 to 36 B/op. */
-  const uint64_t *ct_meta;     /* [n_ops]                                            */
-  const int32_t *snap_delta;   /* [n_dc][snap_stride]                                */
+  /* Packed streaming view (logs without snap_pres), built on the device by am_store_create /
+   * am_store_update / am_synth_store (NULL in host logs).  The op's commit vector
+   * X = snapshot_time with X[dc] = commit_time (the clock is_op_in_snapshot/7 compares) is
+   * stored relative to a per-key time base:
+   *   pk_vc[d][p] = X[d] - key_tbase[k]   as u32 in [0, 2^32 - 2]
+   * key_tbase[k] = (the smallest entry of the key's first op that lies within 2^31 of its
+   * commit time) - 2^30, saturating at 0.  An op with an entry outside the window, or
+   * carrying AM_META_BAD, has pk_vc[0][p] = AM_PK_ESC and is read from the full columns
+   * above.  The inclusion test then runs on u32 (one compare and one max per DC) and
+   * streams 4 * n_dc bytes per op: 32 B at D = 8 instead of 72 B. */
+  const uint64_t *key_tbase;   /* [n_keys]                                           */
+  const uint32_t *pk_vc;       /* [n_dc][snap_stride]                                */
   /* Token-group view (add-wins set and MV register keys), built on the device with the
    * packed view (am_store_create / am_store_update / am_synth_store).  Every effect is
    * flattened to births and kills of tokens:
@@ -168,7 +173,7 @@ typedef struct am_op_log {
    * twice).  A materialization then streams the ops (inclusion), the records (born / killed
    * bits per group) and only the surviving groups' pairs, with no sort.  Ops carrying
    * AM_META_BAD produce no record; an op whose variable payload is malformed (Type:update/2
-   * would raise) gets AM_META_BAD set in op_meta and ct_meta. */
+   * would raise) gets AM_META_BAD set in op_meta and is escaped in the packed view. */
   uint64_t n_rec;
   const uint64_t *rec_key_off; /* [n_keys+1]                                         */
   const uint32_t *rec_g;       /* [n_rec]                                            */
@@ -181,7 +186,7 @@ typedef struct am_op_log {
 #define AM_REC_GRP(m) ((m) >> 17)
 #define AM_NGRP_NONE 0xFFFFFFFFu
 #define AM_GRP_MAX_REC 2048u
-#define AM_CT_ESC (1ull << 55)
+#define AM_PK_ESC 0xFFFFFFFFu
 
 /*
  * CRDT values (base snapshots in, materialized values out), SoA over reads.

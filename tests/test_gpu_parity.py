@@ -398,6 +398,50 @@ def test_gpu_packed_view_escapes(mat, t):
     _batch_compare(log, reads, mat, 3)
 
 
+@pytest.mark.parametrize("t", GPU_TYPES)
+@pytest.mark.parametrize("n_dc", [1, 3, 8])
+def test_gpu_packed_view_time_base(mat, t, n_dc):
+    """The packed view stores each op's commit vector as u32 offsets from a per-key time base
+    (include/antidote_mat.h key_tbase / pk_vc).  With wall-clock microsecond timestamps the
+    base is non-zero; ops with an entry below the base or 2^32 above it (a snapshot entry
+    far behind, a late commit, a key whose log spans hours), and a first op with a stale
+    entry (left out of the base), must read like the rest.  Read clocks below the base,
+    inside the window and far above it; then incremental reads against the cached base clock
+    (belongs_to_snapshot_op on the packed view)."""
+    rng = random.Random(4242 + 17 * t + n_dc)
+    T0 = 1_700_000_000_000_000
+    keys, reads = [], []
+    for k in range(48):
+        n_ops = rng.choice([1, 5, 40, 130, 300]) if t in SET_TYPES else rng.choice([1, 5, 40, 130, 300, 900])
+        ops = randlog.rand_key_ops(rng, t, n_dc, n_ops, t0=T0 + rng.randint(0, 10**6))
+        mode = k % 6
+        for i, op in enumerate(ops):
+            x = rng.random()
+            if mode == 1 and x < 0.1:    # a snapshot entry far behind
+                op.snap[rng.randrange(n_dc)] = op.commit_time - 2**32 - rng.randint(0, 99)
+            elif mode == 2 and x < 0.1:  # a late commit (clock jump)
+                op.commit_time += 2**33
+            elif mode == 3 and i >= n_ops // 2:  # the log spans more than 2^32 us
+                op.commit_time += 2**32 + 5
+                op.snap = {d: v + 2**32 for d, v in op.snap.items()}
+            elif mode == 4 and i == 0:   # stale entry in the first op
+                op.snap[rng.randrange(n_dc)] = 7
+        keys.append(ops)
+        lo, hi = min(op.commit_time for op in ops), max(op.commit_time for op in ops)
+        clock = {d: rng.choice([lo - 2**31, lo - 5, (lo + hi) // 2, hi, hi + 2**32, 2**63 + 1])
+                 for d in range(n_dc)}
+        reads.append(Read(k, t, clock))
+    log = HostLog(n_dc, keys, key_types=[t] * len(keys))
+    first = _batch_compare(log, reads, mat, n_dc)
+    reads2 = []
+    for i, r in enumerate(reads):
+        res = first.result(i)
+        if res[0] == "ok":
+            clock2 = {d: v + rng.choice([0, 3, 2**31]) for d, v in r.clock.items()}
+            reads2.append(Read(r.key, t, clock2, None, res[3], res[2], res[1]))
+    _batch_compare(log, reads2, mat, n_dc)
+
+
 def _seq_ops(t, effects, n_dc=2):
     return [Op(t, i % n_dc, 10 + 2 * i, {d: 10 + 2 * i - 1 for d in range(n_dc)}, eff) for i, eff in enumerate(effects)]
 
