@@ -39,6 +39,36 @@
 namespace amk_grp {
 using namespace amk;
 
+#ifndef AMK_VOPL8
+#define AMK_VOPL8 0
+#endif
+#ifndef AMK_SKIP
+#define AMK_SKIP 0  // timing experiments only: 1 records, 2 survivors, 4 op tiles
+#endif
+// phase timing of the wave kernel (experiments only, -DAMK_PHASE_PROF): per-wave cycles
+// spent from one phase boundary to the next, summed into amk_phase_cycles
+#ifdef AMK_PHASE_PROF
+__device__ unsigned long long amk_phase_cycles[8];
+#define PH_BEGIN() uint64_t ph_t = clock64()
+#define PH(i)                                   \
+  {                                             \
+    const uint64_t ph_n = clock64();            \
+    ph_acc[i] += ph_n - ph_t;                   \
+    ph_t = ph_n;                                \
+  }
+#define PH_END()                                                               \
+  if ((threadIdx.x & 63) == 0)                                                 \
+    for (int q = 0; q < 6; ++q) atomicAdd(&amk_phase_cycles[q], (unsigned long long)ph_acc[q])
+#define PH_DECL() uint64_t ph_acc[6] = {0, 0, 0, 0, 0, 0}
+#else
+#define PH_BEGIN()
+#define PH(i)
+#define PH_END()
+#define PH_DECL()
+#endif
+#ifndef AMK_WAVE_OCC
+#define AMK_WAVE_OCC 4  // waves per SIMD the wave kernel is compiled for
+#endif
 constexpr int BLOCK = 256;
 constexpr int NW = BLOCK / WAVE;
 constexpr uint32_t RCAP = AM_GRP_MAX_REC;
@@ -107,6 +137,12 @@ template <int N>
 __device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
   if constexpr (N == 1) {
     o[0] = *p;
+  } else if constexpr (N == 8) {
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const u64x2 a = *(const u64x2 *)(p + i);
+      o[i] = a.x, o[i + 1] = a.y;
+    }
   } else {
     const u64x2 a = *(const u64x2 *)p;
     o[0] = a.x, o[1] = a.y;
@@ -118,7 +154,10 @@ __device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
 }
 template <int N>
 __device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
-  if constexpr (N == 4) {
+  if constexpr (N == 8) {
+    const u32x4 a = *(const u32x4 *)p, b = *(const u32x4 *)(p + 4);
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = b.x, o[5] = b.y, o[6] = b.z, o[7] = b.w;
+  } else if constexpr (N == 4) {
     const u32x4 a = *(const u32x4 *)p;
     o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w;
   } else if constexpr (N == 2) {
@@ -143,6 +182,8 @@ __device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, c
   uint64_t tx[OPL] = {};
   if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
   if (PACKED) {
+    // branch-free: x - thr saturates to 0 iff x <= thr, so one OR per op tests every DC;
+    // LastOpCt takes the included ops' entries through max chains
     uint32_t x[OPL][DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
@@ -151,16 +192,38 @@ __device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, c
 #pragma unroll
       for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
     }
+    uint32_t ev = 0;  // evaluated: in range, in the packed view, a candidate
 #pragma unroll
     for (int k = 0; k < OPL; ++k) {
       const uint64_t p = g + k;
-      if (p < off0 || p >= off1) continue;
-      if (x[k][0] == AM_PK_ESC) {
-        esc = true;
-        continue;
+      const bool inr = p >= off0 && p < off1;
+      const bool e = x[k][0] == AM_PK_ESC;
+      esc |= inr && e;
+      uint32_t over = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(x[k][d], pk.thr[d]);
+      bool cand = inr && !e;
+      if (GENERAL) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
+        uint32_t cov = 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) cov |= __builtin_elementwise_sub_sat(x[k][d], pk.cthr[d]);
+        const bool le = !pk.cnever && cov == 0;
+        cand = cand && (u.base_ignore || (u.has_txid && tx[k] == u.txid) || !le);
       }
-      if (pk_eval<DMAX, GENERAL>(pk, u, x[k], GENERAL && u.has_txid && tx[k] == u.txid, p, ap)) ib |= 1u << k;
+      ib |= (uint32_t)(cand && !pk.never && over == 0) << k;
+      ev |= (uint32_t)cand << k;
     }
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      uint32_t m = ap.mx[d];
+#pragma unroll
+      for (int k = 0; k < OPL; ++k) m = max(m, ((ib >> k) & 1u) ? x[k][d] : 0u);
+      ap.mx[d] = m;
+    }
+    ap.count += (uint32_t)__popc(ib);
+    const uint32_t ex = ev & ~ib;
+    if (ex) ap.min_excl = umin64(ap.min_excl, g + (uint64_t)__builtin_ctz(ex));
+    if (ev) ap.flags |= pk.miss;
   } else {
     uint64_t ct[OPL], sv[OPL][DMAX];
     uint32_t sp[OPL];
@@ -242,6 +305,14 @@ __device__ __forceinline__ void wave_scalars(const AccP<DMAX> &ap, const Acc<DMA
 __device__ __forceinline__ int64_t new_last_op(const am_op_log &L, uint64_t key, uint64_t off0, uint64_t off1,
                                                uint64_t min_excl) {
   const uint64_t idb = L.key_id_base ? L.key_id_base[key] : 1;
+  if (min_excl != NONE) return (L.op_id ? (int64_t)L.op_id[min_excl] : (int64_t)(idb + (min_excl - off0))) - 1;
+  if (off1 == off0) return 0;
+  return L.op_id ? (int64_t)L.op_id[off1 - 1] : (int64_t)(idb + (off1 - off0) - 1);
+}
+
+// the same from the key's op-id base (key_id_base[key], or 1)
+__device__ __forceinline__ int64_t new_last_op_b(const am_op_log &L, uint64_t idb, uint64_t off0, uint64_t off1,
+                                                 uint64_t min_excl) {
   if (min_excl != NONE) return (L.op_id ? (int64_t)L.op_id[min_excl] : (int64_t)(idb + (min_excl - off0))) - 1;
   if (off1 == off0) return 0;
   return L.op_id ? (int64_t)L.op_id[off1 - 1] : (int64_t)(idb + (off1 - off0) - 1);
@@ -465,20 +536,32 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
 // dependent steps (metadata -> ops + records -> survivors' pairs) hide behind the others.
 constexpr uint32_t VG = AM_GRP_MAX_REC;    // groups of a wave-kernel read
 constexpr uint32_t VOPS = 8192;            // ops of a wave-kernel read
-constexpr uint32_t VWORDS = VOPS / 32 + 8;
+constexpr uint32_t VWORDS = VOPS / 32 + 16;
 constexpr int VRPT = 8;                    // records per lane per chunk (512 per wave)
+// per-read metadata of a wave's batch of WB reads, loaded lane-parallel into LDS, so a read
+// starts with no dependent global load (key -> key_off / records / time base / output range)
+constexpr uint32_t WB = 32;
+struct WSlot {
+  uint64_t off0, rk0, ooff, K, idb;
+  uint32_t r, nops, nrec, G, ocap, _pad;
+};
 struct WaveSmem {
   uint32_t born[VG / 32], killed[VG / 32];
   uint32_t incl[VWORDS];
   uint16_t list[VG];  // surviving groups in order
+  WSlot slot[WB];
 };
-template <int DMAX>
-constexpr int vopl() { return DMAX <= 8 ? 4 : DMAX <= 16 ? 2 : 1; }  // 32 VGPRs of u32 entries per tile
+// ops per lane of a wave-kernel tile: the packed view's u32 entries fill 32-64 VGPRs; the
+// full view's u64 columns 2 ops at D >= 8
+template <int DMAX, bool PACKED>
+constexpr int vopl() {
+  return PACKED ? (AMK_VOPL8 && DMAX <= 8 ? 8 : DMAX <= 8 ? 4 : DMAX <= 16 ? 2 : 1) : (DMAX < 8 ? 4 : DMAX <= 16 ? 2 : 1);
+}
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
-__global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
-                                                    am_retry next) {
-  constexpr int OPL = vopl<DMAX>();
+__global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
+                                                                  am_sel S, am_retry next) {
+  constexpr int OPL = vopl<DMAX, PACKED>();
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
   constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -491,141 +574,176 @@ __global__ void __launch_bounds__(BLOCK) k_grp_wave(am_op_log L, am_read_batch B
   const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
   const uint64_t W = (uint64_t)gridDim.x * NW;
   const uint64_t gw = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6);
+  ReadU<DMAX> u;
+  if (!GENERAL) read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
+  PH_DECL();
+  PH_BEGIN();
 
-  for (uint64_t i = gw; i < nsel; i += W) {
-    GMeta m;
-    read_meta(L, B, S.idx ? (uint64_t)uniform_u32(S.idx[sel0 + i]) : i, TYPE, m);
-    m.st = (int32_t)uniform_u32((uint32_t)m.st);
-    m.off0 = uniform_u64(m.off0), m.off1 = uniform_u64(m.off1);
-    m.rk0 = uniform_u64(m.rk0), m.rk1 = uniform_u64(m.rk1), m.G = uniform_u32(m.G);
-    const uint64_t r = m.r;
-    if (m.st != AM_OK) {
-      if (lane == 0) R.status[r] = m.st, R.flags[r] = 0;
-      continue;
+  for (uint64_t b0 = gw; b0 < nsel; b0 += (uint64_t)WB * W) {
+    // ---- lane j < WB: read b0 + j*W -> slot j (errors and hand-offs leave here) ----
+    const uint64_t ii = b0 + (uint64_t)lane * W;
+    bool elig = false, hand = false;
+    uint64_t rr = 0;
+    if (lane < WB && ii < nsel) {
+      GMeta mm;
+      read_meta(L, B, S.idx ? (uint64_t)S.idx[sel0 + ii] : ii, TYPE, mm);
+      rr = mm.r;
+      if (mm.st != AM_OK) {
+        R.status[mm.r] = mm.st, R.flags[mm.r] = 0;
+      } else if (mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || has_base_pairs(B, mm.r)) {
+        hand = true;
+      } else {
+        elig = true;
+        WSlot &w = s.slot[lane];
+        const uint64_t o0 = R.value.set_off[mm.r], o1 = R.value.set_off[mm.r + 1];
+        w.off0 = mm.off0, w.rk0 = mm.rk0, w.ooff = o0;
+        w.K = PACKED ? L.key_tbase[mm.key] : 0;
+        w.idb = L.key_id_base ? L.key_id_base[mm.key] : 1;
+        w.r = (uint32_t)mm.r, w.nops = (uint32_t)(mm.off1 - mm.off0), w.nrec = (uint32_t)(mm.rk1 - mm.rk0);
+        w.G = mm.G, w.ocap = o1 - o0 < 0xFFFFFFFFull ? (uint32_t)(o1 - o0) : 0xFFFFFFFFu;
+      }
     }
-    const uint32_t G = m.G;
-    if (G == AM_NGRP_NONE || G > VG || m.off1 - m.off0 > VOPS || has_base_pairs(B, r)) {
-      if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
-      continue;
-    }
-    ReadU<DMAX> u;
-    read_inputs<DMAX, GENERAL, true>(L, nd, B, r, u);
-    const uint64_t t0 = m.off0 & ~(uint64_t)(OPL - 1);
-    const uint32_t sh = (uint32_t)(m.off0 & (OPL - 1));
-    // loaded now, used at the end: the output range (lane 0: also the op-id base)
-    const uint64_t ooff = R.value.set_off[r], oend = R.value.set_off[r + 1];
-
-    // the first record chunk is in flight while the ops are evaluated
-    uint32_t rec[VRPT];
-#pragma unroll
-    for (int j = 0; j < VRPT; ++j) {
-      const uint64_t q = m.rk0 + (uint64_t)j * WAVE + lane;
-      rec[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
-    }
-    for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
-
-    // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
-    PkRead<DMAX> pk;
-    if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[m.key]), pk);
-    AccP<DMAX> ap;
-    Acc<DMAX> a;
-    ap.reset();
-    a.reset();
-    bool esc = false;  // some op of this lane did not fit the packed view
-    for (uint64_t t = t0; t < m.off1; t += TILE) {
-      const uint64_t g = t + (uint64_t)lane * OPL;
-      const uint32_t ib =
-          g < m.off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, m.off0, m.off1, stride, ap, a, esc) : 0u;
-      uint32_t word = ib << (OPL * (lane % LPW));
-#pragma unroll
-      for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
-      if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
+    const uint64_t hm = __ballot(hand);
+    if (hm) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(next.count, (uint32_t)__popcll(hm));
+      base = uniform_u32(base);
+      if (hand) next.list[base + (uint32_t)__popcll(hm & lt)] = (uint32_t)rr;
     }
     wave_sync();
-    const bool full = !PACKED || __ballot(esc);
-    if (PACKED && full) {  // rare: ops outside the packed view, from the full columns
-      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, lane, WAVE, s.incl, a);
+
+    for (uint64_t em = __ballot(elig); em; em &= em - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(em);
+      const uint64_t off0 = uniform_u64(s.slot[j].off0), rk0 = uniform_u64(s.slot[j].rk0);
+      const uint64_t off1 = off0 + uniform_u32(s.slot[j].nops), rk1 = rk0 + uniform_u32(s.slot[j].nrec);
+      const uint64_t r = uniform_u32(s.slot[j].r);
+      const uint32_t G = uniform_u32(s.slot[j].G);
+      if (GENERAL) read_inputs<DMAX, true, true>(L, nd, B, r, u);
+      const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
+      const uint32_t sh = (uint32_t)(off0 & (OPL - 1));
+
+      // the first record chunk is in flight while the ops are evaluated
+      uint32_t rec[VRPT];
+#pragma unroll
+      for (int jj = 0; jj < VRPT; ++jj) {
+        const uint64_t q = rk0 + (uint64_t)jj * WAVE + lane;
+        rec[jj] = q < rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+      }
+      for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
+
+      PH(0);
+      // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
+      PkRead<DMAX> pk;
+      if (PACKED) pk_setup(u, nd, uniform_u64(s.slot[j].K), pk);
+      AccP<DMAX> ap;
+      Acc<DMAX> a;
+      ap.reset();
+      a.reset();
+      bool esc = false;  // some op of this lane did not fit the packed view
+      for (uint64_t t = t0; !(AMK_SKIP & 4) && t < off1; t += TILE) {
+        const uint64_t g = t + (uint64_t)lane * OPL;
+        const uint32_t ib =
+            g < off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, off0, off1, stride, ap, a, esc) : 0u;
+        uint32_t word = ib << (OPL * (lane % LPW));
+#pragma unroll
+        for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
+        if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
+      }
+      wave_sync();
+      const bool full = !PACKED || __ballot(esc);
+      if (PACKED && full) {  // rare: ops outside the packed view, from the full columns
+        esc_pass<DMAX, GENERAL>(L, nd, u, off0, off1, t0, stride, lane, WAVE, s.incl, a);
+        wave_sync();
+      }
+
+      PH(1);
+      // ---- 2. records of included ops -> newest birth / kill per group (the next chunk's
+      //      loads in flight while one chunk is applied) ----
+      for (uint64_t q0 = rk0; !(AMK_SKIP & 1);) {
+        const uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
+        uint32_t nxt[VRPT];
+#pragma unroll
+        for (int jj = 0; jj < VRPT; ++jj) {
+          const uint64_t q = q1 + (uint64_t)jj * WAVE + lane;
+          nxt[jj] = q < rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int jj = 0; jj < VRPT; ++jj) {
+          const uint32_t x = rec[jj];
+          if (x == 0xFFFFFFFFu) continue;
+          const uint32_t op = AM_REC_OP(x), bit = op + sh;
+          if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
+          atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
+        }
+        if (q1 >= rk1) break;
+#pragma unroll
+        for (int jj = 0; jj < VRPT; ++jj) rec[jj] = nxt[jj];
+        q0 = q1;
+      }
+      wave_sync();
+
+      PH(2);
+      // ---- 3. scalar outputs (VGPR wave reductions) ----
+      uint32_t count, flags, pres;
+      uint64_t min_excl, mxl;
+      wave_scalars<DMAX, PACKED>(ap, a, full, PACKED ? pk.K : 0, u.allmask, nd, lane, count, flags, pres, min_excl,
+                                 mxl);
+      int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+      const bool ign = u.base_ignore && count == 0;
+      const uint32_t opres = ign ? 0u : (pres | u.cpres);
+      uint64_t c0 = 0;  // lane d: LastOpCt entry d
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if ((uint32_t)d == lane) c0 = u.C0[d];
+      const uint64_t myct = (lane < nd && ((opres >> lane) & 1u)) ? umax64(mxl, c0) : 0;
+
+      PH(3);
+      // ---- 4. survivors in group order -> the output CSR.  Lane w owns alive word w (G <=
+      //      2048 = 64 words): a scan of the popcounts places every survivor, the group ids
+      //      are listed in LDS and the pairs gathered 128 at a time, all loads in flight ----
+      uint32_t ns = 0;
+      if (status == AM_OK && !(AMK_SKIP & 2)) {
+        const uint32_t nwd = (G + 31) / 32;
+        const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
+        const uint32_t c = (uint32_t)__popc(aw);
+        const uint32_t inc = wave_incl_scan_u32(c, lane);
+        ns = (uint32_t)__shfl((int)inc, 63, WAVE);
+        uint32_t o = inc - c;
+        for (uint32_t bits = aw; bits; bits &= bits - 1) s.list[o++] = (uint16_t)(lane * 32 + __builtin_ctz(bits));
+        wave_sync();
+        const uint64_t ooff = uniform_u64(s.slot[j].ooff);
+        const uint32_t ocap = uniform_u32(s.slot[j].ocap);
+        const uint32_t nput = ns < ocap ? ns : ocap;
+        for (uint32_t j0 = 0; j0 < nput; j0 += 2 * WAVE) {
+          const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
+          uint64_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+          if (j1 < nput) a1 = L.grp_a[rk0 + s.list[j1]], b1 = L.grp_b[rk0 + s.list[j1]];
+          if (j2 < nput) a2 = L.grp_a[rk0 + s.list[j2]], b2 = L.grp_b[rk0 + s.list[j2]];
+          if (j1 < nput) R.value.set_a[ooff + j1] = a1, R.value.set_b[ooff + j1] = b1;
+          if (j2 < nput) R.value.set_a[ooff + j2] = a2, R.value.set_b[ooff + j2] = b2;
+        }
+        if (ns > ocap) status = AM_ERR_CAPACITY;
+      }
+      PH(4);
+      if (status == AM_OK && lane < nd) R.last_ct[(uint64_t)lane * B.n_reads + r] = myct;
+      if (lane == 0) {
+        R.status[r] = status;
+        R.flags[r] = (uint8_t)(flags & 0xFFu);
+        if (status == AM_OK) {
+          R.new_last_op[r] = new_last_op_b(L, s.slot[j].idb, off0, off1, min_excl);
+          R.last_ct_ignore[r] = ign ? 1 : 0;
+          R.last_ct_pres[r] = opres;
+          R.is_new_ss[r] = count > 0;
+          R.count[r] = count;
+          R.value.set_len[r] = ns;
+        }
+      }
+      PH(5);
       wave_sync();
     }
-
-    // ---- 2. records of included ops -> newest birth / kill per group (the next chunk's
-    //      loads in flight while one chunk is applied) ----
-    for (uint64_t q0 = m.rk0;;) {
-      const uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
-      uint32_t nxt[VRPT];
-#pragma unroll
-      for (int j = 0; j < VRPT; ++j) {
-        const uint64_t q = q1 + (uint64_t)j * WAVE + lane;
-        nxt[j] = q < m.rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int j = 0; j < VRPT; ++j) {
-        const uint32_t x = rec[j];
-        if (x == 0xFFFFFFFFu) continue;
-        const uint32_t op = AM_REC_OP(x), bit = op + sh;
-        if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
-        atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
-      }
-      if (q1 >= m.rk1) break;
-#pragma unroll
-      for (int j = 0; j < VRPT; ++j) rec[j] = nxt[j];
-      q0 = q1;
-    }
-    wave_sync();
-
-    // ---- 3. scalar outputs (VGPR wave reductions) ----
-    uint32_t count, flags, pres;
-    uint64_t min_excl, mxl;
-    wave_scalars<DMAX, PACKED>(ap, a, full, PACKED ? pk.K : 0, u.allmask, nd, lane, count, flags, pres, min_excl, mxl);
-    int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
-    const bool ign = u.base_ignore && count == 0;
-    const uint32_t opres = ign ? 0u : (pres | u.cpres);
-    uint64_t c0 = 0;  // lane d: LastOpCt entry d
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d)
-      if ((uint32_t)d == lane) c0 = u.C0[d];
-    const uint64_t myct = (lane < nd && ((opres >> lane) & 1u)) ? umax64(mxl, c0) : 0;
-
-    // ---- 4. survivors in group order -> the output CSR.  Lane w owns alive word w (G <=
-    //      2048 = 64 words): a scan of the popcounts places every survivor, the group ids are
-    //      listed in LDS and the pairs gathered 64 at a time, all loads of a pass in flight ----
-    uint32_t ns = 0;
-    if (status == AM_OK) {
-      const uint32_t nwd = (G + 31) / 32;
-      const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
-      const uint32_t c = (uint32_t)__popc(aw);
-      const uint32_t inc = wave_incl_scan_u32(c, lane);
-      ns = (uint32_t)__shfl((int)inc, 63, WAVE);
-      uint32_t o = inc - c;
-      for (uint32_t bits = aw; bits; bits &= bits - 1) s.list[o++] = (uint16_t)(lane * 32 + __builtin_ctz(bits));
-      wave_sync();
-      const uint64_t ocap = oend - ooff;
-      const uint32_t nput = (uint64_t)ns < ocap ? ns : (uint32_t)ocap;
-      for (uint32_t j0 = 0; j0 < nput; j0 += 2 * WAVE) {
-        const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
-        uint64_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
-        if (j1 < nput) a1 = L.grp_a[m.rk0 + s.list[j1]], b1 = L.grp_b[m.rk0 + s.list[j1]];
-        if (j2 < nput) a2 = L.grp_a[m.rk0 + s.list[j2]], b2 = L.grp_b[m.rk0 + s.list[j2]];
-        if (j1 < nput) R.value.set_a[ooff + j1] = a1, R.value.set_b[ooff + j1] = b1;
-        if (j2 < nput) R.value.set_a[ooff + j2] = a2, R.value.set_b[ooff + j2] = b2;
-      }
-      if ((uint64_t)ns > ocap) status = AM_ERR_CAPACITY;
-    }
-    if (status == AM_OK && lane < nd) R.last_ct[(uint64_t)lane * B.n_reads + r] = myct;
-    if (lane == 0) {
-      R.status[r] = status;
-      R.flags[r] = (uint8_t)(flags & 0xFFu);
-      if (status == AM_OK) {
-        R.new_last_op[r] = new_last_op(L, m.key, m.off0, m.off1, min_excl);
-        R.last_ct_ignore[r] = ign ? 1 : 0;
-        R.last_ct_pres[r] = opres;
-        R.is_new_ss[r] = count > 0;
-        R.count[r] = count;
-        R.value.set_len[r] = ns;
-      }
-    }
-    wave_sync();
+    wave_sync();  // the slots are rewritten by the next batch
   }
+  PH_END();
 }
 
 // ---------------------------------------------------------------- 16-lane row per short read

@@ -15,3 +15,14 @@ int AM_CAT(am_grp_launch_d, GRP_D)(am_ctx *ctx, const am_op_log *L, const am_rea
   if (type == AM_MVREG) return launch_v<GRP_D, AM_MVREG>(ctx, L, B, R, S, next, tier);
   return AM_ERR_UNSUPPORTED;
 }
+
+#ifdef AMK_PHASE_PROF
+// experiments only: read and clear the wave kernel's phase cycle sums
+extern "C" int am_debug_phase_cycles(uint64_t *out) {
+  unsigned long long h[8] = {0};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(amk_grp::amk_phase_cycles), sizeof(h)) != hipSuccess) return AM_ERR_HIP;
+  for (int i = 0; i < 8; ++i) out[i] = h[i];
+  const unsigned long long z[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(amk_grp::amk_phase_cycles), z, sizeof(z)) == hipSuccess ? AM_OK : AM_ERR_HIP;
+}
+#endif
