@@ -54,8 +54,8 @@ class am_op_log(ctypes.Structure):
         ("op_txid", c_void_p), ("op_id", c_void_p), ("p0", c_void_p), ("p1", c_void_p),
         ("var_off", c_void_p), ("var_data", c_void_p),
         ("key_tbase", c_void_p), ("pk_vc", c_void_p),
-        ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp_a", c_void_p),
-        ("grp_b", c_void_p), ("key_ngrp", c_void_p),
+        ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp", c_void_p),
+        ("key_ngrp", c_void_p),
     ]
 
 

@@ -490,8 +490,9 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
         if (alive) {
           const uint64_t o = ns + woff + (uint32_t)__popcll(bm & lt);
           if (o < ocap) {
-            R.value.set_a[ooff + o] = L.grp_a[m.rk0 + g];
-            R.value.set_b[ooff + o] = L.grp_b[m.rk0 + g];
+            const u64x2 ab = *(const u64x2 *)(L.grp + 2 * (m.rk0 + g));
+            R.value.set_a[ooff + o] = ab.x;
+            R.value.set_b[ooff + o] = ab.y;
           }
         }
         ns += total;
@@ -716,11 +717,11 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
         const uint32_t nput = ns < ocap ? ns : ocap;
         for (uint32_t j0 = 0; j0 < nput; j0 += 2 * WAVE) {
           const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
-          uint64_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
-          if (j1 < nput) a1 = L.grp_a[rk0 + s.list[j1]], b1 = L.grp_b[rk0 + s.list[j1]];
-          if (j2 < nput) a2 = L.grp_a[rk0 + s.list[j2]], b2 = L.grp_b[rk0 + s.list[j2]];
-          if (j1 < nput) R.value.set_a[ooff + j1] = a1, R.value.set_b[ooff + j1] = b1;
-          if (j2 < nput) R.value.set_a[ooff + j2] = a2, R.value.set_b[ooff + j2] = b2;
+          u64x2 p1 = {0, 0}, p2 = {0, 0};
+          if (j1 < nput) p1 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j1]));
+          if (j2 < nput) p2 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j2]));
+          if (j1 < nput) R.value.set_a[ooff + j1] = p1.x, R.value.set_b[ooff + j1] = p1.y;
+          if (j2 < nput) R.value.set_a[ooff + j2] = p2.x, R.value.set_b[ooff + j2] = p2.y;
         }
         if (ns > ocap) status = AM_ERR_CAPACITY;
       }
@@ -894,8 +895,9 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
         if (alive) {
           const uint64_t o = ns + (uint32_t)__popc(rm & ((1u << sl) - 1u));
           if (o < ocap) {
-            R.value.set_a[ooff + o] = L.grp_a[m.rk0 + g];
-            R.value.set_b[ooff + o] = L.grp_b[m.rk0 + g];
+            const u64x2 ab = *(const u64x2 *)(L.grp + 2 * (m.rk0 + g));
+            R.value.set_a[ooff + o] = ab.x;
+            R.value.set_b[ooff + o] = ab.y;
           }
         }
         ns += (uint32_t)__popc(rm);

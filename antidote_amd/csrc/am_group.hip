@@ -105,7 +105,7 @@ __device__ uint32_t raw_groups(BuildSmem &s, uint32_t n) {
 
 template <int TYPE>
 __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t off0, uint64_t off1, uint64_t r0,
-                          uint32_t n, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp_a, uint64_t *grp_b,
+                          uint32_t n, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
                           uint32_t *ngrp) {
   const uint32_t tid = threadIdx.x;
   // 1. the key's births / kills into LDS (record order = op order, effect order within an op)
@@ -165,8 +165,8 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
   for (uint32_t j = tid; j < G; j += BLOCK) {
     const uint32_t rg = (uint32_t)s.kp[j];
     s.fin[rg] = j;
-    grp_a[r0 + j] = s.ka[j];  // AW elem; MV value (~0: no birth)
-    grp_b[r0 + j] = TYPE == AM_AWSET ? s.tok[s.rep[rg]] : s.kb[j];
+    grp[2 * (r0 + j)] = s.ka[j];  // AW elem; MV value (~0: no birth)
+    grp[2 * (r0 + j) + 1] = TYPE == AM_AWSET ? s.tok[s.rep[rg]] : s.kb[j];
   }
   __syncthreads();
   // records; a kill is EFFECTIVE only after its group's birth (a kill in the birth's own op
@@ -183,8 +183,8 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp_a,
-                                                     uint64_t *grp_b, uint32_t *ngrp) {
+__global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
+                                                     uint32_t *ngrp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   BuildSmem &s = *reinterpret_cast<BuildSmem *>(smem_raw);
   for (uint64_t k = blockIdx.x; k < L.n_keys; k += gridDim.x) {
@@ -198,15 +198,15 @@ __global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t
       if (threadIdx.x == 0) ngrp[k] = AM_NGRP_NONE;
       continue;
     }
-    if (type == AM_AWSET) build_key<AM_AWSET>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp_a, grp_b, ngrp);
-    else build_key<AM_MVREG>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp_a, grp_b, ngrp);
+    if (type == AM_AWSET) build_key<AM_AWSET>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp, ngrp);
+    else build_key<AM_MVREG>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp, ngrp);
   }
 }
 
 }  // namespace
 
 bool am_group_applies(const am_op_log *L, const am_read_result *R, uint32_t type) {
-  return (type == AM_AWSET || type == AM_MVREG) && L->rec_key_off && L->rec_g && L->grp_a && L->grp_b && L->key_ngrp &&
+  return (type == AM_AWSET || type == AM_MVREG) && L->rec_key_off && L->rec_g && L->grp && L->key_ngrp &&
          L->op_meta && R->value.set_off && R->value.set_len && R->value.set_a && R->value.set_b;
 }
 
@@ -222,8 +222,8 @@ int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_
   return am_grp_launch_d32(ctx, L, B, R, S, type, next, tier);
 }
 
-int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp_a,
-                          uint64_t *grp_b, uint32_t *key_ngrp) {
+int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
+                          uint32_t *key_ngrp) {
   if (L->n_keys == 0) return AM_OK;
   constexpr size_t smem = sizeof(BuildSmem);
   static bool attr = false;
@@ -232,7 +232,7 @@ int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt,
     attr = true;
   }
   const uint64_t blocks = L->n_keys < (uint64_t)ctx->n_cu * 8 ? L->n_keys : (uint64_t)ctx->n_cu * 8;
-  hipLaunchKernelGGL(k_grp_build, dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, rcnt, rec_g, grp_a, grp_b,
+  hipLaunchKernelGGL(k_grp_build, dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, rcnt, rec_g, grp,
                      key_ngrp);
   AM_HIP(hipGetLastError());
   return AM_OK;

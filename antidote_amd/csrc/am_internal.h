@@ -89,8 +89,8 @@ bool am_group_applies(const am_op_log *L, const am_read_result *R, uint32_t type
 int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                     uint32_t type, am_retry next, int tier);
 // the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
-int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp_a,
-                          uint64_t *grp_b, uint32_t *key_ngrp);
+int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
+                          uint32_t *key_ngrp);
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
 
 // Short-read tier (am_rows.hip): reads with at most short_max ops (and error reads) are

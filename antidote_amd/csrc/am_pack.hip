@@ -140,19 +140,18 @@ int build_records(am_store *st) {
     return AM_ERR_HIP;
   }
   rc = AM_OK;
-  void *rko = nullptr, *rg = nullptr, *ga = nullptr, *gb = nullptr, *ng = nullptr;
+  void *rko = nullptr, *rg = nullptr, *gp = nullptr, *ng = nullptr;
   rc = am_dev_alloc(c, (d.n_keys + 1) * 8, &rko);
   if (!rc) st->allocs.push_back(rko), rc = am_dev_alloc(c, (n_rec + 4) * 4, &rg);
-  if (!rc) st->allocs.push_back(rg), rc = am_dev_alloc(c, (n_rec + 4) * 8, &ga);
-  if (!rc) st->allocs.push_back(ga), rc = am_dev_alloc(c, (n_rec + 4) * 8, &gb);
-  if (!rc) st->allocs.push_back(gb), rc = am_dev_alloc(c, (d.n_keys + 1) * 4, &ng);
+  if (!rc) st->allocs.push_back(rg), rc = am_dev_alloc(c, (n_rec + 4) * 16, &gp);
+  if (!rc) st->allocs.push_back(gp), rc = am_dev_alloc(c, (d.n_keys + 1) * 4, &ng);
   if (!rc) st->allocs.push_back(ng);
   if (!rc) {
     hipLaunchKernelGGL(k_rec_key_off, dim3(grid_of(d.n_keys + 1)), dim3(256), 0, c->stream, d.key_off, d.n_keys, cnt,
                        (uint64_t *)rko);
     am_op_log v = d;
     v.rec_key_off = (const uint64_t *)rko;
-    rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)ga, (uint64_t *)gb, (uint32_t *)ng);
+    rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng);
     if (!rc && (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)) {
       am_set_error("token-group view: build pass failed");
       rc = AM_ERR_HIP;
@@ -163,8 +162,7 @@ int build_records(am_store *st) {
   d.n_rec = n_rec;
   d.rec_key_off = (const uint64_t *)rko;
   d.rec_g = (const uint32_t *)rg;
-  d.grp_a = (const uint64_t *)ga;
-  d.grp_b = (const uint64_t *)gb;
+  d.grp = (const uint64_t *)gp;
   d.key_ngrp = (const uint32_t *)ng;
   return AM_OK;
 }

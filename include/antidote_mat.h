@@ -166,7 +166,7 @@ typedef struct am_op_log {
    * [rec_key_off[k], rec_key_off[k+1]):
    *   rec_g = op index within the key (bits 0-15) | kill << 16 | group << 17, or 0xFFFFFFFF
    *           for a kill slot that is not effective
-   * and group g of key k is (grp_a, grp_b)[rec_key_off[k] + g] (AW (elem, token), MV
+   * and group g of key k is the pair grp[2 (rec_key_off[k] + g) + {0, 1}] (AW (elem, token), MV
    * (Value, Token); MV groups without a birth (~0, token)).  key_ngrp[k] = number of groups,
    * or AM_NGRP_NONE when the key is materialized from var_data instead (more than
    * AM_GRP_MAX_REC records or 2^16 ops, or a log outside the closed form: a token born
@@ -177,8 +177,7 @@ typedef struct am_op_log {
   uint64_t n_rec;
   const uint64_t *rec_key_off; /* [n_keys+1]                                         */
   const uint32_t *rec_g;       /* [n_rec]                                            */
-  const uint64_t *grp_a;       /* [n_rec]                                            */
-  const uint64_t *grp_b;       /* [n_rec]                                            */
+  const uint64_t *grp;         /* [n_rec][2], 16-byte aligned: one load per survivor */
   const uint32_t *key_ngrp;    /* [n_keys]                                           */
 } am_op_log;
 #define AM_REC_KILL (1u << 16)
