@@ -181,7 +181,7 @@ def load_traffic(config: str, workload: str):
             d = json.load(f)
         e = d.get(config, d)
         if e.get("workload") == workload:
-            return e.get("bytes_per_launch")
+            return e.get("calibrated_bytes_per_launch", e.get("bytes_per_launch"))
     except Exception:
         pass
     return None

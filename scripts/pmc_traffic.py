@@ -10,28 +10,42 @@ import sys
 
 
 def per_kernel(path, counter, match):
-    vals = []
+    """counter value per dispatch of every kernel whose name contains `match`, by name"""
+    vals = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter and match in r["Kernel_Name"]:
-            vals.append(float(r["Counter_Value"]))
+            vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return vals
 
 
+def avg_sum(vals):
+    """one materialize launch = one dispatch of each matched kernel: sum of per-kernel means"""
+    return sum(sum(v) / len(v) for v in vals.values())
+
+
 def main():
-    fetch_csv, write_csv, workload, out = sys.argv[1:5]
-    match = sys.argv[5] if len(sys.argv) > 5 else "k_stream"
+    fetch_csv, write_csv, config, workload, out = sys.argv[1:6]
+    match = sys.argv[6] if len(sys.argv) > 6 else "k_grp_wave"
     f = per_kernel(fetch_csv, "FETCH_SIZE", match)
     w = per_kernel(write_csv, "WRITE_SIZE", match)
     if not f or not w:
         raise SystemExit(f"no {match} dispatches found")
-    fetch = sum(f) / len(f) * 1024 * 2
-    write = sum(w) / len(w) * 1024
-    d = {"workload": workload, "kernel": match, "dispatches": [len(f), len(w)],
+    fetch = avg_sum(f) * 1024 * 2
+    write = avg_sum(w) * 1024
+    d = {"workload": workload, "kernel": match, "dispatches": [sum(len(v) for v in f.values()),
+                                                               sum(len(v) for v in w.values())],
          "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
          "bytes_per_launch": fetch + write,
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 "
                    "(gfx950 half-count on wide streaming reads), KiB -> bytes"}
-    json.dump(d, open(out, "w"), indent=1)
+    try:
+        allc = json.load(open(out))
+        if "workload" in allc:  # the r01 single-config layout
+            allc = {}
+    except Exception:
+        allc = {}
+    allc[config] = d
+    json.dump(allc, open(out, "w"), indent=1)
     print(json.dumps(d))
 
 
