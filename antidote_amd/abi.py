@@ -64,6 +64,7 @@ class am_values(ctypes.Structure):
         ("v0", c_void_p), ("v1", c_void_p), ("vflag", c_void_p),
         ("set_off", c_void_p), ("set_len", c_void_p), ("set_a", c_void_p), ("set_b", c_void_p),
         ("bc_p", c_void_p), ("bc_p_pres", c_void_p), ("bc_d", c_void_p), ("bc_d_pres", c_void_p),
+        ("bc_off", c_void_p),
     ]
 
 
@@ -138,6 +139,16 @@ SIGNATURES = [
     ("am_snapcache_get", c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint32), c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p]),
     ("am_snapcache_gc_threshold", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("am_snapcache_read_gc", c_int, [c_void_p, c_void_p, POINTER(am_op_log), POINTER(am_read_batch), c_void_p,
+                                     POINTER(am_read_result), c_void_p, c_void_p, c_void_p]),
+    ("am_snapcache_get_value", c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, POINTER(c_uint32), c_void_p,
+                                       c_void_p, c_void_p]),
+    ("am_vnode_create", c_int, [c_void_p, c_uint32, c_uint64, POINTER(c_void_p)]),
+    ("am_vnode_destroy", c_int, [c_void_p]),
+    ("am_vnode_insert_host", c_int, [c_void_p, POINTER(am_op_log)]),
+    ("am_vnode_read_host", c_int, [c_void_p, POINTER(am_read_batch), c_void_p, POINTER(am_read_result)]),
+    ("am_vnode_parts", c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    ("am_vnode_key_info", c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
     ("am_store_update", c_int, [c_void_p, c_void_p, POINTER(am_op_log), c_void_p, c_void_p, c_void_p, c_void_p,
                                 POINTER(c_void_p)]),
     ("am_synth_store", c_int, [c_void_p, POINTER(am_synth_params), POINTER(c_void_p)]),

@@ -116,15 +116,8 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
     if (TYPE == AM_BCOUNTER) {  // slots start from the base snapshot's orddicts
       const uint32_t nd = L.n_dc, np = nd * nd;
       for (uint32_t i = 0; i < SL.ns; ++i) {
-        int64_t bv = 0;
         uint32_t bp = 0;
-        if (i < np) {
-          if (B.base.bc_p) bv = B.base.bc_p[r * np + i];
-          if (B.base.bc_p_pres) bp = B.base.bc_p_pres[r * np + i];
-        } else {
-          if (B.base.bc_d) bv = B.base.bc_d[r * nd + (i - np)];
-          if (B.base.bc_d_pres) bp = B.base.bc_d_pres[r * nd + (i - np)];
-        }
+        const int64_t bv = bc_base(B, r, np, nd, i, bp);
         const uint64_t q = (uint64_t)b * SL.ns + i;
         SL.lo[q] = (uint64_t)bv;
         SL.hi[q] = bv < 0 ? -1 : 0;

@@ -25,7 +25,8 @@ struct Arena {
 // Stages a host batch into one device arena, runs `run` on the device batch/result and
 // copies the result columns back.
 static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr,
-                    const std::function<int(const am_read_batch *, am_read_result *)> &run) {
+                    const std::function<int(const am_read_batch *, am_read_result *, const void *)> &run,
+                    const void *extra_host = nullptr, size_t extra_bytes = 0) {
   if (!c || !st || !hb || !hr || !hb->key || !hb->type || !hb->read_vc || !hb->read_pres) return AM_ERR_INVALID;
   const uint64_t n = hb->n_reads;
   if (n == 0) return AM_OK;
@@ -47,6 +48,7 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
   };
   am_read_batch db = *hb;
   am_read_result dr = *hr;
+  db.base.bc_off = nullptr;  // a device-side layout (snapshot-cache bases); host bases use rows
   std::vector<In> ins;
   std::vector<Out> outs;
   auto in = [&](const void *h, size_t bytes, const void **slot) {
@@ -77,6 +79,8 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
   in(hb->base.bc_d, n * nd * 8, (const void **)&db.base.bc_d);
   in(hb->base.bc_d_pres, n * nd, (const void **)&db.base.bc_d_pres);
   in(hr->value.set_off, (n + 1) * 8, (const void **)&dr.value.set_off);
+  const void *extra_dev = nullptr;
+  in(extra_host, extra_bytes, &extra_dev);
 
   out(hr->status, n * 4, (void **)&dr.status);
   out(hr->new_last_op, n * 8, (void **)&dr.new_last_op);
@@ -126,7 +130,7 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
     *outs[i].dptr = arena + out_off[i];
   }
   if (e == hipSuccess) {
-    rc = run(&db, &dr);
+    rc = run(&db, &dr, extra_dev);
     for (size_t i = 0; i < outs.size() && e == hipSuccess && !rc; ++i)
       e = hipMemcpyAsync(outs[i].h, arena + out_off[i], outs[i].bytes, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -141,7 +145,7 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
 
 extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr) {
   if (!st) return AM_ERR_INVALID;
-  return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr) {
+  return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr, const void *) {
     return am_launch_materialize(c, &st->dev, db, dr);
   });
 }
@@ -149,7 +153,18 @@ extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_
 extern "C" int am_snapcache_read_host(am_ctx *c, am_snapcache *sc, const am_store *st, const am_read_batch *hb,
                                       am_read_result *hr) {
   if (!st || !sc) return AM_ERR_INVALID;
-  return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr) {
+  return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr, const void *) {
     return am_snapcache_read(c, sc, &st->dev, db, dr);
   });
+}
+
+// run_host for internal callers: `run` also gets extra_host staged to the device (am_vnode.hip)
+int am_run_host_batch(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr,
+                      const void *extra_host, size_t extra_bytes,
+                      int (*run)(void *arg, const am_read_batch *db, am_read_result *dr, const void *extra_dev),
+                      void *arg) {
+  return run_host(
+      c, st, hb, hr,
+      [&](const am_read_batch *db, am_read_result *dr, const void *extra_dev) { return run(arg, db, dr, extra_dev); },
+      extra_host, extra_bytes);
 }

@@ -360,12 +360,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                 auto base_of = [&](uint32_t i, uint32_t &bpres) -> int64_t {
                   bpres = 0;
                   if (!GENERAL) return 0;
-                  if (i < np) {
-                    bpres = B.base.bc_p_pres ? B.base.bc_p_pres[rj * np + i] : 0;
-                    return B.base.bc_p ? B.base.bc_p[rj * np + i] : 0;
-                  }
-                  bpres = B.base.bc_d_pres ? B.base.bc_d_pres[rj * nd + (i - np)] : 0;
-                  return B.base.bc_d ? B.base.bc_d[rj * nd + (i - np)] : 0;
+                  return bc_base(B, rj, np, nd, i, bpres);
                 };
                 if (big) {  // pass 1: exact 128-bit sums of the lane's slots, overflow check
                   uint32_t ovf = 0;

@@ -172,15 +172,8 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
     if (tid < 16) s.ctr[tid] = 0;
     if (TYPE == AM_BCOUNTER) {
       for (uint32_t i = tid; i < np + nd; i += BLOCK) {
-        int64_t bv = 0;
         uint32_t bpres = 0;
-        if (i < np) {
-          if (B.base.bc_p) bv = B.base.bc_p[r * np + i];
-          if (B.base.bc_p_pres) bpres = B.base.bc_p_pres[r * np + i];
-        } else {
-          if (B.base.bc_d) bv = B.base.bc_d[r * nd + (i - np)];
-          if (B.base.bc_d_pres) bpres = B.base.bc_d_pres[r * nd + (i - np)];
-        }
+        const int64_t bv = bc_base(B, r, np, nd, i, bpres);
         s.slo[i] = (uint64_t)bv;
         s.shi[i] = bv < 0 ? -1 : 0;
         s.spres[i] = bpres;

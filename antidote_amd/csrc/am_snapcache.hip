@@ -9,17 +9,22 @@
 //   am_materialize materialize/4 on the selected bases (every tier of am_plan.hip)
 //   k_sc_store     the empty-dict insertion of get_from_snapshot_cache, then
 //                  materialize_snapshot/7's write-back (:469-509): only when the key has
-//                  ops, LastOpCt /= ignore and WasUpdated, IsNewest and Count >=
-//                  MIN_OP_STORE_SS; internal_store_ss/4 (:342-364) with its
-//                  NewLastOp - first.last_op_id >= MIN_OP_STORE_SS test;
-//                  vector_orddict:insert_bigger/3 (:127-140); snapshot_insert_gc/3's list
-//                  pruning (:515-563: at SNAPSHOT_THRESHOLD entries keep SNAPSHOT_MIN)
+//                  ops, LastOpCt /= ignore, and (WasUpdated, IsNewest and Count >=
+//                  MIN_OP_STORE_SS) or ShouldGC; internal_store_ss/4 (:342-364) with its
+//                  NewLastOp - first.last_op_id >= MIN_OP_STORE_SS test (or ShouldGC);
+//                  vector_orddict:insert_bigger/3 (:127-140); snapshot_insert_gc/4
+//                  (:515-563): at SNAPSHOT_THRESHOLD entries, or on ShouldGC, the dict
+//                  keeps its newest SNAPSHOT_MIN entries and the key's prune threshold
+//                  (vectorclock:min over them) is emitted for prune_ops (am_store_update)
 //   k_sc_release   frees the key claims
 // Layout: per key a fixed array of CAP entries, newest first (clock [n_dc] + presence,
-// last_op_id, value).  Scalar-valued types (PN counter, LWW register).  The op-cache
-// pruning that snapshot_insert_gc also does (prune_ops) is not applied: pruned ops are
-// already inside every retained snapshot, so no read's result depends on it (SURVEY.md
-// 8(f) rank 1 is the device op-cache GC).
+// last_op_id, value).  Scalar values (PN counter, LWW register) live in the entry; set
+// values (add-wins set / MV register pairs) and bounded-counter slots live in a value pool
+// (pool_a / pool_b / pool_p words, bump-allocated, compacted on the host side when a batch
+// could overflow it) that the next read's base points into (base.set_off/set_len,
+// base.bc_off), so a cached base is never copied.
+#include <hipcub/hipcub.hpp>
+
 #include "am_wave.h"
 
 using namespace amk;
@@ -36,6 +41,12 @@ struct am_snapcache {
   int64_t *v0 = nullptr;       // [n_keys][CAP]
   uint64_t *v1 = nullptr;      // [n_keys][CAP]
   uint8_t *vflag = nullptr;    // [n_keys][CAP]
+  uint64_t *poff = nullptr;    // [n_keys][CAP] value words in the pool
+  uint32_t *plen = nullptr;    // [n_keys][CAP]
+  uint64_t *pool_a = nullptr, *pool_b = nullptr;  // set pairs (a, b); bcounter slot values in a
+  uint8_t *pool_p = nullptr;                      // bcounter slot presence
+  uint64_t pool_cap = 0;                          // words
+  uint64_t *ctr = nullptr;     // device [0] pool words used
   std::vector<void *> allocs;
 };
 
@@ -58,18 +69,31 @@ struct ScView {  // kernel-side copy of the cache pointers
   int64_t *last_op, *v0;
   uint64_t *v1;
   uint8_t *vflag;
+  uint64_t *poff;
+  uint32_t *plen;
+  uint64_t *pool_a, *pool_b;
+  uint8_t *pool_p;
+  uint64_t pool_cap;
+  uint64_t *ctr;
 };
 // selected bases (scratch, columns of the batch handed to am_materialize)
 struct ScSel {
   uint8_t *code, *newest, *base_ignore, *vflag;
-  uint64_t *base_vc, *v1;
-  uint32_t *base_pres;
+  uint64_t *base_vc, *v1, *set_off, *bc_off;
+  uint32_t *base_pres, *set_len;
   int64_t *base_last_op, *v0;
+};
+// prune thresholds emitted by snapshot_insert_gc (optional)
+struct ScGc {
+  uint8_t *mask;     // [n_keys]
+  uint64_t *thr_vc;  // [n_dc][n_keys]
+  uint32_t *thr_pres;
 };
 
 __device__ __forceinline__ uint64_t clk(const uint64_t *vc, uint32_t pres, uint32_t d) {
   return ((pres >> d) & 1u) ? vc[d] : 0;
 }
+__device__ __forceinline__ uint32_t n_slots(uint32_t nd) { return nd * nd + nd; }
 
 __global__ void k_sc_claim(ScView C, am_read_batch B) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < B.n_reads; r += (uint64_t)gridDim.x * blockDim.x)
@@ -89,12 +113,12 @@ __global__ void k_sc_select(ScView C, am_read_batch B, ScSel S) {
     const uint64_t key = B.key[r];
     const uint32_t t = B.type[r];
     uint8_t code = SEL_NEW_DICT, newest = 1;
-    uint32_t bpres = 0;
+    uint32_t bpres = 0, blen = 0;
     int64_t blast = 0, bv0 = 0;
-    uint64_t bv1 = 0;
-    uint8_t bvf = t == AM_LWW ? 1 : 0, bign = 1;  // new(): 0 / {0, <<>>}
+    uint64_t bv1 = 0, boff = 0;  // pool offset 0: the reserved zero words (new() bounded counter)
+    uint8_t bvf = t == AM_LWW ? 1 : 0, bign = 1;  // new(): 0 / {0, <<>>} / [] / {[], []}
     uint32_t sel = CAP;
-    if (key >= C.n_keys || (t != AM_PN && t != AM_LWW)) {
+    if (key >= C.n_keys || t < AM_PN || t > AM_BCOUNTER) {
       code = SEL_BAD;
     } else if (C.owner[key] != (uint32_t)r) {
       code = SEL_DUP;
@@ -126,6 +150,8 @@ __global__ void k_sc_select(ScView C, am_read_batch B, ScSel S) {
         bv0 = C.v0[slot];
         bv1 = C.v1[slot];
         bvf = C.vflag[slot];
+        boff = C.poff[slot];
+        blen = C.plen[slot];
       }
     }
     if (bign)
@@ -138,16 +164,28 @@ __global__ void k_sc_select(ScView C, am_read_batch B, ScSel S) {
     S.v0[r] = bv0;
     S.v1[r] = bv1;
     S.vflag[r] = bvf;
+    S.set_off[r] = boff;
+    S.set_len[r] = t == AM_BCOUNTER ? 0u : blen;
+    S.bc_off[r] = t == AM_BCOUNTER && blen ? boff : 0;
   }
 }
 
-__global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_result R, ScSel S) {
+// value words of read r's result (sets: pairs; bounded counter: every slot), or 0 when the
+// result columns for its type are absent (not cached then)
+__device__ __forceinline__ uint32_t value_words(const am_read_result &R, uint64_t r, uint32_t t, uint32_t nd) {
+  if (t == AM_AWSET || t == AM_MVREG) return (R.value.set_len && R.value.set_a && R.value.set_b) ? R.value.set_len[r] : 0u;
+  if (t == AM_BCOUNTER) return (R.value.bc_p && R.value.bc_p_pres && R.value.bc_d && R.value.bc_d_pres) ? n_slots(nd) : 0u;
+  return 0;
+}
+
+__global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_result R, ScSel S, const uint8_t *should_gc,
+                           ScGc G) {
   const uint32_t nd = C.n_dc;
   const uint64_t n = B.n_reads;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint8_t code = S.code[r];
     if (code == SEL_BAD) {
-      if (R.status[r] == AM_OK) R.status[r] = AM_ERR_UNSUPPORTED;  // set / bcounter values: not cached here
+      if (R.status[r] == AM_OK) R.status[r] = AM_ERR_INVALID;
       continue;
     }
     if (code == SEL_DUP) {
@@ -160,26 +198,28 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
     }
     const uint64_t key = B.key[r];
     const uint32_t t = B.type[r];
+    const uint64_t s0 = key * CAP;
     uint32_t ne = C.cnt[key];
     if (code == SEL_NEW_DICT) {  // store_snapshot(TxId, Key, Empty, vectorclock:new(), false)
-      const uint64_t s0 = key * CAP;
       C.pres[s0] = 0;
       for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = 0;
       C.last_op[s0] = 0;
       C.v0[s0] = 0;
       C.v1[s0] = 0;
       C.vflag[s0] = t == AM_LWW ? 1 : 0;
+      C.poff[s0] = 0;
+      C.plen[s0] = 0;
       ne = 1;
       C.cnt[key] = 1;
     }
     // materialize_snapshot/7: number_of_ops == 0 returns the base; errors and
     // CommitTime == ignore return without caching
     if (R.status[r] != AM_OK || L.key_off[key + 1] == L.key_off[key] || R.last_ct_ignore[r]) continue;
-    if (!(R.is_new_ss[r] && S.newest[r] && R.count[r] >= MIN_OP_STORE_SS)) continue;
+    const bool sg = should_gc && should_gc[r];
+    if (!((R.is_new_ss[r] && S.newest[r] && R.count[r] >= MIN_OP_STORE_SS) || sg)) continue;
     // internal_store_ss/4: ShouldInsert = NewLastOp - first.last_op_id >= MIN_OP_STORE_SS
-    const uint64_t s0 = key * CAP;
     const int64_t nlo = R.new_last_op[r];
-    if (!(nlo - C.last_op[s0] >= (int64_t)MIN_OP_STORE_SS)) continue;
+    if (!(nlo - C.last_op[s0] >= (int64_t)MIN_OP_STORE_SS || sg)) continue;
     // vector_orddict:insert_bigger: prepend iff not vectorclock:le(New, First)
     const uint32_t np = R.last_ct_pres[r];
     const uint32_t fp = C.pres[s0];
@@ -188,42 +228,84 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       const uint64_t x = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
       le = x <= clk(C.vc + s0 * nd, fp, d);
     }
-    if (le) continue;
-    // snapshot_insert_gc: at SNAPSHOT_THRESHOLD entries keep the newest SNAPSHOT_MIN
-    const uint32_t grown = ne + 1;
-    const uint32_t keep = grown >= CAP ? SMIN : grown;
-    for (uint32_t e = keep - 1; e >= 1; --e) {  // shift right by one (newest first)
-      const uint64_t dst = s0 + e, src = s0 + e - 1;
-      for (uint32_t d = 0; d < nd; ++d) C.vc[dst * nd + d] = C.vc[src * nd + d];
-      C.pres[dst] = C.pres[src];
-      C.last_op[dst] = C.last_op[src];
-      C.v0[dst] = C.v0[src];
-      C.v1[dst] = C.v1[src];
-      C.vflag[dst] = C.vflag[src];
+    const bool ins = !le;
+    // snapshot_insert_gc/4: at SNAPSHOT_THRESHOLD entries (or ShouldGC) keep the newest
+    // SNAPSHOT_MIN and prune the ops below their vectorclock:min
+    const uint32_t grown = ne + (ins ? 1u : 0u);
+    const bool gc = grown >= CAP || sg;
+    const uint32_t keep = gc ? (grown < SMIN ? grown : SMIN) : grown;
+    if (ins) {
+      for (uint32_t e = keep - 1; e >= 1; --e) {  // shift right by one (newest first)
+        const uint64_t dst = s0 + e, src = s0 + e - 1;
+        for (uint32_t d = 0; d < nd; ++d) C.vc[dst * nd + d] = C.vc[src * nd + d];
+        C.pres[dst] = C.pres[src];
+        C.last_op[dst] = C.last_op[src];
+        C.v0[dst] = C.v0[src];
+        C.v1[dst] = C.v1[src];
+        C.vflag[dst] = C.vflag[src];
+        C.poff[dst] = C.poff[src];
+        C.plen[dst] = C.plen[src];
+      }
+      for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
+      C.pres[s0] = np;
+      C.last_op[s0] = nlo;
+      C.v0[s0] = (t == AM_PN || t == AM_LWW) ? R.value.v0[r] : 0;
+      C.v1[s0] = t == AM_LWW ? R.value.v1[r] : 0;
+      C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
+      // the value words into the pool (sized on the host before the batch: never overflows)
+      const uint32_t w = value_words(R, r, t, nd);
+      uint64_t off = 0;
+      if (w) {
+        off = atomicAdd((unsigned long long *)C.ctr, (unsigned long long)w);
+        if (off + w > C.pool_cap) off = 0, atomicOr((unsigned long long *)(C.ctr + 1), 1ull);  // host sizing bug
+      }
+      if (w && off) {
+        if (t == AM_BCOUNTER) {
+          const uint32_t q = nd * nd;
+          for (uint32_t i = 0; i < w; ++i) {
+            const bool p = i < q;
+            C.pool_a[off + i] = (uint64_t)(p ? R.value.bc_p[r * q + i] : R.value.bc_d[r * nd + (i - q)]);
+            C.pool_p[off + i] = p ? R.value.bc_p_pres[r * q + i] : R.value.bc_d_pres[r * nd + (i - q)];
+          }
+        } else {
+          const uint64_t so = R.value.set_off[r];
+          for (uint32_t i = 0; i < w; ++i) C.pool_a[off + i] = R.value.set_a[so + i], C.pool_b[off + i] = R.value.set_b[so + i];
+        }
+      }
+      C.poff[s0] = off;
+      C.plen[s0] = off ? w : 0;
     }
-    for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
-    C.pres[s0] = np;
-    C.last_op[s0] = nlo;
-    C.v0[s0] = R.value.v0[r];
-    C.v1[s0] = t == AM_LWW ? R.value.v1[r] : 0;
-    C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
     C.cnt[key] = (uint8_t)keep;
+    if (gc && G.mask) {  // CommitTime = vectorclock:min over the kept entries (dict merge)
+      uint32_t pr = 0;
+      for (uint32_t e = 0; e < keep; ++e) pr |= C.pres[s0 + e];
+      for (uint32_t d = 0; d < nd; ++d) {
+        uint64_t m = ~0ull;
+        for (uint32_t e = 0; e < keep; ++e)
+          if ((C.pres[s0 + e] >> d) & 1u) m = min(m, C.vc[(s0 + e) * nd + d]);
+        G.thr_vc[(uint64_t)d * C.n_keys + key] = ((pr >> d) & 1u) ? m : 0;
+      }
+      G.thr_pres[key] = pr;
+      G.mask[key] = 1;
+    }
   }
 }
 
 ScView view(const am_snapcache *c) {
-  return ScView{c->n_dc, c->n_keys, c->cnt, c->owner, c->vc, c->pres, c->last_op, c->v0, c->v1, c->vflag};
+  return ScView{c->n_dc, c->n_keys, c->cnt, c->owner, c->vc, c->pres, c->last_op, c->v0, c->v1, c->vflag,
+                c->poff, c->plen, c->pool_a, c->pool_b, c->pool_p, c->pool_cap, c->ctr};
 }
 unsigned grid(uint64_t n) { return (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096); }
 
-// snapshot_insert_gc/4's threshold (src/materializer_vnode.erl:522-527): PrunedSnapshots =
-// sublist(Dict, 1, SNAPSHOT_MIN) (newest first), CommitTime = vectorclock:min over them
+// forced snapshot_insert_gc/4 on every cached key (src/materializer_vnode.erl:519-536): the
+// dict keeps its newest SNAPSHOT_MIN entries and CommitTime = vectorclock:min over them
 // (dict merge: a DC present in any of the clocks is kept, with the min over those having it)
 __global__ void k_sc_threshold(ScView C, uint8_t *mask, uint64_t *thr_vc, uint32_t *thr_pres) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < C.n_keys;
        k += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t cnt = C.cnt[k];
     const uint32_t m = (cnt == ABSENT) ? 0 : (cnt < SMIN ? cnt : SMIN);
+    if (cnt != ABSENT) C.cnt[k] = (uint8_t)m;
     uint32_t pres = 0;
     for (uint32_t e = 0; e < m; ++e) pres |= C.pres[k * CAP + e];
     for (uint32_t d = 0; d < C.n_dc; ++d) {
@@ -240,12 +322,96 @@ __global__ void k_sc_threshold(ScView C, uint8_t *mask, uint64_t *thr_vc, uint32
   }
 }
 
+// ---- value pool compaction: the live entries' words moved to a fresh pool ----
+__global__ void k_pool_len(ScView C, uint64_t *len) {
+  const uint64_t ne = C.n_keys * CAP;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = i / CAP, e = i % CAP;
+    const uint32_t cnt = C.cnt[k];
+    len[i] = (cnt != ABSENT && e < cnt && C.poff[i]) ? C.plen[i] : 0;
+  }
+}
+__global__ void k_pool_move(ScView C, const uint64_t *off, uint64_t base, uint64_t *na, uint64_t *nb, uint8_t *np) {
+  const uint64_t ne = C.n_keys * CAP;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = i / CAP, e = i % CAP;
+    const uint32_t cnt = C.cnt[k];
+    if (cnt == ABSENT || e >= cnt || !C.poff[i]) continue;
+    const uint64_t src = C.poff[i], dst = base + off[i];
+    for (uint32_t j = 0; j < C.plen[i]; ++j) na[dst + j] = C.pool_a[src + j], nb[dst + j] = C.pool_b[src + j], np[dst + j] = C.pool_p[src + j];
+    C.poff[i] = dst;
+  }
+}
+
+// words at the pool start kept zero: a new() bounded counter's base (every slot absent)
+uint64_t reserved_words(uint32_t nd) { return (uint64_t)nd * nd + nd + 1; }
+
+// at least `need` free pool words after the used ones: compact, and grow when compaction
+// does not free enough (synchronizes the stream)
+int pool_reserve(am_snapcache *c, uint64_t need) {
+  am_ctx *ctx = c->ctx;
+  uint64_t used = 0;
+  int rc = am_ctx_fetch(ctx, c->ctr, 1, &used);
+  if (rc) return rc;
+  if (used + need <= c->pool_cap) return AM_OK;
+  const uint64_t ne = c->n_keys * CAP;
+  uint64_t *len = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_b = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, len, len, ne + 1, ctx->stream) != hipSuccess) return AM_ERR_HIP;
+  AM_HIP(hipMalloc((void **)&len, (ne + 1) * 8));
+  if (hipMalloc(&tmp, tmp_b + 16) != hipSuccess) {
+    (void)hipFree(len);
+    return AM_ERR_NOMEM;
+  }
+  ScView V = view(c);
+  uint64_t live = 0;
+  bool ok = hipMemsetAsync(len + ne, 0, 8, ctx->stream) == hipSuccess;
+  if (ok && ne) {
+    hipLaunchKernelGGL(k_pool_len, dim3(grid(ne)), dim3(256), 0, ctx->stream, V, len);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  ok = ok && hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, len, len, ne + 1, ctx->stream) == hipSuccess;
+  if (ok) ok = am_ctx_fetch(ctx, len + ne, 1, &live) == AM_OK;
+  const uint64_t res = reserved_words(c->n_dc);
+  uint64_t cap = c->pool_cap;
+  if (cap < 2 * (res + live + need)) cap = 2 * (res + live + need);  // grow: room for this batch twice
+  uint64_t *na = nullptr, *nb = nullptr;
+  uint8_t *np = nullptr;
+  ok = ok && hipMalloc((void **)&na, cap * 8) == hipSuccess && hipMalloc((void **)&nb, cap * 8) == hipSuccess &&
+       hipMalloc((void **)&np, cap) == hipSuccess;
+  ok = ok && hipMemsetAsync(na, 0, res * 8, ctx->stream) == hipSuccess &&
+       hipMemsetAsync(nb, 0, res * 8, ctx->stream) == hipSuccess && hipMemsetAsync(np, 0, res, ctx->stream) == hipSuccess;
+  if (ok && ne) {
+    hipLaunchKernelGGL(k_pool_move, dim3(grid(ne)), dim3(256), 0, ctx->stream, V, len, res, na, nb, np);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  const uint64_t nused = res + live;
+  ok = ok && hipMemcpyAsync(c->ctr, &nused, 8, hipMemcpyHostToDevice, ctx->stream) == hipSuccess &&
+       hipStreamSynchronize(ctx->stream) == hipSuccess;
+  (void)hipFree(len);
+  (void)hipFree(tmp);
+  if (!ok) {
+    if (na) (void)hipFree(na);
+    if (nb) (void)hipFree(nb);
+    if (np) (void)hipFree(np);
+    am_set_error("snapshot cache: value pool compaction failed");
+    return AM_ERR_HIP;
+  }
+  (void)hipFree(c->pool_a);
+  (void)hipFree(c->pool_b);
+  (void)hipFree(c->pool_p);
+  c->pool_a = na, c->pool_b = nb, c->pool_p = np, c->pool_cap = cap;
+  return AM_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcache **out) {
   if (!ctx || !out || n_dc == 0 || n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(ctx->device));
   am_snapcache *c = new am_snapcache();
   c->ctx = ctx;
   c->n_dc = n_dc;
@@ -264,8 +430,26 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
   if (!rc) rc = alloc(ne * 8, (void **)&c->v0);
   if (!rc) rc = alloc(ne * 8, (void **)&c->v1);
   if (!rc) rc = alloc(ne, (void **)&c->vflag);
-  if (!rc && hipMemsetAsync(c->cnt, ABSENT, n_keys + 16, ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
-  if (!rc && hipMemsetAsync(c->owner, 0xFF, (n_keys + 1) * 4, ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
+  if (!rc) rc = alloc(ne * 8, (void **)&c->poff);
+  if (!rc) rc = alloc(ne * 4, (void **)&c->plen);
+  if (!rc) rc = alloc(16, (void **)&c->ctr);
+  const uint64_t res = reserved_words(n_dc);
+  c->pool_cap = 4 * res + 4096;
+  if (!rc && (hipMalloc((void **)&c->pool_a, c->pool_cap * 8) != hipSuccess ||
+              hipMalloc((void **)&c->pool_b, c->pool_cap * 8) != hipSuccess ||
+              hipMalloc((void **)&c->pool_p, c->pool_cap) != hipSuccess))
+    rc = AM_ERR_NOMEM;
+  if (!rc && (hipMemsetAsync(c->cnt, ABSENT, n_keys + 16, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->owner, 0xFF, (n_keys + 1) * 4, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->poff, 0, ne * 8, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->plen, 0, ne * 4, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->pool_a, 0, res * 8, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->pool_b, 0, res * 8, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->pool_p, 0, res, ctx->stream) != hipSuccess ||
+              hipMemcpyAsync(c->ctr, &res, 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->ctr + 1, 0, 8, ctx->stream) != hipSuccess ||
+              hipStreamSynchronize(ctx->stream) != hipSuccess))
+    rc = AM_ERR_HIP;
   if (rc) {
     am_snapcache_destroy(c);
     return rc;
@@ -278,25 +462,54 @@ int am_snapcache_destroy(am_snapcache *c) {
   if (!c) return AM_OK;
   if (c->ctx) (void)hipStreamSynchronize(c->ctx->stream);
   for (void *p : c->allocs) (void)hipFree(p);
+  if (c->pool_a) (void)hipFree(c->pool_a);
+  if (c->pool_b) (void)hipFree(c->pool_b);
+  if (c->pool_p) (void)hipFree(c->pool_p);
   delete c;
   return AM_OK;
 }
 
-int am_snapcache_read(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am_read_batch *B,
+                         const uint8_t *should_gc, am_read_result *R, uint8_t *gc_mask, uint64_t *thr_vc,
+                         uint32_t *thr_pres) {
   if (!ctx || !c || !L || !B || !R || c->ctx != ctx) return AM_ERR_INVALID;
-  if (L->n_dc != c->n_dc || L->n_keys > c->n_keys) {
+  if (L->n_dc != c->n_dc || L->n_keys != c->n_keys) {
     am_set_error("snapshot cache: n_dc / n_keys do not match the log");
     return AM_ERR_INVALID;
   }
-  if (!R->value.v0 || !R->value.v1 || !R->value.vflag) {
-    am_set_error("snapshot cache reads need value.v0/v1/vflag");
+  if ((gc_mask || thr_vc || thr_pres) && !(gc_mask && thr_vc && thr_pres)) {
+    am_set_error("snapshot cache: gc_mask, thr_vc and thr_pres go together");
     return AM_ERR_INVALID;
   }
+  const uint32_t th = B->type_hint;
+  if ((th == 0 || th == AM_PN || th == AM_LWW) && !(R->value.v0 && R->value.v1 && R->value.vflag)) {
+    am_set_error("snapshot cache reads of PN / LWW keys need value.v0/v1/vflag");
+    return AM_ERR_INVALID;
+  }
+  AM_HIP(hipSetDevice(ctx->device));
   const uint64_t n = B->n_reads;
+  if (gc_mask) AM_HIP(hipMemsetAsync(gc_mask, 0, c->n_keys, ctx->stream));
   if (n == 0) return AM_OK;
   const uint32_t nd = c->n_dc;
-  // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres [n] u32 | base_last_op, v0, v1 [n] u64 | base_vc [nd][n]
-  const size_t bytes = n * (4 + 4 + 3 * 8 + (size_t)nd * 8) + 1024;
+  // value pool room for every value this batch could store
+  uint64_t need = 0;
+  if (th == 0 || th == AM_AWSET || th == AM_MVREG) {
+    if (R->value.set_off) {
+      uint64_t so[2] = {0, 0};
+      int rc = am_ctx_fetch(ctx, R->value.set_off, 1, &so[0]);
+      if (!rc) rc = am_ctx_fetch(ctx, R->value.set_off + n, 1, &so[1]);
+      if (rc) return rc;
+      need += so[1] - so[0];
+    }
+  }
+  if ((th == 0 || th == AM_BCOUNTER) && R->value.bc_p) need += n * ((uint64_t)nd * nd + nd);
+  if (need) {
+    int rc = pool_reserve(c, need);
+    if (rc) return rc;
+  }
+  // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres, set_len [n] u32 |
+  // base_last_op, v0, v1, set_off, bc_off [n] u64 | base_vc [nd][n]
+  const size_t bytes = n * (4 + 8 + 5 * 8 + (size_t)nd * 8) + 4096;
   void *scr = nullptr;
   int rc = am_ctx_scratch(ctx, AM_SCR_SNAP, bytes, &scr);
   if (rc) return rc;
@@ -310,8 +523,11 @@ int am_snapcache_read(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am
   S.base_last_op = (int64_t *)take(n * 8);
   S.v0 = (int64_t *)take(n * 8);
   S.v1 = (uint64_t *)take(n * 8);
+  S.set_off = (uint64_t *)take(n * 8);
+  S.bc_off = (uint64_t *)take(n * 8);
   S.base_vc = (uint64_t *)take(n * nd * 8);
   S.base_pres = (uint32_t *)take(n * 4);
+  S.set_len = (uint32_t *)take(n * 4);
   S.code = (uint8_t *)take(n);
   S.newest = (uint8_t *)take(n);
   S.base_ignore = (uint8_t *)take(n);
@@ -319,27 +535,43 @@ int am_snapcache_read(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am
   const ScView V = view(c);
   hipLaunchKernelGGL(k_sc_claim, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B);
   hipLaunchKernelGGL(k_sc_select, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B, S);
-  AM_HIP(hipGetLastError());
-  am_read_batch db = *B;
-  db.base_ignore = S.base_ignore;
-  db.base_vc = S.base_vc;
-  db.base_pres = S.base_pres;
-  db.base_last_op = S.base_last_op;
-  db.base.v0 = S.v0;
-  db.base.v1 = S.v1;
-  db.base.vflag = S.vflag;
-  rc = am_launch_materialize(ctx, L, &db, R);
+  rc = hipGetLastError() == hipSuccess ? AM_OK : AM_ERR_HIP;
   if (rc == AM_OK) {
-    hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S);
-    AM_HIP(hipGetLastError());
+    am_read_batch db = *B;
+    db.base_ignore = S.base_ignore;
+    db.base_vc = S.base_vc;
+    db.base_pres = S.base_pres;
+    db.base_last_op = S.base_last_op;
+    db.base = am_values{};
+    db.base.v0 = S.v0;
+    db.base.v1 = S.v1;
+    db.base.vflag = S.vflag;
+    db.base.set_off = S.set_off;  // cached pairs: offsets into the pool (set_off[r], set_len[r])
+    db.base.set_len = S.set_len;
+    db.base.set_a = c->pool_a;
+    db.base.set_b = c->pool_b;
+    db.base.bc_off = S.bc_off;    // cached bounded counters: slots in the pool
+    db.base.bc_p = (int64_t *)c->pool_a;
+    db.base.bc_p_pres = c->pool_p;
+    db.base.bc_d = (int64_t *)c->pool_a + (uint64_t)nd * nd;
+    db.base.bc_d_pres = c->pool_p + (uint64_t)nd * nd;
+    rc = am_launch_materialize(ctx, L, &db, R);
+    if (rc == AM_OK) {
+      const ScGc G{gc_mask, thr_vc, thr_pres};
+      hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G);
+      if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
+    }
   }
-  hipLaunchKernelGGL(k_sc_release, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B);
+  hipLaunchKernelGGL(k_sc_release, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B);  // every exit path
   AM_HIP(hipGetLastError());
   return rc;
 }
 
-int am_snapcache_gc_threshold(am_ctx *ctx, const am_snapcache *c, uint8_t *mask, uint64_t *thr_vc,
-                              uint32_t *thr_pres) {
+int am_snapcache_read(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
+  return am_snapcache_read_gc(ctx, c, L, B, nullptr, R, nullptr, nullptr, nullptr);
+}
+
+int am_snapcache_gc_threshold(am_ctx *ctx, am_snapcache *c, uint8_t *mask, uint64_t *thr_vc, uint32_t *thr_pres) {
   if (!ctx || !c || !mask || !thr_vc || !thr_pres) return AM_ERR_INVALID;
   AM_HIP(hipSetDevice(ctx->device));
   if (c->n_keys == 0) return AM_OK;
@@ -351,6 +583,7 @@ int am_snapcache_gc_threshold(am_ctx *ctx, const am_snapcache *c, uint8_t *mask,
 int am_snapcache_get(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t *n_entries, uint64_t *vc,
                      uint32_t *pres, int64_t *last_op, int64_t *v0, uint64_t *v1, uint8_t *vflag) {
   if (!ctx || !c || !n_entries || key >= c->n_keys) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(ctx->device));
   uint8_t cnt = 0;
   const uint64_t s0 = key * CAP, nd = c->n_dc;
   AM_HIP(hipMemcpyAsync(&cnt, c->cnt + key, 1, hipMemcpyDeviceToHost, ctx->stream));
@@ -362,6 +595,25 @@ int am_snapcache_get(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t 
   if (vflag) AM_HIP(hipMemcpyAsync(vflag, c->vflag + s0, CAP, hipMemcpyDeviceToHost, ctx->stream));
   AM_HIP(hipStreamSynchronize(ctx->stream));
   *n_entries = cnt == ABSENT ? AM_SNAPCACHE_ABSENT : cnt;
+  return AM_OK;
+}
+
+int am_snapcache_get_value(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t e, uint32_t cap_words,
+                           uint32_t *n_words, uint64_t *a, uint64_t *b, uint8_t *pres) {
+  if (!ctx || !c || !n_words || key >= c->n_keys || e >= CAP) return AM_ERR_INVALID;
+  AM_HIP(hipSetDevice(ctx->device));
+  const uint64_t s = key * CAP + e;
+  uint64_t off = 0;
+  uint32_t len = 0;
+  AM_HIP(hipMemcpyAsync(&off, c->poff + s, 8, hipMemcpyDeviceToHost, ctx->stream));
+  AM_HIP(hipMemcpyAsync(&len, c->plen + s, 4, hipMemcpyDeviceToHost, ctx->stream));
+  AM_HIP(hipStreamSynchronize(ctx->stream));
+  *n_words = len;
+  const uint32_t m = len < cap_words ? len : cap_words;
+  if (m && a) AM_HIP(hipMemcpyAsync(a, c->pool_a + off, (size_t)m * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (m && b) AM_HIP(hipMemcpyAsync(b, c->pool_b + off, (size_t)m * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (m && pres) AM_HIP(hipMemcpyAsync(pres, c->pool_p + off, m, hipMemcpyDeviceToHost, ctx->stream));
+  AM_HIP(hipStreamSynchronize(ctx->stream));
   return AM_OK;
 }
 

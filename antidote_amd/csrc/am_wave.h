@@ -345,6 +345,20 @@ __device__ __forceinline__ void pk_fold(const AccP<DMAX> &p, uint64_t K, uint32_
   a.min_excl = umin64(a.min_excl, p.min_excl);
 }
 
+// base bounded-counter slot i of read r (P slots i < np, then the nd D slots): row r of the
+// [n][np] / [n][nd] arrays, or at base.bc_off[r] (snapshot-cache bases in the value pool)
+__device__ __forceinline__ int64_t bc_base(const am_read_batch &B, uint64_t r, uint32_t np, uint32_t nd, uint32_t i,
+                                           uint32_t &pres) {
+  const bool p = i < np;
+  const uint64_t idx = B.base.bc_off ? B.base.bc_off[r] + (p ? i : i - np) : (p ? r * np + i : r * nd + (i - np));
+  if (p) {
+    pres = B.base.bc_p_pres ? B.base.bc_p_pres[idx] : 0u;
+    return B.base.bc_p ? B.base.bc_p[idx] : 0;
+  }
+  pres = B.base.bc_d_pres ? B.base.bc_d_pres[idx] : 0u;
+  return B.base.bc_d ? B.base.bc_d[idx] : 0;
+}
+
 // ---- per-type value reductions (apply_operations folds of commutative updates) ----
 struct PnVal {  // antidote_crdt_counter_pn: integer sum, exact in 128 bits
   int64_t hi;

@@ -156,6 +156,52 @@ class _DevBuf:
             self.p = ctypes.c_void_p()
 
 
+def _cache_snapshots(mat, sc, n_dc: int, key: int, type_: int):
+    """A snapshot cache's dict for a key: [(clock, last_op_id, value)] newest first (values as
+    HostBatch.value renders them), or None before the key's first read."""
+    import numpy as np
+    nd, cap = n_dc, abi.AM_SNAPSHOT_THRESHOLD
+    n = ctypes.c_uint32()
+    vc = np.zeros(cap * nd, np.uint64)
+    pres = np.zeros(cap, np.uint32)
+    lo = np.zeros(cap, np.int64)
+    v0 = np.zeros(cap, np.int64)
+    v1 = np.zeros(cap, np.uint64)
+    vf = np.zeros(cap, np.uint8)
+    L = mat.L
+    abi.check(L.am_snapcache_get(mat.ctx, sc, key, ctypes.byref(n), vc.ctypes.data, pres.ctypes.data,
+                                 lo.ctypes.data, v0.ctypes.data, v1.ctypes.data, vf.ctypes.data), "am_snapcache_get")
+    if n.value == abi.AM_SNAPCACHE_ABSENT:
+        return None
+    out = []
+    for e in range(n.value):
+        clock = {d: int(vc[e * nd + d]) for d in range(nd) if (int(pres[e]) >> d) & 1}
+        if type_ == abi.AM_PN:
+            val: Any = int(v0[e])
+        elif type_ == abi.AM_LWW:
+            val = (int(v0[e:e + 1].view(np.uint64)[0]), int(v1[e]), bool(vf[e]))
+        else:
+            nw = ctypes.c_uint32()
+            abi.check(L.am_snapcache_get_value(mat.ctx, sc, key, e, 0, ctypes.byref(nw), None, None, None),
+                      "am_snapcache_get_value")
+            m = max(int(nw.value), 1)
+            a, b, p = np.zeros(m, np.uint64), np.zeros(m, np.uint64), np.zeros(m, np.uint8)
+            abi.check(L.am_snapcache_get_value(mat.ctx, sc, key, e, m, ctypes.byref(nw), a.ctypes.data,
+                                               b.ctypes.data, p.ctypes.data), "am_snapcache_get_value")
+            w = int(nw.value)
+            if type_ == abi.AM_BCOUNTER:
+                if w == 0:
+                    val = ({}, {})
+                else:
+                    val = ({(j // nd, j % nd): int(a[j:j + 1].view(np.int64)[0]) for j in range(nd * nd) if p[j]},
+                           {j: int(a[nd * nd + j:nd * nd + j + 1].view(np.int64)[0]) for j in range(nd)
+                            if p[nd * nd + j]})
+            else:
+                val = [(int(a[j]), int(b[j])) for j in range(w)]
+        out.append((clock, int(lo[e]), val))
+    return out
+
+
 class SnapshotCache:
     """A partition's snapshot cache on the device: reads run materializer_vnode:internal_read/7
     (src/materializer_vnode.erl:371-376) -- base from the cache, materialize/4, write-back."""
@@ -166,14 +212,18 @@ class SnapshotCache:
         abi.check(mat.L.am_snapcache_create(mat.ctx, store.n_dc, n_keys, ctypes.byref(self.handle)),
                   "am_snapcache_create")
 
-    def read(self, reads: Sequence[Read]) -> HostBatch:
+    def read(self, reads: Sequence[Read], set_capacity=None) -> HostBatch:
         """internal_read/7 (ShouldGC = false) for reads of distinct keys; read.base_* are ignored.
         Per read: ('ok', Value, ...) or ('error', AM_ERR_COLD_PATH) when the log would be read."""
-        hb = HostBatch(self.store.n_dc, reads)
+        hb = HostBatch(self.store.n_dc, reads, set_capacity)
         b, r = hb.structs()
         abi.check(self.mat.L.am_snapcache_read_host(self.mat.ctx, self.handle, self.store.handle, ctypes.byref(b),
                                                     ctypes.byref(r)), "am_snapcache_read_host")
         return hb
+
+    def snapshots(self, key: int, type_: int):
+        """[(clock, last_op_id, value)] newest first, or None before the key's first read."""
+        return _cache_snapshots(self.mat, self.handle, self.store.n_dc, key, type_)
 
     def entries(self, key: int):
         """[(clock, last_op_id, v0, v1, vflag)] newest first, or None before the key's first read."""
@@ -200,6 +250,76 @@ class SnapshotCache:
     def close(self):
         if self.handle:
             self.mat.L.am_snapcache_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+class Vnode:
+    """One partition's materializer_vnode state on the device (am_vnode): the ops cache and the
+    snapshot cache, driven by op_insert_gc/3 and internal_read/7 with the reference's GC
+    (src/materializer_vnode.erl:371-376, 515-563, 622-647)."""
+
+    def __init__(self, mat: "Materializer", n_dc: int, n_keys: int):
+        self.mat, self.n_dc, self.n_keys = mat, n_dc, n_keys
+        self.handle = ctypes.c_void_p()
+        abi.check(mat.L.am_vnode_create(mat.ctx, n_dc, n_keys, ctypes.byref(self.handle)), "am_vnode_create")
+
+    def insert(self, ops_by_key: Sequence[Sequence[Op]], key_types: Sequence[int]):
+        """op_insert_gc/3 for every op (each key's ops oldest -> newest; op ids are assigned)."""
+        log = HostLog(self.n_dc, ops_by_key, key_types=key_types)
+        s = log.as_struct()
+        abi.check(self.mat.L.am_vnode_insert_host(self.handle, ctypes.byref(s)), "am_vnode_insert_host")
+
+    def read(self, reads: Sequence[Read], should_gc: Optional[Sequence[bool]] = None, set_capacity=None) -> HostBatch:
+        """internal_read/7 per read (read.base_* ignored); ('error', AM_ERR_COLD_PATH) for the log path."""
+        import numpy as np
+        hb = HostBatch(self.n_dc, reads, set_capacity)
+        b, r = hb.structs()
+        sg = np.ascontiguousarray([1 if x else 0 for x in should_gc], np.uint8) if should_gc is not None else None
+        abi.check(self.mat.L.am_vnode_read_host(self.handle, ctypes.byref(b), sg.ctypes.data if sg is not None else None,
+                                                ctypes.byref(r)), "am_vnode_read_host")
+        return hb
+
+    def key_info(self, key: int):
+        """(Length, ListLen, OpCounter) of the key's ops-cache tuple."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        abi.check(self.mat.L.am_vnode_key_info(self.handle, key, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                  "am_vnode_key_info")
+        return int(a.value), int(b.value), int(c.value)
+
+    def _parts(self):
+        st, sc = ctypes.c_void_p(), ctypes.c_void_p()
+        abi.check(self.mat.L.am_vnode_parts(self.handle, ctypes.byref(st), ctypes.byref(sc)), "am_vnode_parts")
+        return st, sc
+
+    def op_ids(self, key: int) -> List[int]:
+        """The op ids in the key's ops cache, oldest first."""
+        import numpy as np
+        st, _ = self._parts()
+        d = abi.am_op_log()  # the vnode's store is borrowed: no Store wrapper (it would destroy it)
+        abi.check(self.mat.L.am_store_log(st, ctypes.byref(d)), "am_store_log")
+        L = self.mat.L
+        ko = np.zeros(2, np.uint64)
+        abi.check(L.am_memcpy_d2h(self.mat.ctx, ko.ctypes.data, d.key_off + key * 8, 16), "am_memcpy_d2h")
+        n = int(ko[1] - ko[0])
+        if n == 0:
+            return []
+        if d.op_id:
+            ids = np.zeros(n, np.uint64)
+            abi.check(L.am_memcpy_d2h(self.mat.ctx, ids.ctypes.data, d.op_id + int(ko[0]) * 8, n * 8), "am_memcpy_d2h")
+            return [int(x) for x in ids]
+        base = np.ones(1, np.uint64)
+        if d.key_id_base:
+            abi.check(L.am_memcpy_d2h(self.mat.ctx, base.ctypes.data, d.key_id_base + key * 8, 8), "am_memcpy_d2h")
+        return [int(base[0]) + i for i in range(n)]
+
+    def snapshots(self, key: int, type_: int):
+        """[(clock, last_op_id, value)] newest first, or None before the key's first read."""
+        _, sc = self._parts()
+        return _cache_snapshots(self.mat, sc, self.n_dc, key, type_)
+
+    def close(self):
+        if self.handle:
+            self.mat.L.am_vnode_destroy(self.handle)
             self.handle = ctypes.c_void_p()
 
 
@@ -261,6 +381,9 @@ class Materializer:
     # ---- snapshot cache (materializer_vnode snapshot_cache-P in HBM) ----
     def snapshot_cache(self, store: Store, n_keys: int) -> "SnapshotCache":
         return SnapshotCache(self, store, n_keys)
+
+    def vnode(self, n_dc: int, n_keys: int) -> Vnode:
+        return Vnode(self, n_dc, n_keys)
 
     def materialize(self, type_: int, txid: Optional[int], min_snapshot_time: Dict[int, int],
                     ops_newest_first: Sequence[Tuple[int, Op]], base_clock: Optional[Dict[int, int]] = None,

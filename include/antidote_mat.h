@@ -213,6 +213,9 @@ typedef struct am_values {
   uint8_t *bc_p_pres;
   int64_t *bc_d;
   uint8_t *bc_d_pres;
+  /* bases only: read r's bcounter slots at bc_p / bc_p_pres + bc_off[r] (P, i < n_dc^2) and
+   * bc_d / bc_d_pres + bc_off[r] (D) instead of rows r * n_dc^2 / r * n_dc; NULL => rows */
+  const uint64_t *bc_off;
 } am_values;
 
 /* One batch of snapshot reads: the materialize/4 inputs per key. */
@@ -283,11 +286,12 @@ int am_materialize_host(am_ctx *ctx, const am_store *st, const am_read_batch *ho
                         am_read_result *host_res);
 
 /* ---- snapshot cache (materializer_vnode snapshot_cache-P) ----
- * Replaces get_from_snapshot_cache/5 + materialize_snapshot/7 + internal_store_ss/4 around
- * materialize/4, i.e. materializer_vnode:internal_read/7 (src/materializer_vnode.erl:371-376,
- * 384-413, 469-509, 342-364) and vector_orddict get_smaller / insert_bigger
- * (src/vector_orddict.erl:75-87, 127-140): per key at most AM_SNAPSHOT_THRESHOLD snapshots,
- * newest first, in HBM.  PN counter and LWW register values. */
+ * Replaces get_from_snapshot_cache/5 + materialize_snapshot/7 + internal_store_ss/4 +
+ * snapshot_insert_gc/4 around materialize/4, i.e. materializer_vnode:internal_read/7
+ * (src/materializer_vnode.erl:371-376, 384-413, 469-509, 342-364, 515-563) and vector_orddict
+ * get_smaller / insert_bigger (src/vector_orddict.erl:75-87, 127-140): per key at most
+ * AM_SNAPSHOT_THRESHOLD snapshots, newest first, in HBM.  Every type's value: PN / LWW in
+ * the entry, set pairs and bounded-counter slots in a device value pool. */
 #define AM_SNAPSHOT_THRESHOLD 10   /* src/materializer_vnode.erl:37 */
 #define AM_SNAPSHOT_MIN 3          /* :39 */
 #define AM_MIN_OP_STORE_SS 5       /* :47 */
@@ -299,10 +303,21 @@ int am_snapcache_destroy(am_snapcache *cache);
  * cache (the batch's base members are ignored), materialize/4 runs on it, and the result is
  * written back under materialize_snapshot/7's policy.  Per read status: AM_ERR_COLD_PATH
  * when no cached snapshot is vectorclock:le the read clock; AM_ERR_INVALID for a key read
- * a second time in the same batch (the first read, by index, owns the key);
- * AM_ERR_UNSUPPORTED for set / bounded-counter reads.  Device pointers, async. */
+ * a second time in the same batch (the first read, by index, owns the key; am_vnode_read
+ * serves repeated keys in batch order).  The log's n_keys must equal the cache's.  Device
+ * pointers; synchronizes once to size the value pool when the batch holds set or
+ * bounded-counter reads. */
 int am_snapcache_read(am_ctx *ctx, am_snapcache *cache, const am_op_log *dev_log, const am_read_batch *dev_batch,
                       am_read_result *dev_res);
+/* The same with internal_read's ShouldGC per read (should_gc [n] or NULL = all false).  When
+ * snapshot_insert_gc/4 runs for a key (its dict reached AM_SNAPSHOT_THRESHOLD, or ShouldGC),
+ * the dict keeps its newest AM_SNAPSHOT_MIN entries and, if gc_mask is given, gc_mask[key] =
+ * 1 with the prune threshold (vectorclock:min over the kept entries) in thr_vc[n_dc][n_keys]
+ * / thr_pres[n_keys]: exactly the prune arguments of am_store_update (gc_mask is cleared
+ * first). */
+int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *cache, const am_op_log *dev_log, const am_read_batch *dev_batch,
+                         const uint8_t *should_gc, am_read_result *dev_res, uint8_t *gc_mask, uint64_t *thr_vc,
+                         uint32_t *thr_pres);
 /* The same with host batch/result (blocks). */
 int am_snapcache_read_host(am_ctx *ctx, am_snapcache *cache, const am_store *st, const am_read_batch *host_batch,
                            am_read_result *host_res);
@@ -310,14 +325,39 @@ int am_snapcache_read_host(am_ctx *ctx, am_snapcache *cache, const am_store *st,
  * *n_entries = AM_SNAPCACHE_ABSENT before the key's first read.  NULL arrays are skipped. */
 int am_snapcache_get(am_ctx *ctx, const am_snapcache *cache, uint64_t key, uint32_t *n_entries, uint64_t *vc,
                      uint32_t *pres, int64_t *last_op, int64_t *v0, uint64_t *v1, uint8_t *vflag);
+/* Entry e's pool words (set pairs a/b; bounded-counter slot values a + presence pres, P slots
+ * From*n_dc+To then D slots): *n_words, at most cap_words copied to the host arrays. */
+int am_snapcache_get_value(am_ctx *ctx, const am_snapcache *cache, uint64_t key, uint32_t e, uint32_t cap_words,
+                           uint32_t *n_words, uint64_t *a, uint64_t *b, uint8_t *pres);
 
-/* The prune threshold snapshot_insert_gc/4 computes (src/materializer_vnode.erl:519-527):
- * for each key with cached snapshots, Thr = vectorclock:min (dict merge: a DC present in
- * any clock is kept) over the newest min(n, SNAPSHOT_MIN) entries.  Device outputs:
- * mask[n_keys] (1 = the key has a threshold), thr_vc[n_dc][n_keys], thr_pres[n_keys] --
- * exactly the prune arguments of am_store_update. */
-int am_snapcache_gc_threshold(am_ctx *ctx, const am_snapcache *cache, uint8_t *mask, uint64_t *thr_vc,
+/* A forced snapshot_insert_gc/4 on every cached key (src/materializer_vnode.erl:519-536): the
+ * dict keeps its newest min(n, SNAPSHOT_MIN) entries and Thr = vectorclock:min (dict merge: a
+ * DC present in any clock is kept) over them.  Device outputs: mask[n_keys] (1 = the key has
+ * a threshold), thr_vc[n_dc][n_keys], thr_pres[n_keys] -- exactly the prune arguments of
+ * am_store_update (so ops are only pruned below snapshots that stay cached). */
+int am_snapcache_gc_threshold(am_ctx *ctx, am_snapcache *cache, uint8_t *mask, uint64_t *thr_vc,
                               uint32_t *thr_pres);
+
+/* ---- one partition's materializer_vnode state: ops cache + snapshot cache ----
+ * am_vnode_insert_host runs op_insert_gc/3 (src/materializer_vnode.erl:622-647) for every op
+ * of host_ops (a host log over the vnode's n_keys keys, each key's ops oldest -> newest):
+ * NewId = OpCounter + 1, and when Length >= ListLen or NewId rem 50 == 0 the GC read
+ * internal_read(Key, Type, Op.snapshot_time, ignore, [], true) runs first (store the
+ * snapshot, snapshot_insert_gc/4: keep SNAPSHOT_MIN snapshots, prune_ops below their min,
+ * resize ListLen); load_ops/2 (:312-319) replays the log through this call.
+ * am_vnode_read_host runs internal_read/7 (:371-376) for a host batch (should_gc [n] or
+ * NULL), repeated keys served in batch order.  Reads whose dict reaches SNAPSHOT_THRESHOLD
+ * GC the same way.  Both block. */
+typedef struct am_vnode am_vnode;
+int am_vnode_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_vnode **out);
+int am_vnode_destroy(am_vnode *v);
+int am_vnode_insert_host(am_vnode *v, const am_op_log *host_ops);
+int am_vnode_read_host(am_vnode *v, const am_read_batch *host_batch, const uint8_t *should_gc,
+                       am_read_result *host_res);
+/* the vnode's current store and snapshot cache (borrowed; the store changes on GC) */
+int am_vnode_parts(am_vnode *v, am_store **st, am_snapcache **sc);
+/* the ops-cache tuple header of a key: {Length, ListLen} and OpCounter (element 3) */
+int am_vnode_key_info(am_vnode *v, uint64_t key, uint64_t *length, uint64_t *list_len, uint64_t *op_counter);
 
 /* ---- op-cache ingestion + garbage collection ----
  * Builds a new store from `st` (st is unchanged; destroy it when no read uses it):

@@ -46,16 +46,19 @@ def _dev_value(t, v0, v1, vflag):
     return (v0 & (2**64 - 1), v1, bool(vflag))
 
 
+@pytest.mark.parametrize("t", [abi.AM_PN, abi.AM_LWW, abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER])
 @pytest.mark.parametrize("seed", range(3))
-def test_gpu_snapcache_internal_read(mat, seed):
-    rng = random.Random(3300 + seed)
+def test_gpu_snapcache_internal_read(mat, seed, t):
+    """Every type's values are cached (PN / LWW in the entry, set pairs and bounded-counter
+    slots in the value pool) and serve later reads as bases."""
+    rng = random.Random(3300 + seed + 17 * t)
     n_dc = [1, 3, 5][seed]
     n_keys = 40
     keys, types = [], []
     for k in range(n_keys):
-        t = abi.AM_PN if k % 2 == 0 else abi.AM_LWW
-        keys.append(randlog.rand_key_ops(rng, t, n_dc, rng.choice([0, 3, 12, 40, 90, 200])))
-        types.append(t)
+        kt = t if k % 2 == 0 else (abi.AM_PN if t != abi.AM_PN else abi.AM_LWW)  # two types per batch
+        keys.append(randlog.rand_key_ops(rng, kt, n_dc, rng.choice([0, 3, 12, 40, 90, 200])))
+        types.append(kt)
     log = HostLog(n_dc, keys, key_types=types)
     store = mat.store(log)
     cache = mat.snapshot_cache(store, n_keys)
@@ -71,7 +74,7 @@ def test_gpu_snapcache_internal_read(mat, seed):
                 clock = {d: c + rng.randint(0, 3) for d in range(n_dc)}
                 reads.append(Read(k, types[k], clock))
             dup = Read(sel[0], types[sel[0]], dict(reads[0].clock))
-            got = cache.read(reads + [dup])
+            got = cache.read(reads + [dup], set_capacity=4096)
             assert got.result(len(reads)) == ("error", abi.AM_ERR_INVALID)  # second read of a key in a batch
             for i, rd in enumerate(reads):
                 try:
@@ -86,16 +89,15 @@ def test_gpu_snapcache_internal_read(mat, seed):
                 else:
                     assert g[0] == "ok" and g[1] == randlog.canon_state(rd.type, ref[1]), (rnd, rd, g, ref)
             for k in sel:
-                dev = cache.entries(k)
+                dev = cache.snapshots(k, types[k])
                 if k not in st.snapshot_cache:
                     assert dev is None
                     continue
                 lst, size = st.snapshot_cache[k]
                 assert len(dev) == size == len(lst), (rnd, k, dev, lst)
-                for (clock, snap), (dclock, dlo, v0, v1, vf) in zip(lst, dev):
+                for (clock, snap), (dclock, dlo, dval) in zip(lst, dev):
                     assert dict(clock) == dclock, (rnd, k)
-                    lo, val = _canon_entry(types[k], snap)
-                    assert (lo, val) == (dlo, _dev_value(types[k], v0, v1, vf)), (rnd, k, lo, val, dlo, v0, v1, vf)
+                    assert _canon_entry(types[k], snap) == (dlo, dval), (rnd, k, snap, dlo, dval)
     finally:
         cache.close()
         store.close()
