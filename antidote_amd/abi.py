@@ -37,6 +37,7 @@ AM_ERR_INVALID = -1
 AM_ERR_UNSUPPORTED = -5
 AM_FLAG_MISSING_DC_LOGGED = 0x1
 AM_META_BAD = 0x80
+AM_KEY_BINARY, AM_KEY_TERM = 0, 1
 AM_KEY_MIXED_TYPES = 0x1
 AM_MAX_DC = 32
 
@@ -130,6 +131,8 @@ SIGNATURES = [
     ("am_gst_finalize", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                 c_void_p]),
     ("am_key_partition", c_uint32, [c_int64, c_uint32]),
+    ("am_key_partition_bytes", c_uint32, [c_void_p, c_uint64, c_int, c_uint32]),
+    ("am_chash_key", c_int, [c_void_p, c_uint64, c_void_p]),
     ("am_snapcache_create", c_int, [c_void_p, c_uint32, c_uint64, POINTER(c_void_p)]),
     ("am_snapcache_destroy", c_int, [c_void_p]),
     ("am_snapcache_read", c_int, [c_void_p, c_void_p, POINTER(am_op_log), POINTER(am_read_batch),

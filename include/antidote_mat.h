@@ -403,6 +403,17 @@ int am_gst_finalize(am_ctx *ctx, uint32_t n_dc, const uint64_t *lanes, uint64_t 
 /* ---- sharding ---- */
 /* 0-based partition position for integer keys: abs(K) rem n_partitions. */
 uint32_t am_key_partition(int64_t key, uint32_t n_partitions);
+/* The same for keys passed as bytes (log_utilities:convert_key/1, src/log_utilities.erl:
+ * 100-118): AM_KEY_BINARY -- the key is a binary; its text, if list_to_integer accepts it
+ * ([+-]?[0-9]+, any length), gives abs(Int) rem n, else the SHA-1 chash_key path;
+ * AM_KEY_TERM -- bytes = term_to_binary(Key) of a key that is neither an integer nor a
+ * binary (chash_key({?BUCKET, term_to_binary(Key)})).  chash_key(B) = SHA-1 of
+ * term_to_binary({<<"antidote">>, B}); crypto:bytes_to_integer of it rem n. */
+#define AM_KEY_BINARY 0
+#define AM_KEY_TERM 1
+uint32_t am_key_partition_bytes(const uint8_t *bytes, uint64_t len, int kind, uint32_t n_partitions);
+/* riak_core_util:chash_key({<<"antidote">>, B}) for a binary B: 20-byte SHA-1 digest */
+int am_chash_key(const uint8_t *bytes, uint64_t len, uint8_t out[20]);
 
 /* ---- synthetic op logs (bench + parity; counter-based, regenerable per key) ---- */
 typedef struct am_synth_params {

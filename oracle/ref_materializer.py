@@ -761,15 +761,40 @@ def gst_gr(ss: dict) -> dict:
 # ---------------------------------------------------------------------------
 # key -> partition (src/log_utilities.erl:60-118)
 # ---------------------------------------------------------------------------
-def convert_key(key) -> int:
+BUCKET = b"antidote"       # include/antidote.hrl:2
+
+
+def chash_key(b: bytes) -> bytes:
+    """riak_core_util:chash_key({?BUCKET, B}) = crypto:hash(sha, term_to_binary({<<"antidote">>, B}))
+    for a binary B (SMALL_TUPLE_EXT of two BINARY_EXT; riak_core, un-vendored)."""
+    import hashlib
+    t2b = bytes([131, 104, 2, 109]) + len(BUCKET).to_bytes(4, "big") + BUCKET + bytes([109]) + \
+        len(b).to_bytes(4, "big") + b
+    return hashlib.sha1(t2b).digest()
+
+
+def _list_to_integer(text: bytes):
+    """erlang:list_to_integer/1 on a byte list: [+-]?[0-9]+, or None (badarg)."""
+    i = 1 if text[:1] in (b"+", b"-") else 0
+    if i == len(text) or not all(0x30 <= c <= 0x39 for c in text[i:]):
+        return None
+    v = int(text[i:].decode())
+    return -v if text[:1] == b"-" else v
+
+
+def convert_key(key, term_bytes: Optional[bytes] = None) -> int:
+    """:100-118.  A key that is neither an integer nor a binary is given as term_to_binary(Key)
+    (term_bytes)."""
     if isinstance(key, (bytes, Bin)):
-        try:
-            return abs(int(bytes(key).decode()))
-        except ValueError:
-            raise NotImplementedError("chash_key (SHA-1) path is out of scope")
+        v = _list_to_integer(bytes(key))
+        if v is not None:
+            return abs(v)
+        return abs(int.from_bytes(chash_key(bytes(key)), "big"))
     if isinstance(key, int):
         return abs(key)
-    raise NotImplementedError("chash_key (SHA-1) path is out of scope")
+    if term_bytes is None:
+        raise ValueError("a non-integer, non-binary key needs its term_to_binary bytes")
+    return abs(int.from_bytes(chash_key(term_bytes), "big"))
 
 
 def get_partition_index(key, num_partitions: int) -> int:
