@@ -7,7 +7,7 @@
     materializer_vnode:op_insert_gc/3 + prune_ops/2 (src/materializer_vnode.erl:565-647)
         -> Store.update(new_log, prune)
     materializer_vnode:load_from_log_to_tables/2 + load_ops/2 (:288-319)
-        -> Materializer.load_ops(n_dc, ops_by_key, key_types)
+        -> Materializer.load_ops(n_dc, ops_by_key, key_types) (a Vnode)
     stable_time_functions:get_min_time/1 + meta_data_sender:update_stable/3
         -> antidote_amd.gst
 
@@ -352,17 +352,14 @@ class Materializer:
         import numpy as np
         return _DevBuf.of(self, np.ascontiguousarray(arr))
 
-    def load_ops(self, n_dc: int, ops_by_key: Sequence[Sequence[Op]], key_types=None) -> Store:
-        """load_ops/2 (src/materializer_vnode.erl:312-319): every committed op of every key, in
-        log order, through op_insert_gc/3 -- one am_store_update of an empty ops cache, ids
-        1, 2, ... per key.  The write-triggered GC reads of op_insert_gc are not replayed
-        during the load (the keys come back flagged AM_GC_TRIGGER for a prune pass)."""
-        empty = self.store(HostLog(n_dc, [[] for _ in ops_by_key], key_types=key_types))
-        try:
-            st, _flags = empty.update(new_log=HostLog(n_dc, ops_by_key, key_types=key_types))
-            return st
-        finally:
-            empty.close()
+    def load_ops(self, n_dc: int, ops_by_key: Sequence[Sequence[Op]], key_types) -> "Vnode":
+        """load_from_log_to_tables/2 -> load_ops/2 (src/materializer_vnode.erl:288-319): every
+        committed op of every key, in log order, through op_insert_gc/3 -- ids 1, 2, ... per
+        key and the write-triggered GC reads (snapshots cached, ops pruned, ListLen resized)
+        exactly as the reference replays its log.  Returns the partition's Vnode."""
+        vn = Vnode(self, n_dc, len(ops_by_key))
+        vn.insert(ops_by_key, key_types)
+        return vn
 
     def synth_store(self, params: abi.am_synth_params) -> Store:
         h = ctypes.c_void_p()

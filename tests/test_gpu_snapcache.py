@@ -74,7 +74,7 @@ def test_gpu_snapcache_internal_read(mat, seed, t):
                 clock = {d: c + rng.randint(0, 3) for d in range(n_dc)}
                 reads.append(Read(k, types[k], clock))
             dup = Read(sel[0], types[sel[0]], dict(reads[0].clock))
-            got = cache.read(reads + [dup], set_capacity=4096)
+            got = cache.read(reads + [dup], set_capacity=[4096] * (len(reads) + 1))
             assert got.result(len(reads)) == ("error", abi.AM_ERR_INVALID)  # second read of a key in a batch
             for i, rd in enumerate(reads):
                 try:
