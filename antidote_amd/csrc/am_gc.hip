@@ -308,6 +308,8 @@ unsigned grid_keys(uint64_t n_keys) {
 
 extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *dev_new, const uint8_t *prune_mask,
                                const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags, am_store **out) {
+  if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   if (!c || !st || !out) return AM_ERR_INVALID;
   const am_op_log &L = st->dev;
   if (prune_mask && (!thr_vc || !thr_pres)) {

@@ -144,6 +144,8 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
 }
 
 extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_read_result *hr) {
+  if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   if (!st) return AM_ERR_INVALID;
   return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr, const void *) {
     return am_launch_materialize(c, &st->dev, db, dr);
@@ -153,6 +155,8 @@ extern "C" int am_materialize_host(am_ctx *c, const am_store *st, const am_read_
 extern "C" int am_snapcache_read_host(am_ctx *c, am_snapcache *sc, const am_store *st, const am_read_batch *hb,
                                       am_read_result *hr) {
   if (!st || !sc) return AM_ERR_INVALID;
+  if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   return run_host(c, st, hb, hr, [&](const am_read_batch *db, am_read_result *dr, const void *) {
     return am_snapcache_read(c, sc, &st->dev, db, dr);
   });

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../../include/antidote_mat.h"
@@ -20,7 +21,13 @@ struct am_ctx {
   void *scratch[AM_N_SCR] = {};  // grow-only device scratch slots (planner, row/group hand-offs, big-read path)
   size_t scratch_bytes[AM_N_SCR] = {};
   uint64_t *pinned = nullptr;    // small pinned host buffer for device -> host counters
+  // Every entry point that touches the stream, the scratch slots or the pinned buffer holds
+  // this lock, so concurrent callers on one context (a partition's READ_CONCURRENCY read
+  // servers, include/antidote.hrl:28) serialize instead of sharing scratch; recursive
+  // because composite calls (am_vnode_*, the *_host wrappers) re-enter.
+  std::recursive_mutex mu;
 };
+#define AM_LOCK(ctxp) std::lock_guard<std::recursive_mutex> am_lock_((ctxp)->mu)
 
 // A selection of a batch's reads: the planner's per-kernel sub-batches.  idx == nullptr
 // means the identity over [0, n_reads); otherwise the reads idx[range[0] .. range[1])

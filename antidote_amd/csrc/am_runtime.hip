@@ -59,18 +59,21 @@ void *am_ctx_stream(am_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 int am_ctx_sync(am_ctx *c) {
   if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   AM_HIP(hipStreamSynchronize(c->stream));
   return AM_OK;
 }
 
 int am_timer_start(am_ctx *c) {
   if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   AM_HIP(hipEventRecord(c->ev0, c->stream));
   return AM_OK;
 }
 
 int am_timer_stop(am_ctx *c, float *ms) {
   if (!c || !ms) return AM_ERR_INVALID;
+  AM_LOCK(c);
   AM_HIP(hipEventRecord(c->ev1, c->stream));
   AM_HIP(hipEventSynchronize(c->ev1));
   AM_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
@@ -104,6 +107,7 @@ int am_ctx_scratch(am_ctx *c, int slot, size_t bytes, void **out) {
 }
 
 int am_ctx_fetch(am_ctx *c, const void *dev, uint32_t n, uint64_t *host) {
+  AM_LOCK(c);
   if (n > 64) return AM_ERR_INVALID;
   if (!c->pinned) AM_HIP(hipHostMalloc((void **)&c->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault));
   AM_HIP(hipMemcpyAsync(c->pinned, dev, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -134,6 +138,7 @@ int am_dev_free(am_ctx *c, void *p) {
 
 int am_memcpy_h2d(am_ctx *c, void *dst, const void *src, size_t bytes) {
   if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   if (!bytes) return AM_OK;
   AM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
   AM_HIP(hipStreamSynchronize(c->stream));
@@ -142,6 +147,7 @@ int am_memcpy_h2d(am_ctx *c, void *dst, const void *src, size_t bytes) {
 
 int am_memcpy_d2h(am_ctx *c, void *dst, const void *src, size_t bytes) {
   if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   if (!bytes) return AM_OK;
   AM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
   AM_HIP(hipStreamSynchronize(c->stream));
@@ -179,6 +185,7 @@ extern "C" {
 
 int am_store_destroy(am_store *st) {
   if (!st) return AM_OK;
+  AM_LOCK(st->ctx);
   (void)hipSetDevice(st->ctx->device);
   (void)hipStreamSynchronize(st->ctx->stream);
   for (void *p : st->allocs) (void)hipFree(p);
@@ -187,6 +194,8 @@ int am_store_destroy(am_store *st) {
 }
 
 int am_store_create(am_ctx *c, const am_op_log *h, am_store **out) {
+  if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   if (!c || !h || !out || !h->key_off || !h->key_type || !h->op_meta || !h->commit_time || !h->p0) {
     am_set_error("am_store_create: missing required arrays");
     return AM_ERR_INVALID;
@@ -258,6 +267,7 @@ int am_store_log(const am_store *st, am_op_log *out) {
 // ---------------------------------------------------------------- hot path
 int am_materialize(am_ctx *c, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
   if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   AM_HIP(hipSetDevice(c->device));
   return am_launch_materialize(c, L, B, R);
 }
@@ -272,12 +282,15 @@ uint32_t am_key_partition(int64_t key, uint32_t n_partitions) {
 int am_gst_local_min(am_ctx *c, uint32_t n_dc, uint32_t n_part, const uint64_t *part_vc, const uint32_t *part_pres,
                      const uint8_t *part_undef, uint64_t *lanes) {
   if (!c || !lanes || n_dc == 0 || n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  AM_LOCK(c);
   AM_HIP(hipSetDevice(c->device));
   return am_launch_gst_local_min(c, n_dc, n_part, part_vc, part_pres, part_undef, lanes);
 }
 
 int am_gst_finalize(am_ctx *c, uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres, int gr,
                     uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed) {
+  if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   if (!c || !lanes || !last_vc || !last_pres || !out_vc || !out_pres || n_dc == 0 || n_dc > AM_MAX_DC)
     return AM_ERR_INVALID;
   AM_HIP(hipSetDevice(c->device));

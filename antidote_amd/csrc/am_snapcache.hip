@@ -411,6 +411,7 @@ extern "C" {
 
 int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcache **out) {
   if (!ctx || !out || n_dc == 0 || n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  AM_LOCK(ctx);
   AM_HIP(hipSetDevice(ctx->device));
   am_snapcache *c = new am_snapcache();
   c->ctx = ctx;
@@ -460,7 +461,10 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
 
 int am_snapcache_destroy(am_snapcache *c) {
   if (!c) return AM_OK;
-  if (c->ctx) (void)hipStreamSynchronize(c->ctx->stream);
+  if (!c->ctx) return AM_ERR_INVALID;
+  AM_LOCK(c->ctx);
+  (void)hipSetDevice(c->ctx->device);
+  (void)hipStreamSynchronize(c->ctx->stream);
   for (void *p : c->allocs) (void)hipFree(p);
   if (c->pool_a) (void)hipFree(c->pool_a);
   if (c->pool_b) (void)hipFree(c->pool_b);
@@ -473,6 +477,7 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
                          const uint8_t *should_gc, am_read_result *R, uint8_t *gc_mask, uint64_t *thr_vc,
                          uint32_t *thr_pres) {
   if (!ctx || !c || !L || !B || !R || c->ctx != ctx) return AM_ERR_INVALID;
+  AM_LOCK(ctx);
   if (L->n_dc != c->n_dc || L->n_keys != c->n_keys) {
     am_set_error("snapshot cache: n_dc / n_keys do not match the log");
     return AM_ERR_INVALID;
@@ -573,6 +578,7 @@ int am_snapcache_read(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const am
 
 int am_snapcache_gc_threshold(am_ctx *ctx, am_snapcache *c, uint8_t *mask, uint64_t *thr_vc, uint32_t *thr_pres) {
   if (!ctx || !c || !mask || !thr_vc || !thr_pres) return AM_ERR_INVALID;
+  AM_LOCK(ctx);
   AM_HIP(hipSetDevice(ctx->device));
   if (c->n_keys == 0) return AM_OK;
   hipLaunchKernelGGL(k_sc_threshold, dim3(grid(c->n_keys)), dim3(256), 0, ctx->stream, view(c), mask, thr_vc, thr_pres);
@@ -583,6 +589,7 @@ int am_snapcache_gc_threshold(am_ctx *ctx, am_snapcache *c, uint8_t *mask, uint6
 int am_snapcache_get(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t *n_entries, uint64_t *vc,
                      uint32_t *pres, int64_t *last_op, int64_t *v0, uint64_t *v1, uint8_t *vflag) {
   if (!ctx || !c || !n_entries || key >= c->n_keys) return AM_ERR_INVALID;
+  AM_LOCK(ctx);
   AM_HIP(hipSetDevice(ctx->device));
   uint8_t cnt = 0;
   const uint64_t s0 = key * CAP, nd = c->n_dc;
@@ -601,6 +608,7 @@ int am_snapcache_get(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t 
 int am_snapcache_get_value(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t e, uint32_t cap_words,
                            uint32_t *n_words, uint64_t *a, uint64_t *b, uint8_t *pres) {
   if (!ctx || !c || !n_words || key >= c->n_keys || e >= CAP) return AM_ERR_INVALID;
+  AM_LOCK(ctx);
   AM_HIP(hipSetDevice(ctx->device));
   const uint64_t s = key * CAP + e;
   uint64_t off = 0;

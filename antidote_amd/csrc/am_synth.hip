@@ -144,6 +144,8 @@ __global__ void k_gen_var(am_synth_params p, const uint64_t *key_off, const uint
 extern "C" {
 
 int am_synth_store(am_ctx *c, const am_synth_params *p, am_store **out) {
+  if (!c) return AM_ERR_INVALID;
+  AM_LOCK(c);
   int rc = check_params(p);
   if (rc) return rc;
   if (!c || !out) return AM_ERR_INVALID;

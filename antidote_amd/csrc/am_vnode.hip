@@ -295,6 +295,8 @@ int am_vnode_destroy(am_vnode *v) {
 }
 
 int am_vnode_insert_host(am_vnode *v, const am_op_log *h) {
+  if (!v) return AM_ERR_INVALID;
+  AM_LOCK(v->ctx);
   if (!v || !h || h->n_keys != v->n_keys || h->n_dc != v->n_dc || !h->key_off || !h->key_type || !h->op_meta ||
       !h->commit_time || !h->p0 || (h->n_ops && !h->snap_vc)) {
     am_set_error("am_vnode_insert_host: the new ops must be a host log over the vnode's keys");
@@ -340,6 +342,8 @@ int am_vnode_insert_host(am_vnode *v, const am_op_log *h) {
 }
 
 int am_vnode_read_host(am_vnode *v, const am_read_batch *hb, const uint8_t *should_gc, am_read_result *hr) {
+  if (!v) return AM_ERR_INVALID;
+  AM_LOCK(v->ctx);
   if (!v || !hb || !hr || !hb->key || !hb->type || !hb->read_vc || !hb->read_pres) return AM_ERR_INVALID;
   AM_HIP(hipSetDevice(v->ctx->device));
   const uint64_t n = hb->n_reads, nd = v->n_dc;
@@ -424,6 +428,8 @@ int am_vnode_parts(am_vnode *v, am_store **st, am_snapcache **sc) {
 }
 
 int am_vnode_key_info(am_vnode *v, uint64_t key, uint64_t *length, uint64_t *list_len, uint64_t *op_counter) {
+  if (!v) return AM_ERR_INVALID;
+  AM_LOCK(v->ctx);
   if (!v || key >= v->n_keys) return AM_ERR_INVALID;
   if (length) *length = ref_len(v, key);
   if (list_len) *list_len = v->list_len[key];
