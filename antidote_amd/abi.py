@@ -91,7 +91,7 @@ class am_synth_params(ctypes.Structure):
     _fields_ = [
         ("seed", c_uint64), ("n_keys", c_uint64), ("ops_per_key", c_uint32), ("n_dc", c_uint32),
         ("type", c_uint32), ("key_base", c_uint32), ("max_lag", c_uint32), ("zipf_milli", c_uint32),
-        ("total_ops", c_uint64), ("hot_cap", c_uint32), ("universe", c_uint32),
+        ("total_ops", c_uint64), ("hot_cap", c_uint32), ("universe", c_uint32), ("part_mask", c_uint64),
     ]
 
 
@@ -156,6 +156,7 @@ SIGNATURES = [
                                 POINTER(c_void_p)]),
     ("am_synth_store", c_int, [c_void_p, POINTER(am_synth_params), POINTER(c_void_p)]),
     ("am_synth_read_clock", c_int, [POINTER(am_synth_params), c_double, c_void_p]),
+    ("am_synth_key", c_uint64, [POINTER(am_synth_params), c_uint64]),
     ("am_synth_host_sizes", c_int, [POINTER(am_synth_params), c_uint64, c_uint64, POINTER(c_uint64),
                                     POINTER(c_uint64)]),
     ("am_synth_host", c_int, [POINTER(am_synth_params), c_uint64, c_uint64, POINTER(am_op_log)]),

@@ -64,6 +64,18 @@ AM_HD void var_write(const am_synth_params &p, uint64_t key, uint64_t i, uint32_
   }
 }
 
+// Global key of local key k: contiguous from key_base, or the k-th key of the owned
+// partitions (key mod 64 in part_mask), so a rank holds exactly the keys
+// get_key_partition/1 sends to its partitions (src/log_utilities.erl:60-79).
+AM_HD uint64_t global_key(const am_synth_params &p, uint64_t k) {
+  if (!p.part_mask) return p.key_base + k;
+  const uint32_t m = (uint32_t)__builtin_popcountll(p.part_mask);
+  uint64_t r = k % m, bits = p.part_mask;
+  for (; r; --r) bits &= bits - 1;  // drop the r lowest owned partitions
+  const uint64_t base = ((uint64_t)p.key_base + 63) / 64 * 64;
+  return base + (k / m) * 64 + (uint64_t)__builtin_ctzll(bits);
+}
+
 bool needs_var(const am_synth_params &p) { return p.type == 0 || p.type == AM_AWSET || p.type == AM_MVREG || p.type == AM_SYNTH_MV_BC; }
 bool needs_p1(const am_synth_params &p) { return p.type != AM_PN; }
 
@@ -112,7 +124,7 @@ void key_lengths(const am_synth_params &p, uint64_t k0, uint64_t nk, std::vector
 __global__ void k_gen_ops(am_synth_params p, const uint64_t *key_off, uint64_t stride, uint8_t *key_type,
                           uint8_t *meta, uint64_t *ct, uint64_t *snap, uint64_t *p0, uint64_t *p1, uint64_t *vlen) {
   for (uint64_t k = blockIdx.x; k < p.n_keys; k += gridDim.x) {
-    const uint64_t key = p.key_base + k;
+    const uint64_t key = global_key(p, k);
     const uint32_t kt = am_syn_key_type(p.seed, key, p.type);
     if (threadIdx.x == 0) key_type[k] = (uint8_t)kt;
     const uint64_t off = key_off[k], n = key_off[k + 1] - off;
@@ -132,7 +144,7 @@ __global__ void k_gen_ops(am_synth_params p, const uint64_t *key_off, uint64_t s
 
 __global__ void k_gen_var(am_synth_params p, const uint64_t *key_off, const uint64_t *var_off, uint64_t *var_data) {
   for (uint64_t k = blockIdx.x; k < p.n_keys; k += gridDim.x) {
-    const uint64_t key = p.key_base + k;
+    const uint64_t key = global_key(p, k);
     const uint32_t kt = am_syn_key_type(p.seed, key, p.type);
     const uint64_t off = key_off[k], n = key_off[k + 1] - off;
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) var_write(p, key, i, kt, var_data + var_off[off + i]);
@@ -264,6 +276,8 @@ int am_synth_read_clock(const am_synth_params *p, double q, uint64_t *out_vc) {
   return AM_OK;
 }
 
+uint64_t am_synth_key(const am_synth_params *p, uint64_t k) { return p ? global_key(*p, k) : 0; }
+
 int am_synth_host_sizes(const am_synth_params *p, uint64_t k0, uint64_t nk, uint64_t *n_ops, uint64_t *n_var) {
   int rc = check_params(p);
   if (rc) return rc;
@@ -271,7 +285,7 @@ int am_synth_host_sizes(const am_synth_params *p, uint64_t k0, uint64_t nk, uint
   key_lengths(*p, k0, nk, len);
   uint64_t no = 0, nv = 0;
   for (uint64_t k = 0; k < nk; ++k) {
-    const uint64_t key = p->key_base + k0 + k;
+    const uint64_t key = global_key(*p, k0 + k);
     const uint32_t kt = am_syn_key_type(p->seed, key, p->type);
     for (uint64_t i = 0; i < len[k]; ++i) nv += var_words(*p, key, i, kt);
     no += len[k];
@@ -305,7 +319,7 @@ int am_synth_host(const am_synth_params *p, uint64_t k0, uint64_t nk, am_op_log 
   uint64_t q = 0, w = 0;
   key_off[0] = 0;
   for (uint64_t k = 0; k < nk; ++k) {
-    const uint64_t key = p->key_base + k0 + k;
+    const uint64_t key = global_key(*p, k0 + k);
     const uint32_t kt = am_syn_key_type(p->seed, key, p->type);
     key_type[k] = (uint8_t)kt;
     for (uint64_t i = 0; i < len[k]; ++i, ++q) {

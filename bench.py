@@ -13,7 +13,8 @@ Default workload (BASELINE.json configs[1], "c2"): antidote_crdt_register_lww, 1
 256 ops per GPU, 3-DC vectorclocks, synthetic counter-based logs generated in HBM.
 --config c1..c5 selects the other BASELINE.json configs (see CONFIGS).
 Weak scaling: each rank owns its own keys (keys shard by riak_core partition:
-partition = key mod 64, GPU = partition mod N), so value = N * ops per GPU / step time.
+partition = key mod 64, GPU = partition mod N; rank r's log holds exactly the keys with
+am_key_partition(key, 64) % N == r), so value = N * ops per GPU / step time.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W --config c2]; for N > 1 under
 torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR from the env).
@@ -92,9 +93,19 @@ def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
     return 8 + 1 + 8 + 1 + 4 + 8 + 8 * n_dc + 4 + 1 + 1 + 4 + 1 + val
 
 
-def synth_params(cfg, key_base):
-    return synth.params(cfg["n_keys"], cfg["n_dc"], cfg["type"], ops_per_key=cfg.get("ops", 0), key_base=key_base,
-                        zipf=cfg.get("zipf", 0.0), total_ops=cfg.get("total_ops", 0), hot_cap=cfg.get("hot_cap", 0))
+def owned_partitions_mask(rank: int, world: int) -> int:
+    """The riak_core partitions (of N_PARTITIONS) rank owns: p % world == rank."""
+    return sum(1 << pp for pp in range(N_PARTITIONS) if pp % world == rank)
+
+
+def synth_params(cfg, rank=0, world=1):
+    """This rank's log: exactly the integer keys whose partition am_key_partition(key, 64)
+    (= key mod 64, src/log_utilities.erl:60-79) this rank owns -- local key k is the k-th
+    of them (am_synth_params.part_mask).  Per-GPU work is fixed (weak scaling)."""
+    p = synth.params(cfg["n_keys"], cfg["n_dc"], cfg["type"], ops_per_key=cfg.get("ops", 0),
+                     zipf=cfg.get("zipf", 0.0), total_ops=cfg.get("total_ops", 0), hot_cap=cfg.get("hot_cap", 0))
+    p.part_mask = owned_partitions_mask(rank, world)
+    return p
 
 
 def key_columns(mat, dlog, n_keys):
@@ -234,7 +245,7 @@ def main():
     abi.check(rc, "am_comm_init")
 
     # ---- this GPU's op log, generated in HBM ----
-    p = synth_params(cfg, key_base=rank * n_keys)
+    p = synth_params(cfg, rank, world)
     store = mat.synth_store(p)
     dlog = store.device_log()
     ko, kt = key_columns(mat, dlog, n_keys)
@@ -242,7 +253,7 @@ def main():
 
     # ---- partition stable clocks (GST inputs): this rank owns partitions r, r+N, ... ----
     clock = synth.read_clock(p, Q)
-    parts = [pp for pp in range(N_PARTITIONS) if pp % world == rank]
+    parts = [pp for pp in range(N_PARTITIONS) if (p.part_mask >> pp) & 1]
     pvc = np.zeros((len(parts), n_dc), np.uint64)
     for i, pp in enumerate(parts):
         for d in range(n_dc):
@@ -327,6 +338,7 @@ def main():
         "data": f"synthetic (counter-based splitmix64 op logs generated in HBM; seed {hex(p.seed)})",
         "config": {"workload": workload, "keys_per_gpu": n_keys, "ops_per_gpu": n_ops, "n_dc": n_dc,
                    "snapshot_quantile": Q, "partitions": N_PARTITIONS, "parallelism": f"partition-sharded x{world}",
+                   "key_placement": "rank r holds the keys with am_key_partition(key, 64) % N == r",
                    "step": "GST min all-reduce (RCCL) + materialize all keys"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config, workload),

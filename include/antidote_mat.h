@@ -429,12 +429,18 @@ typedef struct am_synth_params {
   uint64_t total_ops;    /* Zipf: target total ops over all keys               */
   uint32_t hot_cap;      /* Zipf: cap on one key's log length                  */
   uint32_t universe;     /* AW-set element universe per key (power of two)     */
+  uint64_t part_mask;    /* 0: local key k is global key key_base + k.  Else the
+                            riak_core partitions (of 64) this GPU owns: local key
+                            k is the k-th integer key >= key_base whose partition
+                            am_key_partition(key, 64) = key mod 64 is in the mask */
 } am_synth_params;
 #define AM_SYNTH_MV_BC 6
 /* Device log owned by the returned store. */
 int am_synth_store(am_ctx *ctx, const am_synth_params *p, am_store **out);
 /* The read clock the generator's quantile q selects (q in [0,1]); host output [n_dc]. */
 int am_synth_read_clock(const am_synth_params *p, double q, uint64_t *out_vc);
+/* The global key of local key k (see part_mask). */
+uint64_t am_synth_key(const am_synth_params *p, uint64_t k);
 /* Regenerate keys [k0, k0+nk) on the host into caller buffers sized by
  * am_synth_host_sizes (for parity checks against the oracle). */
 int am_synth_host_sizes(const am_synth_params *p, uint64_t k0, uint64_t nk, uint64_t *n_ops,

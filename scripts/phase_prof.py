@@ -14,7 +14,7 @@ from antidote_amd.materializer import Materializer  # noqa: E402
 def main():
     cfg = bench.CONFIGS["c3"]
     mat = Materializer(0)
-    p = bench.synth_params(cfg, key_base=0)
+    p = bench.synth_params(cfg)
     store = mat.synth_store(p)
     dlog = store.device_log()
     clock = synth.read_clock(p, 0.75)

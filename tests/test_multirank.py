@@ -103,3 +103,60 @@ def test_lane_encoding_roundtrip():
     assert gst.decode(gst.encode_node(None, 3), 3) == {}
     with pytest.raises(ValueError):
         gst.encode_node({0: 2**64 - 1}, 1)
+
+
+def _placement_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    import bench
+    from antidote_amd import abi, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = abi.lib()
+        cfg = dict(bench.CONFIGS["c4"], n_keys=96, ops=5)
+        p = bench.synth_params(cfg, rank, world)
+        keys = [int(L.am_synth_key(p, k)) for k in range(p.n_keys)]
+        bad = [k for k in keys if L.am_key_partition(k, bench.N_PARTITIONS) % world != rank]
+        mine = [pp for pp in range(bench.N_PARTITIONS) if (p.part_mask >> pp) & 1]
+        # the rank's log is the global log's slice: key k of this rank == global key keys[k]
+        log = synth.host_log(p, 0, p.n_keys)
+        g = bench.synth_params(cfg)  # one rank holding every key (identity placement)
+        g.n_keys = max(keys) + 1
+        same = True
+        for k in (0, 1, p.n_keys // 2, p.n_keys - 1):
+            a = synth.host_log(p, k, 1)
+            b = synth.host_log(g, keys[k], 1)
+            same &= bool((a.commit_time == b.commit_time).all() and (a.p0 == b.p0).all()
+                         and (a.key_type == b.key_type).all() and (a.snap_vc == b.snap_vc).all())
+        out = [None] * world
+        dist.all_gather_object(out, (keys, mine))
+        q.put((rank, bad, same, out, int(log.n_keys)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_key_placement_follows_partitions(world):
+    """bench.py's per-rank logs (am_synth_params.part_mask): rank r holds exactly the keys
+    with am_key_partition(key, 64) % N == r, the GST partitions it reduces are the same
+    partitions, ranks are disjoint and together hold the first n_keys * N integer keys, and a
+    key's ops are the same whichever rank generates them."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_placement_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, bad, same, out, nk in res:
+        assert bad == [] and same and nk == 96, (rank, bad, same)
+        allkeys = [k for keys, _ in out for k in keys]
+        assert sorted(allkeys) == list(range(96 * world))
+        for r, (keys, mine) in enumerate(out):
+            assert mine == [pp for pp in range(N_PART) if pp % world == r]
+            assert {k % N_PART for k in keys} <= set(mine)
