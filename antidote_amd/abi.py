@@ -38,6 +38,7 @@ AM_ERR_UNSUPPORTED = -5
 AM_FLAG_MISSING_DC_LOGGED = 0x1
 AM_META_BAD = 0x80
 AM_KEY_BINARY, AM_KEY_TERM = 0, 1
+AM_CODEC_ABSENT = 1
 AM_KEY_MIXED_TYPES = 0x1
 AM_MAX_DC = 32
 
@@ -154,6 +155,17 @@ SIGNATURES = [
     ("am_vnode_key_info", c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
     ("am_store_update", c_int, [c_void_p, c_void_p, POINTER(am_op_log), c_void_p, c_void_p, c_void_p, c_void_p,
                                 POINTER(c_void_p)]),
+    ("am_codec_create", c_int, [POINTER(c_void_p)]),
+    ("am_codec_destroy", c_int, [c_void_p]),
+    ("am_codec_intern", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, POINTER(c_int)]),
+    ("am_codec_lookup", c_int, [c_void_p, c_char_p, c_uint64, POINTER(c_uint64)]),
+    ("am_codec_term", c_int, [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]),
+    ("am_codec_size", c_uint64, [c_void_p]),
+    ("am_codec_take_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    ("am_codec_compare", c_int, [c_char_p, c_uint64, c_char_p, c_uint64, POINTER(c_int)]),
+    ("am_store_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]),
+    ("am_snapcache_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]),
+    ("am_vnode_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
     ("am_synth_store", c_int, [c_void_p, POINTER(am_synth_params), POINTER(c_void_p)]),
     ("am_synth_read_clock", c_int, [POINTER(am_synth_params), c_double, c_void_p]),
     ("am_synth_key", c_uint64, [POINTER(am_synth_params), c_uint64]),

@@ -125,3 +125,7 @@ inline bool am_batch_general(const am_op_log *L, const am_read_batch *B) {
 }
 // the packed streaming view applies (u32 entries relative to the key time base, full clocks)
 inline bool am_log_packed(const am_op_log *L) { return L->key_tbase && L->pk_vc && !L->snap_pres; }
+// a relabel map (am_codec_take_relabel) copied to the device; old labels strictly increasing.
+// The caller hipFrees both after a stream synchronize.
+int am_relabel_upload(am_ctx *c, const uint64_t *old_labels, const uint64_t *new_labels, uint64_t n, uint64_t **d_old,
+                      uint64_t **d_new);

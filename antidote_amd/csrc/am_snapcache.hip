@@ -405,6 +405,43 @@ int pool_reserve(am_snapcache *c, uint64_t need) {
   return AM_OK;
 }
 
+
+// relabelling (am_codec): LWW entry values in place; the pool words of set entries are
+// marked first, so a pool word two entries share is relabelled once
+__device__ __forceinline__ void sc_relabel_word(uint64_t *w, const uint64_t *old, const uint64_t *nw, uint64_t n) {
+  const uint64_t x = *w;
+  if (x == 0 || x == ~0ull) return;
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (old[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < n && old[lo] == x) *w = nw[lo];
+}
+
+__global__ void k_sc_relabel_entries(const uint8_t *cnt, uint64_t n_keys, const uint8_t *ktype, const uint8_t *vflag,
+                                     uint64_t *v1, const uint64_t *poff, const uint32_t *plen, uint32_t *mark,
+                                     const uint64_t *old, const uint64_t *nw, uint64_t n) {
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_keys * CAP; s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = s / CAP;
+    if (cnt[k] == ABSENT || s % CAP >= cnt[k]) continue;
+    const uint32_t t = ktype[k];
+    if (t == AM_LWW && !vflag[s]) sc_relabel_word(v1 + s, old, nw, n);
+    if (t == AM_AWSET || t == AM_MVREG)
+      for (uint64_t w = poff[s]; w < poff[s] + plen[s]; ++w) atomicOr(&mark[w / 32], 1u << (w % 32));
+  }
+}
+
+__global__ void k_sc_relabel_pool(uint64_t *pa, uint64_t *pb, const uint32_t *mark, uint64_t words, const uint64_t *old,
+                                  const uint64_t *nw, uint64_t n) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (uint64_t)gridDim.x * blockDim.x)
+    if ((mark[w / 32] >> (w % 32)) & 1u) {
+      sc_relabel_word(pa + w, old, nw, n);
+      sc_relabel_word(pb + w, old, nw, n);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -456,6 +493,38 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
     return rc;
   }
   *out = c;
+  return AM_OK;
+}
+
+int am_snapcache_relabel(am_ctx *ctx, am_snapcache *c, const uint8_t *key_type, const uint64_t *old_labels,
+                         const uint64_t *new_labels, uint64_t n) {
+  if (!ctx || !c || c->ctx != ctx || !key_type || (n && (!old_labels || !new_labels))) return AM_ERR_INVALID;
+  AM_LOCK(ctx);
+  if (n == 0 || c->n_keys == 0) return AM_OK;
+  AM_HIP(hipSetDevice(ctx->device));
+  uint64_t *d_old = nullptr, *d_new = nullptr;
+  if (int rc = am_relabel_upload(ctx, old_labels, new_labels, n, &d_old, &d_new)) return rc;
+  uint32_t *mark = nullptr;
+  const uint64_t mwords = c->pool_cap / 32 + 1;
+  bool ok = hipMalloc((void **)&mark, mwords * 4) == hipSuccess &&
+            hipMemsetAsync(mark, 0, mwords * 4, ctx->stream) == hipSuccess;
+  if (ok) {
+    const uint64_t ns = c->n_keys * CAP;
+    hipLaunchKernelGGL(k_sc_relabel_entries, dim3((unsigned)std::min<uint64_t>((ns + 255) / 256, 65536)), dim3(256), 0,
+                       ctx->stream, c->cnt, c->n_keys, key_type, c->vflag, c->v1, c->poff, c->plen, mark, d_old, d_new,
+                       n);
+    hipLaunchKernelGGL(k_sc_relabel_pool, dim3((unsigned)std::min<uint64_t>((c->pool_cap + 255) / 256, 65536)),
+                       dim3(256), 0, ctx->stream, c->pool_a, c->pool_b, mark, c->pool_cap, d_old, d_new, n);
+    ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(ctx->stream) == hipSuccess;
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  if (mark) (void)hipFree(mark);
+  (void)hipFree(d_old);
+  (void)hipFree(d_new);
+  if (!ok) {
+    am_set_error("am_snapcache_relabel: failed");
+    return AM_ERR_HIP;
+  }
   return AM_OK;
 }
 

@@ -420,6 +420,14 @@ int am_vnode_read_host(am_vnode *v, const am_read_batch *hb, const uint8_t *shou
   return AM_OK;
 }
 
+int am_vnode_relabel(am_vnode *v, const uint64_t *old_labels, const uint64_t *new_labels, uint64_t n) {
+  if (!v) return AM_ERR_INVALID;
+  AM_LOCK(v->ctx);
+  int rc = am_store_relabel(v->ctx, v->st, old_labels, new_labels, n);
+  if (!rc) rc = am_snapcache_relabel(v->ctx, v->sc, v->st->dev.key_type, old_labels, new_labels, n);
+  return rc;
+}
+
 int am_vnode_parts(am_vnode *v, am_store **st, am_snapcache **sc) {
   if (!v) return AM_ERR_INVALID;
   if (st) *st = v->st;

@@ -27,8 +27,8 @@ IGNORE = None
 class Store:
     """A device-resident op log (one partition's ops cache in HBM)."""
 
-    def __init__(self, mat: "Materializer", handle: ctypes.c_void_p, n_dc: int):
-        self.mat, self.handle, self.n_dc = mat, handle, n_dc
+    def __init__(self, mat: "Materializer", handle: ctypes.c_void_p, n_dc: int, owned: bool = True):
+        self.mat, self.handle, self.n_dc, self.owned = mat, handle, n_dc, owned
 
     def device_log(self) -> abi.am_op_log:
         s = abi.am_op_log()
@@ -81,6 +81,13 @@ class Store:
             if tmp_store is not None:
                 tmp_store.close()
 
+    def relabel(self, old, new):
+        """Apply a codec relabel map (Codec.take_relabel) to the store's label words in place."""
+        import numpy as np
+        o, n = np.ascontiguousarray(old, np.uint64), np.ascontiguousarray(new, np.uint64)
+        abi.check(self.mat.L.am_store_relabel(self.mat.ctx, self.handle, o.ctypes.data, n.ctypes.data, len(o)),
+                  "am_store_relabel")
+
     def download(self) -> Dict[str, Any]:
         """The device log's columns as numpy arrays (for parity checks); op_id is always
         filled (dense ids from key_id_base when the store keeps no explicit column)."""
@@ -118,7 +125,8 @@ class Store:
 
     def close(self):
         if self.handle:
-            abi.lib().am_store_destroy(self.handle)
+            if self.owned:
+                abi.lib().am_store_destroy(self.handle)
             self.handle = None
 
     def __del__(self):
@@ -225,6 +233,13 @@ class SnapshotCache:
         """[(clock, last_op_id, value)] newest first, or None before the key's first read."""
         return _cache_snapshots(self.mat, self.handle, self.store.n_dc, key, type_)
 
+    def relabel(self, old, new):
+        """Apply a codec relabel map to the cache (key types from the store it serves)."""
+        import numpy as np
+        o, n = np.ascontiguousarray(old, np.uint64), np.ascontiguousarray(new, np.uint64)
+        abi.check(self.mat.L.am_snapcache_relabel(self.mat.ctx, self.handle, self.store.device_log().key_type,
+                                                  o.ctypes.data, n.ctypes.data, len(o)), "am_snapcache_relabel")
+
     def entries(self, key: int):
         """[(clock, last_op_id, v0, v1, vflag)] newest first, or None before the key's first read."""
         import numpy as np
@@ -286,10 +301,21 @@ class Vnode:
                   "am_vnode_key_info")
         return int(a.value), int(b.value), int(c.value)
 
+    def relabel(self, old, new):
+        """Apply a codec relabel map (Codec.take_relabel) to the ops cache and snapshot cache."""
+        import numpy as np
+        o, n = np.ascontiguousarray(old, np.uint64), np.ascontiguousarray(new, np.uint64)
+        abi.check(self.mat.L.am_vnode_relabel(self.handle, o.ctypes.data, n.ctypes.data, len(o)), "am_vnode_relabel")
+
     def _parts(self):
         st, sc = ctypes.c_void_p(), ctypes.c_void_p()
         abi.check(self.mat.L.am_vnode_parts(self.handle, ctypes.byref(st), ctypes.byref(sc)), "am_vnode_parts")
         return st, sc
+
+    def store(self) -> Store:
+        """The ops cache as a borrowed Store (valid until the next insert)."""
+        st, _ = self._parts()
+        return Store(self.mat, st, self.n_dc, owned=False)
 
     def op_ids(self, key: int) -> List[int]:
         """The op ids in the key's ops cache, oldest first."""

@@ -415,6 +415,44 @@ uint32_t am_key_partition_bytes(const uint8_t *bytes, uint64_t len, int kind, ui
 /* riak_core_util:chash_key({<<"antidote">>, B}) for a binary B: 20-byte SHA-1 digest */
 int am_chash_key(const uint8_t *bytes, uint64_t len, uint8_t out[20]);
 
+/* ---- term codec (am_codec.hip) ----
+ * Order-preserving interning of Erlang terms (external term format, enif_term_to_binary)
+ * into the u64 LABELS the device holds for LWW values, MV values and tokens, and add-wins-set
+ * elements and tokens: label order == Erlang term order, so the device's sorted outputs are
+ * the reference's orddict order, and am_codec_term turns labels back into terms.  One codec
+ * per partition (or node); thread-safe.  Labels lie in [1, 2^64-2].  Supported terms:
+ * integers, floats, atoms, tuples, lists (proper and improper), binaries and bitstrings;
+ * maps, pids, ports, references and funs give AM_ERR_UNSUPPORTED.  Terms that compare equal
+ * (1 and 1.0) share one label.
+ * When a call needs room that the label space no longer has between two neighbours, every
+ * label is re-spread (order kept) and *relabeled is set: take the old -> new map with
+ * am_codec_take_relabel and apply it with am_store_relabel / am_snapcache_relabel /
+ * am_vnode_relabel to every structure holding labels BEFORE putting this call's labels on
+ * the device.  Until the map is taken, am_codec_intern fails with AM_ERR_INVALID. */
+typedef struct am_codec am_codec;
+#define AM_CODEC_ABSENT 1 /* am_codec_lookup: the term was never interned */
+int am_codec_create(am_codec **out);
+int am_codec_destroy(am_codec *c);
+int am_codec_intern(am_codec *c, uint64_t n, const uint8_t *const *terms, const uint64_t *lens, uint64_t *labels,
+                    int *relabeled);
+int am_codec_lookup(am_codec *c, const uint8_t *term, uint64_t len, uint64_t *label);
+/* the term of a label (external term format); *len always set; AM_ERR_CAPACITY if cap < len */
+int am_codec_term(am_codec *c, uint64_t label, uint8_t *buf, uint64_t cap, uint64_t *len);
+uint64_t am_codec_size(am_codec *c);
+/* pending relabel map, old labels increasing; old/new NULL: *n = its size only */
+int am_codec_take_relabel(am_codec *c, uint64_t *old_labels, uint64_t *new_labels, uint64_t cap, uint64_t *n);
+/* Erlang term order of two encoded terms: *out = -1, 0, 1 */
+int am_codec_compare(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb, int *out);
+/* apply a relabel map (host arrays from am_codec_take_relabel) in place: the store's LWW
+ * values, MV values and tokens, AW elements and tokens, and its token-group view */
+int am_store_relabel(am_ctx *ctx, am_store *st, const uint64_t *old_labels, const uint64_t *new_labels, uint64_t n);
+/* the same for a snapshot cache: LWW values and the set pairs in the value pool; key_type is
+ * the device key-type column of the store the cache serves ([n_keys]) */
+int am_snapcache_relabel(am_ctx *ctx, am_snapcache *c, const uint8_t *key_type, const uint64_t *old_labels,
+                         const uint64_t *new_labels, uint64_t n);
+/* both, for a vnode's ops cache and snapshot cache */
+int am_vnode_relabel(am_vnode *v, const uint64_t *old_labels, const uint64_t *new_labels, uint64_t n);
+
 /* ---- synthetic op logs (bench + parity; counter-based, regenerable per key) ---- */
 typedef struct am_synth_params {
   uint64_t seed;
