@@ -155,6 +155,11 @@ SIGNATURES = [
     ("am_vnode_key_info", c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
     ("am_store_update", c_int, [c_void_p, c_void_p, POINTER(am_op_log), c_void_p, c_void_p, c_void_p, c_void_p,
                                 POINTER(c_void_p)]),
+    ("am_read_objects_host", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, POINTER(am_read_batch),
+                                     POINTER(am_read_result)]),
+    ("am_read_objects_submit", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, POINTER(am_read_batch),
+                                       POINTER(am_read_result), POINTER(c_void_p)]),
+    ("am_ticket_wait", c_int, [c_void_p]),
     ("am_codec_create", c_int, [POINTER(c_void_p)]),
     ("am_codec_destroy", c_int, [c_void_p]),
     ("am_codec_intern", c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, POINTER(c_int)]),

@@ -17,6 +17,7 @@
 // keys), run the triggered keys' GC reads as one batch, prune them (one rebuild), repeat.
 // The host keeps the per-key tuple header (Length, ListLen, OpCounter) the rounds plan with.
 #include <algorithm>
+#include <thread>
 
 #include "am_internal.h"
 
@@ -443,6 +444,72 @@ int am_vnode_key_info(am_vnode *v, uint64_t key, uint64_t *length, uint64_t *lis
   if (list_len) *list_len = v->list_len[key];
   if (op_counter) *op_counter = v->counter[key];
   return AM_OK;
+}
+
+}  // extern "C"
+
+// ---- read_objects over a node's partitions: one vnode whose key space concatenates them
+struct am_ticket {
+  std::thread th;
+  int rc = AM_OK;
+  am_read_batch b{};
+  std::vector<uint64_t> key;
+};
+
+namespace {
+
+// the requests' vnode keys (part_key_base[part] + local key); an out-of-range request gets a
+// key past the vnode's, which the read reports as AM_ERR_INVALID
+int objects_keys(am_vnode *v, uint32_t n_parts, const uint64_t *base, const uint32_t *part, const am_read_batch *hb,
+                 std::vector<uint64_t> &key) {
+  if (!v || !base || !hb || (hb->n_reads && (!part || !hb->key))) return AM_ERR_INVALID;
+  if (base[n_parts] > v->n_keys) {
+    am_set_error("am_read_objects: partition key ranges exceed the vnode's keys");
+    return AM_ERR_INVALID;
+  }
+  key.resize(hb->n_reads);
+  for (uint64_t i = 0; i < hb->n_reads; ++i) {
+    const uint32_t p = part[i];
+    const bool ok = p < n_parts && base[p] <= base[p + 1] && hb->key[i] < base[p + 1] - base[p];
+    key[i] = ok ? base[p] + hb->key[i] : ~0ull;
+  }
+  return AM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int am_read_objects_host(am_vnode *v, uint32_t n_parts, const uint64_t *part_key_base, const uint32_t *part,
+                         const am_read_batch *hb, am_read_result *hr) {
+  std::vector<uint64_t> key;
+  if (int rc = objects_keys(v, n_parts, part_key_base, part, hb, key)) return rc;
+  am_read_batch b = *hb;
+  b.key = key.data();
+  return am_vnode_read_host(v, &b, nullptr, hr);
+}
+
+int am_read_objects_submit(am_vnode *v, uint32_t n_parts, const uint64_t *part_key_base, const uint32_t *part,
+                           const am_read_batch *hb, am_read_result *hr, am_ticket **out) {
+  if (!out) return AM_ERR_INVALID;
+  am_ticket *t = new am_ticket();
+  if (int rc = objects_keys(v, n_parts, part_key_base, part, hb, t->key)) {
+    delete t;
+    return rc;
+  }
+  t->b = *hb;
+  t->b.key = t->key.data();
+  t->th = std::thread([t, v, hr]() { t->rc = am_vnode_read_host(v, &t->b, nullptr, hr); });
+  *out = t;
+  return AM_OK;
+}
+
+int am_ticket_wait(am_ticket *t) {
+  if (!t) return AM_ERR_INVALID;
+  if (t->th.joinable()) t->th.join();
+  const int rc = t->rc;
+  delete t;
+  return rc;
 }
 
 }  // extern "C"

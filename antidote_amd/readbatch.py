@@ -5,67 +5,94 @@ clocksi_interactive_coord:execute_command(read_objects, Objects, ...)
 (src/clocksi_interactive_coord.erl:732-747) maps every {Key, Type} to its partition with
 log_utilities:get_key_partition/1 (src/log_utilities.erl:60-61) and sends one
 async_read_data_item per key; each read server then calls materializer_vnode:read/6 for
-that key (src/clocksi_readitem_server.erl:217-228, 272).  Here the same fan-out is grouped:
-the objects of one partition become ONE am_materialize batch against that partition's
-ops cache in HBM, and results come back in request order, as the coordinator's
-return_accumulator does.  Integer keys only (get_key_partition's integer branch,
-am_key_partition); every call runs the HIP library (no CPU path).
+that key (src/clocksi_readitem_server.erl:217-228, 272).  Here the partitions this GPU owns
+share one vnode (ops cache + snapshot cache in HBM) whose key space concatenates theirs, and a
+transaction's reads over all of them are ONE asynchronous C-ABI call
+(am_read_objects_submit / am_ticket_wait): internal_read/7 for every object in one batch,
+results in request order, as the coordinator's return_accumulator collects them.  Integer
+keys (get_key_partition's integer branch, am_key_partition); every call runs the HIP library
+(no CPU path).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from . import abi
-from .materializer import Materializer, Store
-from .oplog import HostLog, Op, Read
+from .materializer import Materializer, Vnode
+from .oplog import HostBatch, Op, Read
+
+
+class PendingRead:
+    """A submitted read_objects call (am_ticket); result() waits for it."""
+
+    def __init__(self, ticket, hb: HostBatch, keep):
+        self.ticket, self.hb, self.keep, self.rc = ticket, hb, keep, None
+
+    def result(self) -> list:
+        if self.rc is None:
+            self.rc = abi.lib().am_ticket_wait(self.ticket)
+            self.ticket = None
+        abi.check(self.rc, "am_read_objects")
+        return [self.hb.result(i) for i in range(self.hb.n)]
 
 
 class PartitionedReader:
-    """One node's partitions (vnodes), each with its own ops cache (am_store) on the GPU."""
+    """One node's partitions on one GPU: a vnode over the concatenated key spaces."""
 
     def __init__(self, mat: Materializer, n_partitions: int, n_dc: int,
                  objects: Dict[int, Tuple[int, Sequence[Op]]]):
-        """objects: Key -> (Type, committed ops oldest -> newest) -- the ops caches to load."""
+        """objects: Key -> (Type, committed ops oldest -> newest), inserted through
+        op_insert_gc/3 (am_vnode_insert_host: ids, write-triggered GC)."""
         self.mat, self.n_partitions, self.n_dc = mat, n_partitions, n_dc
         L = abi.lib()
         per_part: List[List[int]] = [[] for _ in range(n_partitions)]
         for key in sorted(objects):
             per_part[L.am_key_partition(key, n_partitions)].append(key)
         self.where: Dict[int, Tuple[int, int]] = {}
-        self.stores: List[Optional[Store]] = []
+        base = [0]
+        order: List[int] = []
         for p, keys in enumerate(per_part):
             for i, key in enumerate(keys):
                 self.where[key] = (p, i)
-            if keys:
-                log = HostLog(n_dc, [list(objects[k][1]) for k in keys], key_types=[objects[k][0] for k in keys])
-                self.stores.append(mat.store(log))
-            else:
-                self.stores.append(None)
+            order += keys
+            base.append(base[-1] + len(keys))
+        self.part_key_base = np.array(base, np.uint64)
+        self.vnode: Vnode = mat.vnode(n_dc, max(len(order), 1))
+        if order:
+            self.vnode.insert([list(objects[k][1]) for k in order], [objects[k][0] for k in order])
 
     def partition_of(self, key: int) -> int:
         return abi.lib().am_key_partition(key, self.n_partitions)
 
-    def read_objects(self, objects: Sequence[Tuple[int, int]], snapshot_time: Dict[int, int],
-                     txid: Optional[int] = None) -> list:
-        """read_objects for one transaction: [(Key, Type)] at one snapshot time ->
-        per object ('ok', Value, NewLastOp, LastOpCt, IsNewSS, Count, flags) or ('error', status),
-        in request order.  A key with no ops cache entry reads as an empty log (new())."""
-        groups: Dict[int, List[Tuple[int, int, int]]] = {}
-        out: list = [None] * len(objects)
-        for pos, (key, type_) in enumerate(objects):
+    def submit(self, objects: Sequence[Tuple[int, int]], snapshot_time: Dict[int, int],
+               txid: Optional[int] = None, set_capacity: int = 4096) -> PendingRead:
+        """read_objects for one transaction, asynchronously: [(Key, Type)] at one snapshot."""
+        parts = np.zeros(max(len(objects), 1), np.uint32)
+        reads = []
+        for i, (key, type_) in enumerate(objects):
             if key not in self.where:
                 raise KeyError(f"key {key} has no ops cache entry on this node")
             p, local = self.where[key]
-            groups.setdefault(p, []).append((pos, local, type_))
-        for p, items in groups.items():
-            reads = [Read(local, type_, dict(snapshot_time), txid) for _pos, local, type_ in items]
-            hb = self.mat.read_batch(self.stores[p], reads)
-            for j, (pos, _local, _t) in enumerate(items):
-                out[pos] = hb.result(j)
-        return out
+            parts[i] = p
+            reads.append(Read(local, type_, dict(snapshot_time), txid))
+        hb = HostBatch(self.n_dc, reads, [set_capacity] * len(reads))
+        b, r = hb.structs()
+        t = ctypes.c_void_p()
+        abi.check(self.mat.L.am_read_objects_submit(self.vnode.handle, self.n_partitions, self.part_key_base.ctypes.data,
+                                                    parts.ctypes.data, ctypes.byref(b), ctypes.byref(r),
+                                                    ctypes.byref(t)), "am_read_objects_submit")
+        return PendingRead(t, hb, (b, r, parts))
+
+    def read_objects(self, objects: Sequence[Tuple[int, int]], snapshot_time: Dict[int, int],
+                     txid: Optional[int] = None) -> list:
+        """Per object ('ok', Value, NewLastOp, LastOpCt, IsNewSS, Count, flags) or
+        ('error', status) -- AM_ERR_COLD_PATH when the read needs the log -- in request order."""
+        return self.submit(objects, snapshot_time, txid).result()
 
     def close(self):
-        for s in self.stores:
-            if s is not None:
-                s.close()
-        self.stores = []
+        if self.vnode is not None:
+            self.vnode.close()
+            self.vnode = None

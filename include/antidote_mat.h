@@ -359,6 +359,25 @@ int am_vnode_parts(am_vnode *v, am_store **st, am_snapcache **sc);
 /* the ops-cache tuple header of a key: {Length, ListLen} and OpCounter (element 3) */
 int am_vnode_key_info(am_vnode *v, uint64_t key, uint64_t *length, uint64_t *list_len, uint64_t *op_counter);
 
+/* ---- read_objects: one transaction's reads over a node's partitions, one call ----
+ * clocksi_interactive_coord's read_objects fan-out (src/clocksi_interactive_coord.erl:
+ * 732-747) sends one read per key to its partition's read server, which calls
+ * materializer_vnode:read/6 (src/clocksi_readitem_server.erl:217-228).  Here the partitions
+ * a GPU owns share one vnode whose key space concatenates theirs: partition p owns vnode
+ * keys [part_key_base[p], part_key_base[p+1]).  Request i reads partition part[i]'s local
+ * key host_batch->key[i]; every request of every partition is ONE internal_read/7 batch
+ * (snapshot cache, materialize/4, write-back), results in request order (repeated keys in
+ * request order).  A request outside its partition's range gets AM_ERR_INVALID.
+ * am_read_objects_submit returns at once; the read runs on a worker thread and
+ * am_ticket_wait returns its status (and frees the ticket).  Every buffer the batch and the
+ * result point to must stay valid until then. */
+typedef struct am_ticket am_ticket;
+int am_read_objects_host(am_vnode *v, uint32_t n_parts, const uint64_t *part_key_base, const uint32_t *part,
+                         const am_read_batch *host_batch, am_read_result *host_res);
+int am_read_objects_submit(am_vnode *v, uint32_t n_parts, const uint64_t *part_key_base, const uint32_t *part,
+                           const am_read_batch *host_batch, am_read_result *host_res, am_ticket **out);
+int am_ticket_wait(am_ticket *t);
+
 /* ---- op-cache ingestion + garbage collection ----
  * Builds a new store from `st` (st is unchanged; destroy it when no read uses it):
  *   1. prune_ops/2 (src/materializer_vnode.erl:565-604): for keys with prune_mask[k] != 0
