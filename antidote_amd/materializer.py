@@ -51,6 +51,9 @@ class Store:
             bufs.append(flags)
             mask = thr = pres = None
             if isinstance(prune, SnapshotCache):
+                if prune.n_keys != n_keys:  # thresholds are laid out [d * n_keys + k] per cache key
+                    raise abi.AmError(f"am_store_update: snapshot cache has {prune.n_keys} keys, "
+                                      f"the store {n_keys} (rc={abi.AM_ERR_INVALID})")
                 mask, thr, pres = (_DevBuf(self.mat, max(n_keys, 1)), _DevBuf(self.mat, max(n_keys, 1) * 8 * self.n_dc),
                                    _DevBuf(self.mat, max(n_keys, 1) * 4))
                 bufs += [mask, thr, pres]
@@ -215,7 +218,7 @@ class SnapshotCache:
     (src/materializer_vnode.erl:371-376) -- base from the cache, materialize/4, write-back."""
 
     def __init__(self, mat: "Materializer", store: "Store", n_keys: int):
-        self.mat, self.store = mat, store
+        self.mat, self.store, self.n_keys = mat, store, int(n_keys)
         self.handle = ctypes.c_void_p()
         abi.check(mat.L.am_snapcache_create(mat.ctx, store.n_dc, n_keys, ctypes.byref(self.handle)),
                   "am_snapcache_create")

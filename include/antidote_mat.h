@@ -334,7 +334,9 @@ int am_snapcache_get_value(am_ctx *ctx, const am_snapcache *cache, uint64_t key,
  * dict keeps its newest min(n, SNAPSHOT_MIN) entries and Thr = vectorclock:min (dict merge: a
  * DC present in any clock is kept) over them.  Device outputs: mask[n_keys] (1 = the key has
  * a threshold), thr_vc[n_dc][n_keys], thr_pres[n_keys] -- exactly the prune arguments of
- * am_store_update (so ops are only pruned below snapshots that stay cached). */
+ * am_store_update (so ops are only pruned below snapshots that stay cached).  n_keys is the
+ * cache's: hand the outputs only to am_store_update of a store with the same key count (the
+ * thr_vc stride; am_snapcache_read already requires it, Store.update checks it). */
 int am_snapcache_gc_threshold(am_ctx *ctx, am_snapcache *cache, uint8_t *mask, uint64_t *thr_vc,
                               uint32_t *thr_pres);
 
