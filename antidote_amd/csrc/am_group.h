@@ -169,6 +169,49 @@ __device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
   }
 }
 
+// the OPL packed-view ops [g, g + OPL) of a read's [off0, off1), entries x already loaded:
+// inclusion bits (is_op_in_snapshot/7), partials in ap.  Branch-free: x - thr saturates to 0
+// iff x <= thr, so one OR per op tests every DC; LastOpCt takes the included ops' entries
+// through max chains.  An escaped op (x[k][0] == AM_PK_ESC) only sets esc.
+template <int DMAX, int OPL, bool GENERAL>
+__device__ __forceinline__ uint32_t pk_tile(const ReadU<DMAX> &u, const PkRead<DMAX> &pk, const uint32_t (&x)[OPL][DMAX],
+                                            const uint64_t (&tx)[OPL], uint64_t g, uint64_t off0, uint64_t off1,
+                                            AccP<DMAX> &ap, bool &esc) {
+  uint32_t ib = 0, ev = 0;  // ev: evaluated (in range, in the packed view, a candidate)
+#pragma unroll
+  for (int k = 0; k < OPL; ++k) {
+    const uint64_t p = g + k;
+    const bool inr = p >= off0 && p < off1;
+    const bool e = x[k][0] == AM_PK_ESC;
+    esc |= inr && e;
+    uint32_t over = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(x[k][d], pk.thr[d]);
+    bool cand = inr && !e;
+    if (GENERAL) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
+      uint32_t cov = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) cov |= __builtin_elementwise_sub_sat(x[k][d], pk.cthr[d]);
+      const bool le = !pk.cnever && cov == 0;
+      cand = cand && (u.base_ignore || (u.has_txid && tx[k] == u.txid) || !le);
+    }
+    ib |= (uint32_t)(cand && !pk.never && over == 0) << k;
+    ev |= (uint32_t)cand << k;
+  }
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    uint32_t m = ap.mx[d];
+#pragma unroll
+    for (int k = 0; k < OPL; ++k) m = max(m, ((ib >> k) & 1u) ? x[k][d] : 0u);
+    ap.mx[d] = m;
+  }
+  ap.count += (uint32_t)__popc(ib);
+  const uint32_t ex = ev & ~ib;
+  if (ex) ap.min_excl = umin64(ap.min_excl, g + (uint64_t)__builtin_ctz(ex));
+  if (ev) ap.flags |= pk.miss;
+  return ib;
+}
+
 // the OPL ops [g, g + OPL) of a read's [off0, off1): inclusion bits (is_op_in_snapshot/7).
 // Packed view: u32 entries relative to the key's time base (am_wave.h pk_eval), partials in
 // ap; an escaped op (pk_vc[0] == AM_PK_ESC) is not evaluated here: esc is set and the
@@ -182,8 +225,6 @@ __device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, c
   uint64_t tx[OPL] = {};
   if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
   if (PACKED) {
-    // branch-free: x - thr saturates to 0 iff x <= thr, so one OR per op tests every DC;
-    // LastOpCt takes the included ops' entries through max chains
     uint32_t x[OPL][DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
@@ -192,38 +233,7 @@ __device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, c
 #pragma unroll
       for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
     }
-    uint32_t ev = 0;  // evaluated: in range, in the packed view, a candidate
-#pragma unroll
-    for (int k = 0; k < OPL; ++k) {
-      const uint64_t p = g + k;
-      const bool inr = p >= off0 && p < off1;
-      const bool e = x[k][0] == AM_PK_ESC;
-      esc |= inr && e;
-      uint32_t over = 0;
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(x[k][d], pk.thr[d]);
-      bool cand = inr && !e;
-      if (GENERAL) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
-        uint32_t cov = 0;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) cov |= __builtin_elementwise_sub_sat(x[k][d], pk.cthr[d]);
-        const bool le = !pk.cnever && cov == 0;
-        cand = cand && (u.base_ignore || (u.has_txid && tx[k] == u.txid) || !le);
-      }
-      ib |= (uint32_t)(cand && !pk.never && over == 0) << k;
-      ev |= (uint32_t)cand << k;
-    }
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) {
-      uint32_t m = ap.mx[d];
-#pragma unroll
-      for (int k = 0; k < OPL; ++k) m = max(m, ((ib >> k) & 1u) ? x[k][d] : 0u);
-      ap.mx[d] = m;
-    }
-    ap.count += (uint32_t)__popc(ib);
-    const uint32_t ex = ev & ~ib;
-    if (ex) ap.min_excl = umin64(ap.min_excl, g + (uint64_t)__builtin_ctz(ex));
-    if (ev) ap.flags |= pk.miss;
+    ib = pk_tile<DMAX, OPL, GENERAL>(u, pk, x, tx, g, off0, off1, ap, esc);
   } else {
     uint64_t ct[OPL], sv[OPL][DMAX];
     uint32_t sp[OPL];

@@ -95,6 +95,14 @@ enum { AM_GRP_ROW = 0, AM_GRP_WAVE = 1, AM_GRP_WG = 2 };
 bool am_group_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
 int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                     uint32_t type, am_retry next, int tier);
+// Lane tier (am_lanes.hip): one lane per short read of the PN counter, LWW register,
+// add-wins set and MV register, every accepted type in one launch.  accept = bit mask
+// (1 << am_type) of the types it may take; am_lane_accept() narrows a wish list to the types
+// the log and the outputs support (packed view; value columns; token-group view).  Reads
+// it does not take go to `next`; unknown keys / types and corrupted logs get their status.
+uint32_t am_lane_accept(const am_op_log *L, const am_read_result *R, uint32_t types);
+int am_launch_lanes(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                    am_retry next, uint32_t accept);
 // the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
                           uint32_t *key_ngrp);

@@ -1,0 +1,308 @@
+// am_lanes.hip -- materialize/4 for SHORT logs, one LANE per read, PN counter, LWW register,
+// add-wins set and MV register reads in ONE launch.
+//
+// Most of a partition's keys are short (the mixed C4 workload: 16 ops per key; C5: 95 % of
+// keys with <= 48 ops).  A 16-lane row per read (am_rows.hip) keeps only 4 reads of a wave in
+// flight, each lane holding one 4-byte entry per column, and pays a row reduction per read;
+// per-type launches over a type-mixed log also re-fetch the cache lines that neighbouring keys
+// of the other types share.  Here lane i of a wave owns read i of a 64-read batch outright:
+//   * the read's ops stream in OPL-op tiles (16-byte loads of the packed view, payload words
+//     with them for PN / LWW), the next tile in flight while one is evaluated
+//     (is_op_in_snapshot/7 on u32 entries, am_group.h pk_tile); inclusion bits in a u64;
+//   * PN: exact 128-bit sum; LWW: erlang:max on {Ts, Value} (am_wave.h PnVal / LwwVal);
+//   * AW / MV: the key's token-group records (am_group.h) set born / killed bits of at most
+//     64 groups in two u64 registers; survivors = born & ~killed, gathered in group order
+//     (already the reference's output order);
+//   * no cross-lane reduction: every output column leaves with one coalesced store per batch.
+// A read the kernel does not take (a longer log, more groups, an ungrouped key, base-snapshot
+// pairs, a bounded counter, a type outside `accept`) goes to `next`; reads with an unknown
+// key or type, or a corrupted ops cache (src/clocksi_materializer.erl:190-191), get their
+// status here.
+#include "am_group.h"
+
+using namespace amk;
+using namespace amk_grp;
+
+namespace {
+
+constexpr uint32_t LBITS = 64;  // inclusion bits of a lane read: ops [off0 & ~(OPL-1), off1)
+constexpr uint32_t LGRP = 64;   // groups of a lane set read (u64 born / killed)
+constexpr int LBLOCK = 256;
+template <int DMAX>
+constexpr int lopl() {
+  return DMAX <= 8 ? 4 : 2;
+}
+
+template <int DMAX, int OPL>
+struct LTile {
+  uint32_t x[OPL][DMAX];
+  uint64_t tx[OPL];
+  uint64_t v0[OPL], v1[OPL];
+};
+
+template <int DMAX, bool GENERAL>
+__global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                 am_retry next, uint32_t accept) {
+  constexpr int OPL = lopl<DMAX>();
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t nd = L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+  const uint64_t n = B.n_reads;
+  ReadU<DMAX> u{};
+  if (!GENERAL) read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
+
+  const uint64_t step = (uint64_t)gridDim.x * LBLOCK;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * LBLOCK + (threadIdx.x & ~(WAVE - 1)); b0 < nsel; b0 += step) {
+    const uint64_t i = b0 + lane;
+    uint64_t r = 0, key = 0, off0 = 0, off1 = 0, rk0 = 0, rk1 = 0;
+    uint32_t t = 0, G = 0;
+    int32_t st = AM_OK;
+    bool take = false, hand = false;
+    if (i < nsel) {
+      r = S.idx ? (uint64_t)S.idx[sel0 + i] : i;
+      key = B.key[r];
+      t = B.type[r];
+      if (key >= L.n_keys || t < AM_PN || t > AM_BCOUNTER) {
+        st = AM_ERR_INVALID;
+      } else {
+        off0 = L.key_off[key];
+        off1 = L.key_off[key + 1];
+        const uint32_t ktype = L.key_type[key];
+        const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;
+        if (off1 > off0 && (ktype != t || (kfl & AM_KEY_MIXED_TYPES))) st = AM_ERR_CORRUPTED_OPS_CACHE;
+      }
+      if (st == AM_OK) {
+        bool ok = ((accept >> t) & 1u) && off1 - (off0 & ~(uint64_t)(OPL - 1)) <= LBITS;
+        if (ok && (t == AM_AWSET || t == AM_MVREG)) {
+          G = L.key_ngrp[key];
+          rk0 = L.rec_key_off[key];
+          rk1 = L.rec_key_off[key + 1];
+          ok = G != AM_NGRP_NONE && G <= LGRP && !has_base_pairs(B, r);
+        }
+        take = ok;
+        hand = !ok;
+      } else {
+        R.status[r] = st;
+        R.flags[r] = 0;
+      }
+    }
+    const uint64_t hm = __ballot(hand);
+    if (hm) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(next.count, (uint32_t)__popcll(hm));
+      base = uniform_u32(base);
+      if (hand) next.list[base + (uint32_t)__popcll(hm & lt)] = (uint32_t)r;
+    }
+    if (!__ballot(take)) continue;
+
+    // ---- this lane's read ----
+    const bool scal = t == AM_PN || t == AM_LWW, setr = t == AM_AWSET || t == AM_MVREG;
+    if (GENERAL && take) read_inputs<DMAX, true, false>(L, nd, B, r, u);
+    PkRead<DMAX> pk;
+    pk_setup(u, nd, take ? L.key_tbase[key] : 0, pk);
+    const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
+    const uint32_t sh = (uint32_t)(off0 - t0);
+    // the first record vector of a set read is in flight with the ops
+    const uint64_t q0 = rk0 & ~3ull;
+    u32x4 rv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (take && setr && rk1 > rk0) rv = *(const u32x4 *)(L.rec_g + q0);
+
+    auto load = [&](LTile<DMAX, OPL> &T, uint64_t g) {
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        uint32_t q[OPL] = {};
+        if (d < (int)nd) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+        for (int k = 0; k < OPL; ++k) T.x[k][d] = q[k];
+      }
+#pragma unroll
+      for (int k = 0; k < OPL; ++k) T.tx[k] = 0, T.v0[k] = 0, T.v1[k] = 0;
+      if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, T.tx);
+      if (scal) ld_n64<OPL>(L.p0 + g, T.v0);
+      if (t == AM_LWW) ld_n64<OPL>(L.p1 + g, T.v1);
+    };
+    AccP<DMAX> ap;
+    Acc<DMAX> a;
+    ap.reset();
+    a.reset();
+    PnVal pv;
+    LwwVal lv;
+    pv.reset();
+    lv.reset();
+    bool esc = false;
+    uint64_t incl = 0;
+    {
+      LTile<DMAX, OPL> cur, nxt;
+      if (take) load(cur, t0);
+      for (uint64_t g = t0; take && g < off1; g += OPL) {
+        if (g + OPL < off1) load(nxt, g + OPL);
+        const uint32_t ib = pk_tile<DMAX, OPL, GENERAL>(u, pk, cur.x, cur.tx, g, off0, off1, ap, esc);
+        incl |= (uint64_t)ib << (g - t0);
+        if (scal) {
+#pragma unroll
+          for (int k = 0; k < OPL; ++k)
+            if ((ib >> k) & 1u) {
+              if (t == AM_PN) pv.add(cur.v0[k], 0);
+              else lv.add(cur.v0[k], cur.v1[k]);
+            }
+        }
+        cur = nxt;
+      }
+    }
+    if (esc) {  // rare: ops outside the packed view, from the full columns
+      for (uint64_t p = off0; p < off1; ++p) {
+        if (L.pk_vc[p] != AM_PK_ESC) continue;
+        uint64_t sv[DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+        const uint32_t meta = L.op_meta[p];
+        const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
+        const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
+        if (!eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], sv, sp, txm, p, a)) continue;
+        if (scal) {
+          if (t == AM_PN) pv.add(L.p0[p], 0);
+          else lv.add(L.p0[p], L.p1[p]);
+        } else if (!(meta & AM_META_BAD)) {
+          incl |= 1ull << (p - t0);
+        }
+      }
+    }
+    pk_fold(ap, pk.K, u.allmask, a);
+    int32_t status = (a.flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+
+    // ---- set reads: records of included ops -> born / killed groups -> survivors ----
+    uint32_t ns = 0;
+    if (take && setr) {
+      uint64_t born = 0, killed = 0;
+      for (uint64_t q = q0; q < rk1; q += 4) {
+        const u32x4 cv = rv;
+        if (q + 4 < rk1) rv = *(const u32x4 *)(L.rec_g + q + 4);
+        const uint32_t xs[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t x = xs[k];
+          if (q + k < rk0 || q + k >= rk1 || x == 0xFFFFFFFFu) continue;
+          if (!((incl >> (AM_REC_OP(x) + sh)) & 1ull)) continue;
+          const uint64_t bit = 1ull << AM_REC_GRP(x);
+          if (x & AM_REC_KILL) killed |= bit;
+          else born |= bit;
+        }
+      }
+      if (status == AM_OK) {
+        uint64_t alive = born & ~killed;
+        ns = (uint32_t)__popcll(alive);
+        const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
+        if (ns > ocap) {
+          status = AM_ERR_CAPACITY;
+        } else {
+          for (uint32_t o = 0; alive; ++o, alive &= alive - 1) {
+            const uint32_t g = (uint32_t)__builtin_ctzll(alive);
+            const u64x2 ab = *(const u64x2 *)(L.grp + 2 * (rk0 + g));
+            R.value.set_a[ooff + o] = ab.x;
+            R.value.set_b[ooff + o] = ab.y;
+          }
+        }
+      }
+    }
+
+    // ---- outputs ----
+    if (take) {
+      uint64_t v0 = 0, v1 = 0;
+      uint32_t vflag = 0;
+      if (t == AM_PN) {
+        int64_t hi = pv.hi;
+        uint64_t lo = pv.lo;
+        const int64_t bv = (GENERAL && B.base.v0) ? B.base.v0[r] : 0;
+        add128(hi, lo, bv < 0 ? -1 : 0, (uint64_t)bv);
+        if (status == AM_OK && hi != ((int64_t)lo < 0 ? -1 : 0)) status = AM_ERR_OVERFLOW;
+        v0 = lo;
+      } else if (t == AM_LWW) {
+        uint64_t bts = 0, bval = 0;
+        uint32_t bbin = 1;  // new() = {0, <<>>}
+        if (GENERAL && B.base.v0) {
+          bts = (uint64_t)B.base.v0[r];
+          bval = B.base.v1 ? B.base.v1[r] : 0;
+          bbin = B.base.vflag ? B.base.vflag[r] : 0;
+        }
+        const bool win = lv.has && (lv.ts > bts || (lv.ts == bts && !bbin && lv.val > bval));
+        v0 = win ? lv.ts : bts;
+        v1 = win ? lv.val : bval;
+        vflag = win ? 0 : bbin;
+      }
+      R.status[r] = status;
+      R.flags[r] = (uint8_t)(a.flags & 0xFFu);
+      if (status == AM_OK) {
+        R.new_last_op[r] = new_last_op(L, key, off0, off1, a.min_excl);
+        const bool ign = u.base_ignore && a.count == 0;
+        const uint32_t opres = ign ? 0u : (a.pres | u.cpres);
+        R.last_ct_ignore[r] = ign ? 1 : 0;
+        R.last_ct_pres[r] = opres;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          if (d >= (int)nd) continue;
+          const uint64_t m = a.mx[d] > u.C0[d] ? a.mx[d] : u.C0[d];
+          R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? m : 0;
+        }
+        R.is_new_ss[r] = a.count > 0;
+        R.count[r] = a.count;
+        if (scal) R.value.v0[r] = (int64_t)v0;
+        if (t == AM_LWW) {
+          R.value.v1[r] = v1;
+          R.value.vflag[r] = (uint8_t)vflag;
+        }
+        if (setr) R.value.set_len[r] = ns;
+      }
+    }
+  }
+}
+
+template <int D, bool GENERAL>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
+             uint32_t accept) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane<D, GENERAL>, LBLOCK, 0) != hipSuccess || occ < 1)
+      occ = 2;
+  }
+  uint64_t blocks = (B->n_reads + LBLOCK - 1) / LBLOCK, cap = (uint64_t)ctx->n_cu * occ;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return AM_OK;
+  hipLaunchKernelGGL((k_lane<D, GENERAL>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next,
+                     accept);
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
+template <bool GENERAL>
+int launch_g(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
+             uint32_t accept) {
+  const uint32_t nd = L->n_dc;
+  if (nd <= 1) return launch_d<1, GENERAL>(ctx, L, B, R, S, next, accept);
+  if (nd <= 2) return launch_d<2, GENERAL>(ctx, L, B, R, S, next, accept);
+  if (nd <= 3) return launch_d<3, GENERAL>(ctx, L, B, R, S, next, accept);
+  if (nd <= 4) return launch_d<4, GENERAL>(ctx, L, B, R, S, next, accept);
+  if (nd <= 8) return launch_d<8, GENERAL>(ctx, L, B, R, S, next, accept);
+  if (nd <= 16) return launch_d<16, GENERAL>(ctx, L, B, R, S, next, accept);
+  return launch_d<32, GENERAL>(ctx, L, B, R, S, next, accept);
+}
+
+}  // namespace
+
+uint32_t am_lane_accept(const am_op_log *L, const am_read_result *R, uint32_t types) {
+  if (!am_log_packed(L)) return 0;
+  uint32_t acc = 0;
+  if ((types & (1u << AM_PN)) && R->value.v0) acc |= 1u << AM_PN;
+  if ((types & (1u << AM_LWW)) && R->value.v0 && R->value.v1 && R->value.vflag) acc |= 1u << AM_LWW;
+  if ((types & (1u << AM_AWSET)) && am_group_applies(L, R, AM_AWSET)) acc |= 1u << AM_AWSET;
+  if ((types & (1u << AM_MVREG)) && am_group_applies(L, R, AM_MVREG)) acc |= 1u << AM_MVREG;
+  return acc;
+}
+
+int am_launch_lanes(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                    am_retry next, uint32_t accept) {
+  return am_batch_general(L, B) ? launch_g<true>(ctx, L, B, R, S, next, accept)
+                                : launch_g<false>(ctx, L, B, R, S, next, accept);
+}

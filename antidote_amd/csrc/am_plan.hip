@@ -40,14 +40,23 @@ __device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read
   return t - 1;
 }
 
-__global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, uint32_t *cnt) {
+// the planner's input: the whole batch, or a selection (the lane tier's hand-off list)
+__device__ __forceinline__ uint64_t in_count(const am_read_batch &B, am_sel in) {
+  return in.idx ? (uint64_t)(uniform_u32(in.range[1]) - uniform_u32(in.range[0])) : B.n_reads;
+}
+__device__ __forceinline__ uint64_t in_read(am_sel in, uint64_t i) {
+  return in.idx ? (uint64_t)in.idx[in.range[0] + i] : i;
+}
+
+__global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
+                                                   uint32_t *cnt) {
   __shared__ uint32_t c[NCLS];
   if (threadIdx.x < NCLS) c[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
+  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
-    const uint64_t r = base + (uint64_t)j * PB + threadIdx.x;
-    if (r < B.n_reads) atomicAdd(&c[read_class(L, B, R, r, true)], 1u);
+    const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
+    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), true)], 1u);
   }
   __syncthreads();
   if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = c[threadIdx.x];
@@ -90,16 +99,17 @@ __global__ void __launch_bounds__(1024) k_plan_scan(uint32_t *cnt, uint32_t n_bl
   }
 }
 
-__global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch B, am_read_result R,
+__global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
                                                      const uint32_t *off, uint32_t *idx) {
   __shared__ uint32_t run[NCLS];
   __shared__ uint32_t wcnt[PB / WAVE][NCLS];
   const uint32_t tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   if (tid < NCLS) run[tid] = off[(uint64_t)blockIdx.x * NCLS + tid];
-  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
+  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
-    const uint64_t r = base + (uint64_t)j * PB + tid;
-    const uint32_t c = r < B.n_reads ? read_class(L, B, R, r, false) : NCLS;
+    const uint64_t i = base + (uint64_t)j * PB + tid;
+    const uint64_t r = i < nin ? in_read(in, i) : 0;
+    const uint32_t c = i < nin ? read_class(L, B, R, r, false) : NCLS;
     uint32_t rank = 0;
     for (uint32_t k = 0; k < NCLS; ++k) {
       const uint64_t m = __ballot(c == k);
@@ -144,7 +154,7 @@ int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
 //   bounded counter: row tier -> (hand-off list) k_sets -> (retry list) big-read tier
 // rows_buf / grp_buf (two lists): [0] = 0, [1] = hand-off count, list at +64.
 int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
-             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf) {
+             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf, bool lanes_done) {
   am_retry retry;
   retry.count = retry_buf;
   retry.list = retry_buf + 1;
@@ -162,15 +172,18 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     cur.idx = C.list;
     cur.range = rows_buf;
   } else if (grp_buf && am_group_applies(L, R, type)) {
-    // row -> wave -> workgroup kernels; each hands what it does not take to the next
+    // lane (or, off the packed view, row) -> wave -> workgroup kernels; each hands what it
+    // does not take to the next.  The lane tier already ran over a mixed batch.
     uint32_t *bufs[3] = {rows_buf, grp_buf, grp_buf + (B->n_reads + 64)};
     for (int k = 0; k < 3; ++k) AM_HIP(hipMemsetAsync(bufs[k], 0, 2 * sizeof(uint32_t), ctx->stream));
+    const uint32_t lanes = lanes_done ? 0u : am_lane_accept(L, R, 1u << type);
     const int tiers[3] = {AM_GRP_ROW, AM_GRP_WAVE, AM_GRP_WG};
-    for (int k = 0; k < 3; ++k) {
+    for (int k = lanes_done ? 1 : 0; k < 3; ++k) {
       am_retry nx;
       nx.count = bufs[k] + 1;
       nx.list = bufs[k] + 64;
-      rc = am_launch_group(ctx, L, B, R, cur, type, nx, tiers[k]);
+      rc = (k == 0 && lanes) ? am_launch_lanes(ctx, L, B, R, cur, nx, lanes)
+                             : am_launch_group(ctx, L, B, R, cur, type, nx, tiers[k]);
       if (rc) return rc;
       cur.idx = nx.list;
       cur.range = bufs[k];
@@ -216,14 +229,32 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     void *scr = nullptr;
     int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &scr);
     if (rc) return rc;
-    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr, (uint32_t *)grp_scr);
+    return run_sets(ctx, L, B, R, all, B->type_hint, (uint32_t *)scr, (uint32_t *)rows_scr, (uint32_t *)grp_scr,
+                    false);
   }
   if (B->type_hint != 0) {
     am_set_error("type_hint %u not supported", B->type_hint);
     return AM_ERR_UNSUPPORTED;
   }
 
-  // ---- mixed batch: partition by class on the device ----
+  // ---- mixed batch: the lane tier takes the short reads of every type it can in one
+  //      launch; the planner partitions the rest by class on the device ----
+  const uint32_t lanes = am_lane_accept(L, R, (1u << AM_PN) | (1u << AM_LWW) | (1u << AM_AWSET) | (1u << AM_MVREG));
+  am_sel in{};
+  if (lanes) {
+    void *lscr = nullptr;
+    int rc = am_ctx_scratch(ctx, AM_SCR_SPARE, (n + 64) * sizeof(uint32_t), &lscr);
+    if (rc) return rc;
+    uint32_t *lbuf = (uint32_t *)lscr;  // [0] = 0, [1] = hand-off count, list at +64
+    AM_HIP(hipMemsetAsync(lbuf, 0, 2 * sizeof(uint32_t), ctx->stream));
+    am_retry nx;
+    nx.count = lbuf + 1;
+    nx.list = lbuf + 64;
+    rc = am_launch_lanes(ctx, L, B, R, all, nx, lanes);
+    if (rc) return rc;
+    in.idx = nx.list;
+    in.range = lbuf;
+  }
   const uint64_t n_blk = (n + PCHUNK - 1) / PCHUNK;
   // scratch: [retry count + list: n+1][range: 2*NCLS][cnt: n_blk*NCLS][idx: n]
   const size_t words = (n + 64) + 2 * NCLS + n_blk * NCLS + n + 64;
@@ -234,11 +265,11 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   uint32_t *range = retry_buf + n + 64;
   uint32_t *cnt = range + 2 * NCLS;
   uint32_t *idx = cnt + n_blk * NCLS;
-  hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, cnt);
+  hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt);
   AM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, (uint32_t)n_blk, range);
   AM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, cnt, idx);
+  hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, idx);
   AM_HIP(hipGetLastError());
   for (uint32_t t = AM_PN; t <= AM_BCOUNTER; ++t) {
     am_sel S;
@@ -247,7 +278,8 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     if (t == AM_PN || t == AM_LWW)
       rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
     else
-      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr, (uint32_t *)grp_scr);
+      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr, (uint32_t *)grp_scr,
+                    ((lanes >> t) & 1u) != 0);
     if (rc) return rc;
   }
   return AM_OK;
