@@ -132,34 +132,27 @@ __device__ __forceinline__ void read_inputs(const am_op_log &L, uint32_t nd, con
   u.txid = u.has_txid ? u64(B.txid[r]) : 0;
 }
 
-// N consecutive elements per lane (N = 1, 2, 4; 16-byte loads at most)
+// N consecutive elements per lane (N = 1, 2 or a multiple of 4 / 2; 16-byte loads)
 template <int N>
 __device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
   if constexpr (N == 1) {
     o[0] = *p;
-  } else if constexpr (N == 8) {
+  } else {
 #pragma unroll
-    for (int i = 0; i < 8; i += 2) {
+    for (int i = 0; i < N; i += 2) {
       const u64x2 a = *(const u64x2 *)(p + i);
       o[i] = a.x, o[i + 1] = a.y;
-    }
-  } else {
-    const u64x2 a = *(const u64x2 *)p;
-    o[0] = a.x, o[1] = a.y;
-    if constexpr (N == 4) {
-      const u64x2 b = *(const u64x2 *)(p + 2);
-      o[2] = b.x, o[3] = b.y;
     }
   }
 }
 template <int N>
 __device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
-  if constexpr (N == 8) {
-    const u32x4 a = *(const u32x4 *)p, b = *(const u32x4 *)(p + 4);
-    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = b.x, o[5] = b.y, o[6] = b.z, o[7] = b.w;
-  } else if constexpr (N == 4) {
-    const u32x4 a = *(const u32x4 *)p;
-    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w;
+  if constexpr (N >= 4) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      const u32x4 a = *(const u32x4 *)(p + i);
+      o[i] = a.x, o[i + 1] = a.y, o[i + 2] = a.z, o[i + 3] = a.w;
+    }
   } else if constexpr (N == 2) {
     typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
     const u32x2_t a = *(const u32x2_t *)p;

@@ -7,10 +7,12 @@
 // am_big.hip: set reads the group tier does not take), so a mixed batch is split on the
 // device, never on the host:
 //   k_plan_count    per 1024-read block: class histogram (class = kernel the read needs;
-//                   reads with an unknown type or key get their status here)
-//   k_plan_scan     one workgroup: per-class block offsets and the [begin, end) range of
-//                   every class in the index array
-//   k_plan_scatter  stable partition of the read indices by class (wave ballots)
+//                   reads with an unknown type or key get their status here); the block
+//                   claims its slice of every class with one atomicAdd per class
+//   k_plan_scatter  partition of the read indices by class (wave ballots; blocks keep their
+//                   reads in order, the order of the blocks inside a class is the claim
+//                   order -- every read writes only its own outputs, so results do not
+//                   depend on it) and the [begin, end) range of every class
 // and each type kernel then runs over its class range (am_sel).  The ranges stay in
 // device memory: kernels are launched with a resident-capacity grid and read their
 // count at start, so the planner adds no host round trip.
@@ -49,7 +51,7 @@ __device__ __forceinline__ uint64_t in_read(am_sel in, uint64_t i) {
 }
 
 __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
-                                                   uint32_t *cnt) {
+                                                   uint32_t *cnt, uint32_t *tot) {
   __shared__ uint32_t c[NCLS];
   if (threadIdx.x < NCLS) c[threadIdx.x] = 0;
   __syncthreads();
@@ -59,52 +61,21 @@ __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B,
     if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), true)], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = c[threadIdx.x];
-}
-
-// one workgroup of 1024: cnt[blk][cls] -> exclusive offsets (class-major), range[2*cls]
-__global__ void __launch_bounds__(1024) k_plan_scan(uint32_t *cnt, uint32_t n_blk, uint32_t *range) {
-  __shared__ uint32_t part[1024];
-  __shared__ uint32_t total[NCLS];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t per = (n_blk + 1023) / 1024;
-  const uint32_t b0 = tid * per, b1 = b0 + per < n_blk ? b0 + per : n_blk;
-  uint32_t start = 0;
-  for (int c = 0; c < NCLS; ++c) {
-    uint32_t s = 0;
-    for (uint32_t b = b0; b < b1; ++b) s += cnt[(uint64_t)b * NCLS + c];
-    part[tid] = s;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 partials
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-      const uint32_t v = tid >= o ? part[tid - o] : 0u;
-      __syncthreads();
-      part[tid] += v;
-      __syncthreads();
-    }
-    uint32_t run = start + part[tid] - s;  // exclusive prefix of this thread's segment
-    for (uint32_t b = b0; b < b1; ++b) {
-      const uint32_t x = cnt[(uint64_t)b * NCLS + c];
-      cnt[(uint64_t)b * NCLS + c] = run;
-      run += x;
-    }
-    if (tid == 1023) total[c] = part[1023];
-    __syncthreads();
-    if (tid == 0) {
-      range[2 * c] = start;
-      range[2 * c + 1] = start + total[c];
-    }
-    start += total[c];
-    __syncthreads();
-  }
+  if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = atomicAdd(&tot[threadIdx.x], c[threadIdx.x]);
 }
 
 __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
-                                                     const uint32_t *off, uint32_t *idx) {
+                                                     const uint32_t *off, const uint32_t *tot, uint32_t *range,
+                                                     uint32_t *idx) {
   __shared__ uint32_t run[NCLS];
   __shared__ uint32_t wcnt[PB / WAVE][NCLS];
   const uint32_t tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
-  if (tid < NCLS) run[tid] = off[(uint64_t)blockIdx.x * NCLS + tid];
+  if (tid < NCLS) {  // class start = the totals of the classes before it
+    uint32_t start = 0;
+    for (uint32_t k = 0; k < tid; ++k) start += tot[k];
+    run[tid] = start + off[(uint64_t)blockIdx.x * NCLS + tid];
+    if (blockIdx.x == 0) range[2 * tid] = start, range[2 * tid + 1] = start + tot[tid];
+  }
   const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = base + (uint64_t)j * PB + tid;
@@ -241,6 +212,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   //      launch; the planner partitions the rest by class on the device ----
   const uint32_t lanes = am_lane_accept(L, R, (1u << AM_PN) | (1u << AM_LWW) | (1u << AM_AWSET) | (1u << AM_MVREG));
   am_sel in{};
+  uint64_t n_in = n;  // reads the planner partitions
   if (lanes) {
     void *lscr = nullptr;
     int rc = am_ctx_scratch(ctx, AM_SCR_SPARE, (n + 64) * sizeof(uint32_t), &lscr);
@@ -252,24 +224,32 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     nx.list = lbuf + 64;
     rc = am_launch_lanes(ctx, L, B, R, all, nx, lanes);
     if (rc) return rc;
+    // one counter readback: a batch of short reads (the common case) ends here instead of
+    // launching the planner and every class's kernels over empty selections
+    uint64_t hc = 0;
+    rc = am_ctx_fetch(ctx, nx.count, 1, &hc);
+    if (rc) return rc;
+    n_in = (uint32_t)hc;
+    if (n_in == 0) return AM_OK;
     in.idx = nx.list;
     in.range = lbuf;
   }
-  const uint64_t n_blk = (n + PCHUNK - 1) / PCHUNK;
-  // scratch: [retry count + list: n+1][range: 2*NCLS][cnt: n_blk*NCLS][idx: n]
-  const size_t words = (n + 64) + 2 * NCLS + n_blk * NCLS + n + 64;
+  const uint64_t n_blk = (n_in + PCHUNK - 1) / PCHUNK;
+  // scratch: [retry count + list: n+1][range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
+  const size_t words = (n + 64) + 3 * NCLS + n_blk * NCLS + n + 64;
   void *scr = nullptr;
   int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, words * sizeof(uint32_t), &scr);
   if (rc) return rc;
   uint32_t *retry_buf = (uint32_t *)scr;
   uint32_t *range = retry_buf + n + 64;
-  uint32_t *cnt = range + 2 * NCLS;
+  uint32_t *tot = range + 2 * NCLS;
+  uint32_t *cnt = tot + NCLS;
   uint32_t *idx = cnt + n_blk * NCLS;
-  hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt);
+  AM_HIP(hipMemsetAsync(tot, 0, NCLS * sizeof(uint32_t), ctx->stream));
+  hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, tot);
   AM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, (uint32_t)n_blk, range);
-  AM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, idx);
+  hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, tot, range,
+                     idx);
   AM_HIP(hipGetLastError());
   for (uint32_t t = AM_PN; t <= AM_BCOUNTER; ++t) {
     am_sel S;

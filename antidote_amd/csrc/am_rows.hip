@@ -13,8 +13,13 @@
 //
 // Types:
 //   PN counter / LWW register  commutative reductions in registers (am_wave.h)
-//   bounded counter            included (slot, amount) pairs in the row's LDS list; lane
-//                              s owns slots s, s+16, ... and sums its slots exactly
+//   bounded counter            n_dc <= 16: every included amount goes into the row's LDS
+//                              slot array with one 64-bit LDS atomic (exact: a row read has
+//                              <= 48 entries, each below 2^56 -- a larger amount defers the
+//                              read to the workgroup tier), then lane s writes slots s,
+//                              s+16, ... with the base added in 128 bits; n_dc > 16: the
+//                              (slot, amount) pairs go to an LDS list that each lane scans
+//                              for its slots
 // (short add-wins-set / MV-register reads have their own row kernel, am_group.hip).
 // A read longer than the short limit, or whose entries do not fit the row's LDS list, is
 // handed to the workgroup tier (k_stream for PN/LWW skips it on its own; the bounded
@@ -30,10 +35,16 @@ constexpr int WPB = BLOCK / WAVE;
 constexpr int G = 16;
 constexpr uint32_t RK = 64;  // bounded counter: (slot, amount) entries per row
 
+template <int DMAX>
 struct RowSmem {
-  uint64_t ka[RK];  // amount
-  int32_t kp[RK];   // slot
-  uint32_t ctr[4];  // [0] entries [2] overflow of a slot sum [3] list overflow
+  static constexpr bool SLOTS = DMAX <= 16;                            // slot-array mode
+  static constexpr uint32_t NS = SLOTS ? DMAX * DMAX + DMAX : 1;      // P then D slots
+  static constexpr uint32_t NL = SLOTS ? 1 : RK;                      // list mode entries
+  uint64_t acc[NS];        // slot sums (slot-array mode)
+  uint32_t pres[(NS + 31) / 32];
+  uint64_t ka[NL];         // amount (list mode)
+  int32_t kp[NL];          // slot (list mode)
+  uint32_t ctr[4];         // [0] entries [2] overflow of a slot sum [3] list overflow / big amount
 };
 
 template <int TYPE>
@@ -61,7 +72,8 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
   constexpr bool LDS = BC;
   using V = typename RowVal<TYPE>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  RowSmem *rs = LDS ? ((RowSmem *)smem_raw) + (threadIdx.x / G) : nullptr;
+  using RS = RowSmem<DMAX>;
+  RS *rs = LDS ? ((RS *)smem_raw) + (threadIdx.x / G) : nullptr;
 
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint32_t row = lane / G, sl = lane % G;
@@ -197,6 +209,10 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         if (PACKED) pk_setup(u, nd, L.key_tbase[keyj], pk);
         if (LDS) {
           if (sl == 0) rs->ctr[0] = 0, rs->ctr[1] = 0, rs->ctr[2] = 0, rs->ctr[3] = 0;
+          if (RS::SLOTS) {
+            for (uint32_t i = sl; i < nslot; i += G) rs->acc[i] = 0;
+            for (uint32_t i = sl; i < (nslot + 31) / 32; i += G) rs->pres[i] = 0;
+          }
           wave_sync();
         }
       };
@@ -270,9 +286,19 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
               if (kind <= AM_BC_TRANSFER && from < nd && to < nd) {
                 const uint32_t slot =
                     kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
-                const uint32_t e = atomicAdd(&rs->ctr[0], 1u);
-                if (e < RK) rs->ka[e] = cur.p0, rs->kp[e] = (int32_t)slot;
-                else rs->ctr[3] = 1;
+                if (RS::SLOTS) {
+                  const int64_t x = (int64_t)cur.p0;
+                  if (x >= (1ll << 56) || x < -(1ll << 56)) {
+                    rs->ctr[3] = 1;  // exactness of the 64-bit sums not guaranteed: defer
+                  } else {
+                    atomicAdd((unsigned long long *)&rs->acc[slot], (unsigned long long)cur.p0);
+                    atomicOr(&rs->pres[slot >> 5], 1u << (slot & 31));
+                  }
+                } else {
+                  const uint32_t e = atomicAdd(&rs->ctr[0], 1u);
+                  if (e < RK) rs->ka[e] = cur.p0, rs->kp[e] = (int32_t)slot;
+                  else rs->ctr[3] = 1;
+                }
               } else {
                 a.flags |= FLAG_BAD;
               }
@@ -326,7 +352,43 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
               vflag = win ? 0 : bbin;
             } else if constexpr (BC) {
               if (status == AM_OK && rs->ctr[3]) defer = true;
-              if (status == AM_OK && !defer) {
+              if (RS::SLOTS && status == AM_OK && !defer) {
+                // |row sum| < 48 * 2^56: exact in int64; the base is added in 128 bits
+                auto total = [&](uint32_t i, int64_t &hi, uint64_t &lo, uint32_t &pr) {
+                  uint32_t bp = 0;
+                  const int64_t bv = GENERAL ? bc_base(B, rj, np, nd, i, bp) : 0;
+                  const int64_t x = (int64_t)rs->acc[i];
+                  hi = bv < 0 ? -1 : 0, lo = (uint64_t)bv;
+                  add128(hi, lo, x < 0 ? -1 : 0, (uint64_t)x);
+                  pr = bp | ((rs->pres[i >> 5] >> (i & 31)) & 1u);
+                };
+                uint32_t ovf = 0;
+                if (GENERAL && (B.base.bc_p || B.base.bc_d))
+                  for (uint32_t i = sl; i < nslot; i += G) {
+                    int64_t hi;
+                    uint64_t lo;
+                    uint32_t pr;
+                    total(i, hi, lo, pr);
+                    ovf |= hi != ((int64_t)lo < 0 ? -1 : 0) ? 1u : 0u;
+                  }
+                if (row_or_u32(ovf)) {
+                  status = AM_ERR_OVERFLOW;
+                } else {
+                  for (uint32_t i = sl; i < nslot; i += G) {
+                    int64_t hi;
+                    uint64_t lo;
+                    uint32_t pr;
+                    total(i, hi, lo, pr);
+                    if (i < np) {
+                      R.value.bc_p[rj * np + i] = (int64_t)lo;
+                      R.value.bc_p_pres[rj * np + i] = pr ? 1 : 0;
+                    } else {
+                      R.value.bc_d[rj * nd + (i - np)] = (int64_t)lo;
+                      R.value.bc_d_pres[rj * nd + (i - np)] = pr ? 1 : 0;
+                    }
+                  }
+                }
+              } else if (status == AM_OK && !defer) {
                 const uint32_t ne = rs->ctr[0];
                 const uint32_t ne4 = (ne + 3) & ~3u;
                 if (sl < ne4 - ne) rs->kp[ne + sl] = -1;  // pad the slot list to whole int4 loads
@@ -462,7 +524,7 @@ template <int D, int TYPE, bool GENERAL, bool PACKED>
 int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
              const am_rows_cfg &C) {
   constexpr bool LDS = TYPE == AM_BCOUNTER;
-  const size_t smem = LDS ? sizeof(RowSmem) * (BLOCK / G) : 0;
+  const size_t smem = LDS ? sizeof(RowSmem<D>) * (BLOCK / G) : 0;
   static int occ = 0;
   if (occ == 0) {
     int nb = 0;

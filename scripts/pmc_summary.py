@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
         for r in csv.DictReader(open(f)):
             vals[r["Kernel_Name"][:70]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in vals.items():
-    if not any("grp" in k or "stream" in k or "rows" in k or "sets" in k or "big" in k for _ in [0]):
+    if not any(s in k for s in ("grp", "stream", "rows", "sets", "big", "lane", "plan")):
         continue
     print(k)
     for c, v in sorted(cs.items()):
