@@ -210,7 +210,7 @@ struct ChunkSink {
   }
 };
 
-template <int DMAX, int TYPE>
+template <int DMAX, int TYPE, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
                                                      const BigRead *br, BigAcc *accs, BigRec G, BigSlots SL,
                                                      uint64_t n_chunks) {
@@ -261,34 +261,48 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
 
     Acc<DMAX> a;
     a.reset();
+    AccP<DMAX> ap;
+    ap.reset();
+    PkRead<DMAX> pk;
+    if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[r])]), pk);
     const uint64_t g = lo + (uint64_t)tid * OPL;
     if (g < hi) {
       const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
-      const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
-      const uint64_t ct[OPL] = {c01.x, c01.y, c23.x, c23.y};
-      uint64_t sv[OPL][DMAX];
+      uint32_t ib = 0;
+      if constexpr (PACKED) {
+        ib = incl4<DMAX, true>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
+      } else {
+        const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
+        const uint64_t ct[OPL] = {c01.x, c01.y, c23.x, c23.y};
+        uint64_t sv[OPL][DMAX];
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        if (d < (int)nd) {
-          const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
-          const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
-          sv[0][d] = s01.x, sv[1][d] = s01.y, sv[2][d] = s23.x, sv[3][d] = s23.y;
-        } else {
-          sv[0][d] = sv[1][d] = sv[2][d] = sv[3][d] = 0;
+        for (int d = 0; d < DMAX; ++d) {
+          if (d < (int)nd) {
+            const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
+            const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
+            sv[0][d] = s01.x, sv[1][d] = s01.y, sv[2][d] = s23.x, sv[3][d] = s23.y;
+          } else {
+            sv[0][d] = sv[1][d] = sv[2][d] = sv[3][d] = 0;
+          }
         }
-      }
-      uint32_t sp[OPL] = {u.allmask, u.allmask, u.allmask, u.allmask};
-      if (L.snap_pres) {
-        const u32x4 q = *(const u32x4 *)(L.snap_pres + g);
-        sp[0] = q.x, sp[1] = q.y, sp[2] = q.z, sp[3] = q.w;
+        uint32_t sp[OPL] = {u.allmask, u.allmask, u.allmask, u.allmask};
+        if (L.snap_pres) {
+          const u32x4 q = *(const u32x4 *)(L.snap_pres + g);
+          sp[0] = q.x, sp[1] = q.y, sp[2] = q.z, sp[3] = q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < OPL; ++k) {
+          const uint64_t p = g + k;
+          if (p < R0.off0 || p >= hi) continue;
+          const bool txm = u.has_txid && L.op_txid[p] == u.txid;
+          if (eval_op<DMAX, true>(u, (meta4 >> (8 * k)) & 0xFFu, ct[k], sv[k], sp[k], txm, p, a)) ib |= 1u << k;
+        }
       }
 #pragma unroll
       for (int k = 0; k < OPL; ++k) {
+        if (!((ib >> k) & 1u)) continue;
         const uint64_t p = g + k;
-        if (p < R0.off0 || p >= hi) continue;
-        const bool txm = u.has_txid && L.op_txid[p] == u.txid;
         const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
-        if (!eval_op<DMAX, true>(u, meta, ct[k], sv[k], sp[k], txm, p, a)) continue;
         if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
         if (TYPE == AM_BCOUNTER) {
           uint32_t slot;
@@ -304,6 +318,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
         }
       }
     }
+    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
     __syncthreads();
 
     // ---- scalar partials -> the read's accumulators ----
@@ -524,13 +539,19 @@ int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_res
   const uint32_t cap = (uint32_t)ctx->n_cu * 2;
   static bool attr = false;
   if (!attr) {
-    AM_HIP(hipFuncSetAttribute((const void *)k_big_chunk<DMAX, TYPE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    AM_HIP(hipFuncSetAttribute((const void *)k_big_chunk<DMAX, TYPE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(ChunkSmem)));
+    AM_HIP(hipFuncSetAttribute((const void *)k_big_chunk<DMAX, TYPE, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(ChunkSmem)));
     attr = true;
   }
   const unsigned g1 = (unsigned)(n_chunks < cap ? n_chunks : cap);
-  hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L, *B, nbig_d,
-                     br, acc, G, SL, n_chunks);
+  if (am_log_packed(L))  // the packed view: u32 commit vectors (4 * n_dc bytes per op, not 8 + 8 * n_dc)
+    hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE, true>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L, *B,
+                       nbig_d, br, acc, G, SL, n_chunks);
+  else
+    hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE, false>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L, *B,
+                       nbig_d, br, acc, G, SL, n_chunks);
   AM_HIP(hipGetLastError());
   if (TYPE != AM_BCOUNTER) {
     const uint64_t eg = (n_rec + 255) / 256;

@@ -331,33 +331,33 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   A.thr_vc = thr_vc;
   A.thr_pres = thr_pres;
 
-  // ---- pass 1: counts + exclusive scans
+  // ---- pass 1: counts + exclusive scans.  Temporaries live in the context's grow-only GC
+  //      scratch slot (no allocation per update once it has grown to the store's size).
   uint64_t *cnt = nullptr, *vcnt = nullptr;
   uint8_t *gap = nullptr, *gap_max = nullptr;
   void *tmp = nullptr;
   size_t tmp_b = 0, t2 = 0;
-  auto cleanup = [&]() {
-    (void)hipStreamSynchronize(c->stream);
-    if (cnt) (void)hipFree(cnt);
-    if (vcnt) (void)hipFree(vcnt);
-    if (gap) (void)hipFree(gap);
-    if (gap_max) (void)hipFree(gap_max);
-    if (A.keep_bits) (void)hipFree(A.keep_bits);
-    if (tmp) (void)hipFree(tmp);
-  };
+  auto cleanup = [&]() { (void)hipStreamSynchronize(c->stream); };
   if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, cnt, cnt, nk + 1, c->stream) != hipSuccess ||
       hipcub::DeviceReduce::Max(nullptr, t2, gap, gap_max, nk ? nk : 1, c->stream) != hipSuccess) {
     am_set_error("am_store_update: scan sizing failed");
     return AM_ERR_HIP;
   }
   if (t2 > tmp_b) tmp_b = t2;
-  if (hipMalloc((void **)&cnt, (nk + 1) * 8) != hipSuccess || hipMalloc((void **)&vcnt, (nk + 1) * 8) != hipSuccess ||
-      hipMalloc((void **)&gap, nk + 1) != hipSuccess || hipMalloc((void **)&gap_max, 8) != hipSuccess ||
-      hipMalloc(&tmp, tmp_b + 16) != hipSuccess ||
-      (prune_mask && hipMalloc((void **)&A.keep_bits, (L.n_ops / 64 + 2) * 8) != hipSuccess)) {
-    cleanup();
-    am_set_error("am_store_update: out of device memory");
-    return AM_ERR_NOMEM;
+  {
+    const size_t o_vcnt = am_round_up((nk + 1) * 8, 256), o_gap = o_vcnt + am_round_up((nk + 1) * 8, 256);
+    const size_t o_gmax = o_gap + am_round_up(nk + 1, 256), o_tmp = o_gmax + 256;
+    const size_t o_keep = o_tmp + am_round_up(tmp_b + 16, 256);
+    const size_t total = o_keep + (prune_mask ? am_round_up((L.n_ops / 64 + 2) * 8, 256) : 0);
+    void *scr = nullptr;
+    if (int rc = am_ctx_scratch(c, AM_SCR_GC, total, &scr)) return rc;
+    char *b = (char *)scr;
+    cnt = (uint64_t *)b;
+    vcnt = (uint64_t *)(b + o_vcnt);
+    gap = (uint8_t *)(b + o_gap);
+    gap_max = (uint8_t *)(b + o_gmax);
+    tmp = b + o_tmp;
+    A.keep_bits = prune_mask ? (uint64_t *)(b + o_keep) : nullptr;
   }
   uint64_t tot[2] = {0, 0};
   bool ok = hipMemsetAsync(cnt + nk, 0, 8, c->stream) == hipSuccess &&

@@ -162,49 +162,6 @@ __device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
   }
 }
 
-// the OPL packed-view ops [g, g + OPL) of a read's [off0, off1), entries x already loaded:
-// inclusion bits (is_op_in_snapshot/7), partials in ap.  Branch-free: x - thr saturates to 0
-// iff x <= thr, so one OR per op tests every DC; LastOpCt takes the included ops' entries
-// through max chains.  An escaped op (x[k][0] == AM_PK_ESC) only sets esc.
-template <int DMAX, int OPL, bool GENERAL>
-__device__ __forceinline__ uint32_t pk_tile(const ReadU<DMAX> &u, const PkRead<DMAX> &pk, const uint32_t (&x)[OPL][DMAX],
-                                            const uint64_t (&tx)[OPL], uint64_t g, uint64_t off0, uint64_t off1,
-                                            AccP<DMAX> &ap, bool &esc) {
-  uint32_t ib = 0, ev = 0;  // ev: evaluated (in range, in the packed view, a candidate)
-#pragma unroll
-  for (int k = 0; k < OPL; ++k) {
-    const uint64_t p = g + k;
-    const bool inr = p >= off0 && p < off1;
-    const bool e = x[k][0] == AM_PK_ESC;
-    esc |= inr && e;
-    uint32_t over = 0;
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(x[k][d], pk.thr[d]);
-    bool cand = inr && !e;
-    if (GENERAL) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
-      uint32_t cov = 0;
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) cov |= __builtin_elementwise_sub_sat(x[k][d], pk.cthr[d]);
-      const bool le = !pk.cnever && cov == 0;
-      cand = cand && (u.base_ignore || (u.has_txid && tx[k] == u.txid) || !le);
-    }
-    ib |= (uint32_t)(cand && !pk.never && over == 0) << k;
-    ev |= (uint32_t)cand << k;
-  }
-#pragma unroll
-  for (int d = 0; d < DMAX; ++d) {
-    uint32_t m = ap.mx[d];
-#pragma unroll
-    for (int k = 0; k < OPL; ++k) m = max(m, ((ib >> k) & 1u) ? x[k][d] : 0u);
-    ap.mx[d] = m;
-  }
-  ap.count += (uint32_t)__popc(ib);
-  const uint32_t ex = ev & ~ib;
-  if (ex) ap.min_excl = umin64(ap.min_excl, g + (uint64_t)__builtin_ctz(ex));
-  if (ev) ap.flags |= pk.miss;
-  return ib;
-}
-
 // the OPL ops [g, g + OPL) of a read's [off0, off1): inclusion bits (is_op_in_snapshot/7).
 // Packed view: u32 entries relative to the key's time base (am_wave.h pk_eval), partials in
 // ap; an escaped op (pk_vc[0] == AM_PK_ESC) is not evaluated here: esc is set and the
@@ -626,12 +583,15 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
       const uint32_t sh = (uint32_t)(off0 & (OPL - 1));
 
-      // the first record chunk is in flight while the ops are evaluated
-      uint32_t rec[VRPT];
+      // the first record chunk is in flight while the ops are evaluated.  A chunk is 512
+      // records from the 16-byte-aligned qa: lane l holds records qa + 4 l + 256 j + {0..3}
+      // (two 16-byte loads; records outside [rk0, rk1) are masked when applied)
+      const uint64_t qa = rk0 & ~3ull;
+      u32x4 rec[VRPT / 4];
 #pragma unroll
-      for (int jj = 0; jj < VRPT; ++jj) {
-        const uint64_t q = rk0 + (uint64_t)jj * WAVE + lane;
-        rec[jj] = q < rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+      for (int jj = 0; jj < VRPT / 4; ++jj) {
+        const uint64_t q = qa + (uint64_t)jj * 4 * WAVE + 4 * lane;
+        rec[jj] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
       }
       for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
 
@@ -663,25 +623,30 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       PH(1);
       // ---- 2. records of included ops -> newest birth / kill per group (the next chunk's
       //      loads in flight while one chunk is applied) ----
-      for (uint64_t q0 = rk0; !(AMK_SKIP & 1);) {
+      for (uint64_t q0 = qa; !(AMK_SKIP & 1);) {
         const uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
-        uint32_t nxt[VRPT];
+        u32x4 nxt[VRPT / 4];
 #pragma unroll
-        for (int jj = 0; jj < VRPT; ++jj) {
-          const uint64_t q = q1 + (uint64_t)jj * WAVE + lane;
-          nxt[jj] = q < rk1 ? L.rec_g[q] : 0xFFFFFFFFu;
+        for (int jj = 0; jj < VRPT / 4; ++jj) {
+          const uint64_t q = q1 + (uint64_t)jj * 4 * WAVE + 4 * lane;
+          nxt[jj] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
         }
 #pragma unroll
-        for (int jj = 0; jj < VRPT; ++jj) {
-          const uint32_t x = rec[jj];
-          if (x == 0xFFFFFFFFu) continue;
-          const uint32_t op = AM_REC_OP(x), bit = op + sh;
-          if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
-          atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
+        for (int jj = 0; jj < VRPT / 4; ++jj) {
+          const uint64_t q = q0 + (uint64_t)jj * 4 * WAVE + 4 * lane;
+          const uint32_t xs[4] = {rec[jj].x, rec[jj].y, rec[jj].z, rec[jj].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t x = xs[k];
+            if (x == 0xFFFFFFFFu || q + k < rk0 || q + k >= rk1) continue;
+            const uint32_t op = AM_REC_OP(x), bit = op + sh;
+            if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
+            atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
+          }
         }
         if (q1 >= rk1) break;
 #pragma unroll
-        for (int jj = 0; jj < VRPT; ++jj) rec[jj] = nxt[jj];
+        for (int jj = 0; jj < VRPT / 4; ++jj) rec[jj] = nxt[jj];
         q0 = q1;
       }
       wave_sync();

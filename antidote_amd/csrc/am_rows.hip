@@ -15,7 +15,7 @@
 //   PN counter / LWW register  commutative reductions in registers (am_wave.h)
 //   bounded counter            n_dc <= 16: every included amount goes into the row's LDS
 //                              slot array with one 64-bit LDS atomic (exact: a row read has
-//                              <= 48 entries, each below 2^56 -- a larger amount defers the
+//                              <= 127 entries, each below 2^56 -- a larger amount defers the
 //                              read to the workgroup tier), then lane s writes slots s,
 //                              s+16, ... with the base added in 128 bits; n_dc > 16: the
 //                              (slot, amount) pairs go to an LDS list that each lane scans
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
             } else if constexpr (BC) {
               if (status == AM_OK && rs->ctr[3]) defer = true;
               if (RS::SLOTS && status == AM_OK && !defer) {
-                // |row sum| < 48 * 2^56: exact in int64; the base is added in 128 bits
+                // |row sum| < 127 * 2^56 < 2^63: exact in int64; the base is added in 128 bits
                 auto total = [&](uint32_t i, int64_t &hi, uint64_t &lo, uint32_t &pr) {
                   uint32_t bp = 0;
                   const int64_t bv = GENERAL ? bc_base(B, rj, np, nd, i, bp) : 0;

@@ -115,7 +115,7 @@ __device__ Smem carve(unsigned char *p) {
 }
 constexpr size_t SMEM_BYTES = (size_t)KCAP * 20 + (size_t)BCAP * 20 + (size_t)BCAP * 16 + 16 * 4 + NW * 8 * 8;
 
-template <int DMAX, int TYPE>
+template <int DMAX, int TYPE, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                 am_retry retry) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -198,37 +198,51 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
 
     Acc<DMAX> a;
     a.reset();
+    AccP<DMAX> ap;
+    ap.reset();
+    PkRead<DMAX> pk;
+    if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[key]), pk);
     LdsSink sink{&s};
     // ---- stream the log, 1024 ops per tile ----
     for (uint64_t t0 = off0 & ~(uint64_t)(OPL - 1); t0 < off1; t0 += TILE) {
       const uint64_t g = t0 + (uint64_t)tid * OPL;
       if (g < off1) {
         const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
-        const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
-        const uint64_t ct[OPL] = {c01.x, c01.y, c23.x, c23.y};
-        uint64_t sv[OPL][DMAX];
+        uint32_t ib = 0;
+        if constexpr (PACKED) {
+          ib = incl4<DMAX, true>(L, nd, stride, u, pk, g, off0, off1, ap, a);
+        } else {
+          const u64x2 c01 = *(const u64x2 *)(L.commit_time + g), c23 = *(const u64x2 *)(L.commit_time + g + 2);
+          const uint64_t ct[OPL] = {c01.x, c01.y, c23.x, c23.y};
+          uint64_t sv[OPL][DMAX];
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          if (d < (int)nd) {
-            const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
-            const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
-            sv[0][d] = s01.x, sv[1][d] = s01.y, sv[2][d] = s23.x, sv[3][d] = s23.y;
-          } else {
-            sv[0][d] = sv[1][d] = sv[2][d] = sv[3][d] = 0;
+          for (int d = 0; d < DMAX; ++d) {
+            if (d < (int)nd) {
+              const uint64_t *col = L.snap_vc + (uint64_t)d * stride + g;
+              const u64x2 s01 = *(const u64x2 *)col, s23 = *(const u64x2 *)(col + 2);
+              sv[0][d] = s01.x, sv[1][d] = s01.y, sv[2][d] = s23.x, sv[3][d] = s23.y;
+            } else {
+              sv[0][d] = sv[1][d] = sv[2][d] = sv[3][d] = 0;
+            }
           }
-        }
-        uint32_t sp[OPL] = {u.allmask, u.allmask, u.allmask, u.allmask};
-        if (L.snap_pres) {
-          const u32x4 q = *(const u32x4 *)(L.snap_pres + g);
-          sp[0] = q.x, sp[1] = q.y, sp[2] = q.z, sp[3] = q.w;
+          uint32_t sp[OPL] = {u.allmask, u.allmask, u.allmask, u.allmask};
+          if (L.snap_pres) {
+            const u32x4 q = *(const u32x4 *)(L.snap_pres + g);
+            sp[0] = q.x, sp[1] = q.y, sp[2] = q.z, sp[3] = q.w;
+          }
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) {
+            const uint64_t p = g + k;
+            if (p < off0 || p >= off1) continue;
+            const bool txm = u.has_txid && L.op_txid[p] == u.txid;
+            if (eval_op<DMAX, true>(u, (meta4 >> (8 * k)) & 0xFFu, ct[k], sv[k], sp[k], txm, p, a)) ib |= 1u << k;
+          }
         }
 #pragma unroll
         for (int k = 0; k < OPL; ++k) {
+          if (!((ib >> k) & 1u)) continue;
           const uint64_t p = g + k;
-          if (p < off0 || p >= off1) continue;
-          const bool txm = u.has_txid && L.op_txid[p] == u.txid;
           const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
-          if (!eval_op<DMAX, true>(u, meta, ct[k], sv[k], sp[k], txm, p, a)) continue;
           if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
           const int32_t pos = (int32_t)(p - off0);
           if (TYPE == AM_BCOUNTER) {
@@ -246,6 +260,7 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
         }
       }
     }
+    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
     __syncthreads();
 
     // ---- scalar outputs (block reductions) ----
@@ -405,17 +420,21 @@ int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
   const uint32_t nd = L->n_dc;
-#define AM_S(D)                                                                                        \
+  const bool packed = am_log_packed(L);
+#define AM_SP(D, P)                                                                                    \
   {                                                                                                    \
     static bool attr = false;                                                                          \
     if (!attr) {                                                                                       \
-      AM_HIP(hipFuncSetAttribute((const void *)k_sets<D, TYPE>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+      AM_HIP(hipFuncSetAttribute((const void *)k_sets<D, TYPE, P>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                  (int)SMEM_BYTES));                                                    \
       attr = true;                                                                                     \
     }                                                                                                  \
-    hipLaunchKernelGGL((k_sets<D, TYPE>), dim3((unsigned)blocks), dim3(BLOCK), SMEM_BYTES, ctx->stream, \
+    hipLaunchKernelGGL((k_sets<D, TYPE, P>), dim3((unsigned)blocks), dim3(BLOCK), SMEM_BYTES, ctx->stream, \
                        *L, *B, *R, S, retry);                                                          \
-  }                                                                                                    \
+  }
+#define AM_S(D)          \
+  if (packed) AM_SP(D, true) \
+  else AM_SP(D, false)   \
   break;
   switch (nd <= 1 ? 1 : nd <= 2 ? 2 : nd <= 3 ? 3 : nd <= 4 ? 4 : nd <= 8 ? 8 : nd <= 16 ? 16 : 32) {
     case 1: AM_S(1)
@@ -427,6 +446,7 @@ int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read
     default: AM_S(32)
   }
 #undef AM_S
+#undef AM_SP
   AM_HIP(hipGetLastError());
   return AM_OK;
 }

@@ -345,6 +345,91 @@ __device__ __forceinline__ void pk_fold(const AccP<DMAX> &p, uint64_t K, uint32_
   a.min_excl = umin64(a.min_excl, p.min_excl);
 }
 
+// the OPL packed-view ops [g, g + OPL) of a read's [off0, off1), entries x already loaded:
+// inclusion bits (is_op_in_snapshot/7), partials in ap.  Branch-free: x - thr saturates to 0
+// iff x <= thr, so one OR per op tests every DC; LastOpCt takes the included ops' entries
+// through max chains.  An escaped op (x[k][0] == AM_PK_ESC) only sets esc.
+template <int DMAX, int OPL, bool GENERAL>
+__device__ __forceinline__ uint32_t pk_tile(const ReadU<DMAX> &u, const PkRead<DMAX> &pk, const uint32_t (&x)[OPL][DMAX],
+                                            const uint64_t (&tx)[OPL], uint64_t g, uint64_t off0, uint64_t off1,
+                                            AccP<DMAX> &ap, bool &esc) {
+  uint32_t ib = 0, ev = 0;  // ev: evaluated (in range, in the packed view, a candidate)
+#pragma unroll
+  for (int k = 0; k < OPL; ++k) {
+    const uint64_t p = g + k;
+    const bool inr = p >= off0 && p < off1;
+    const bool e = x[k][0] == AM_PK_ESC;
+    esc |= inr && e;
+    uint32_t over = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(x[k][d], pk.thr[d]);
+    bool cand = inr && !e;
+    if (GENERAL) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
+      uint32_t cov = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) cov |= __builtin_elementwise_sub_sat(x[k][d], pk.cthr[d]);
+      const bool le = !pk.cnever && cov == 0;
+      cand = cand && (u.base_ignore || (u.has_txid && tx[k] == u.txid) || !le);
+    }
+    ib |= (uint32_t)(cand && !pk.never && over == 0) << k;
+    ev |= (uint32_t)cand << k;
+  }
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    uint32_t m = ap.mx[d];
+#pragma unroll
+    for (int k = 0; k < OPL; ++k) m = max(m, ((ib >> k) & 1u) ? x[k][d] : 0u);
+    ap.mx[d] = m;
+  }
+  ap.count += (uint32_t)__popc(ib);
+  const uint32_t ex = ev & ~ib;
+  if (ex) ap.min_excl = umin64(ap.min_excl, g + (uint64_t)__builtin_ctz(ex));
+  if (ev) ap.flags |= pk.miss;
+  return ib;
+}
+
+// Inclusion of the 4 ops [g, g + 4) of one read inside [lo, hi) (is_op_in_snapshot/7 +
+// belongs_to_snapshot_op/3, every clock general): bit k = op g + k included.  Packed view
+// (PACKED): u32 entries through pk_tile, partials in ap, escaped ops from the full columns;
+// full view: eval_op on the u64 columns, partials in a.  AM_META_BAD ops are included here
+// (eval_op flags them); callers skip their effects.
+template <int DMAX, bool PACKED>
+__device__ __forceinline__ uint32_t incl4(const am_op_log &L, uint32_t nd, uint64_t stride, const ReadU<DMAX> &u,
+                                          const PkRead<DMAX> &pk, uint64_t g, uint64_t lo, uint64_t hi, AccP<DMAX> &ap,
+                                          Acc<DMAX> &a) {
+  uint64_t tx[4] = {0, 0, 0, 0};
+  if (u.has_txid) {
+    const u64x2 t01 = *(const u64x2 *)(L.op_txid + g), t23 = *(const u64x2 *)(L.op_txid + g + 2);
+    tx[0] = t01.x, tx[1] = t01.y, tx[2] = t23.x, tx[3] = t23.y;
+  }
+  uint32_t ib = 0;
+  bool esc = false;
+  if (PACKED) {
+    uint32_t x[4][DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      u32x4 q = {0, 0, 0, 0};
+      if (d < (int)nd) q = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
+      x[0][d] = q.x, x[1][d] = q.y, x[2][d] = q.z, x[3][d] = q.w;
+    }
+    ib = pk_tile<DMAX, 4, true>(u, pk, x, tx, g, lo, hi, ap, esc);
+    if (!esc) return ib;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t p = g + k;
+    if (p < lo || p >= hi) continue;
+    if (PACKED && L.pk_vc[p] != AM_PK_ESC) continue;
+    uint64_t sv[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+    const uint32_t sp = L.snap_pres ? L.snap_pres[p] : u.allmask;
+    if (eval_op<DMAX, true>(u, L.op_meta[p], L.commit_time[p], sv, sp, u.has_txid && tx[k] == u.txid, p, a))
+      ib |= 1u << k;
+  }
+  return ib;
+}
+
 // base bounded-counter slot i of read r (P slots i < np, then the nd D slots): row r of the
 // [n][np] / [n][nd] arrays, or at base.bc_off[r] (snapshot-cache bases in the value pool)
 __device__ __forceinline__ int64_t bc_base(const am_read_batch &B, uint64_t r, uint32_t np, uint32_t nd, uint32_t i,

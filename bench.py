@@ -56,7 +56,8 @@ CONFIGS = {
                     "(64M keys at 8 GPUs), D=3"),
     "c5": dict(type=abi.AM_SYNTH_MV_BC, n_dc=16, n_keys=2 << 20, zipf=1.1, total_ops=128 << 20, hot_cap=1 << 20,
                set_cap=8, desc="MV register + bounded counter (50/50), Zipf s=1.1 key popularity, 2097152 keys / "
-                               "134217728 ops per GPU (16M keys / 1G ops at 8 GPUs), hot-key cap 2^20, D=16"),
+                               "99935993 ops per GPU (Zipf lengths for a 2^27-op target, hot keys capped at "
+                               "2^20; 16M keys at 8 GPUs), D=16"),
 }
 
 

@@ -34,8 +34,17 @@
  *                           + check_filter/7 (:565-604) as one batched log rebuild
  *   am_snapcache_gc_threshold  the prune threshold of snapshot_insert_gc/4 (:515-535):
  *                           vectorclock:min over the first SNAPSHOT_MIN cached snapshots
- *   am_key_partition        log_utilities:get_key_partition/1 for integer keys
- *                           (src/log_utilities.erl:60-79,100-118)
+ *   am_vnode_insert_host    one partition's materializer_vnode state: op_insert_gc/3 with
+ *   am_vnode_read_host      its write-triggered GC read (src/materializer_vnode.erl:622-647),
+ *                           internal_read/7 with ShouldGC (:371-376), load_ops/2 (:312-319)
+ *   am_read_objects_submit  clocksi_interactive_coord's read_objects fan-out over a GPU's
+ *                           partitions (src/clocksi_interactive_coord.erl:732-747,
+ *                           src/clocksi_readitem_server.erl:217-228) as one async batch
+ *   am_key_partition        log_utilities:get_key_partition/1 + convert_key/1: integer
+ *   am_key_partition_bytes  keys, binaries (list_to_integer text or SHA-1 chash_key) and
+ *                           other terms (src/log_utilities.erl:60-79,100-118)
+ *   am_codec_*              Erlang terms of CRDT states <-> order-preserving u64 labels
+ *                           (the NIF's term conversion)
  *
  * Conventions
  *   - Plain C, POD structure-of-arrays, no framework types.  Status codes
