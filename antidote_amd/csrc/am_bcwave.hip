@@ -1,0 +1,223 @@
+// am_bcwave.hip -- materialize/4 for bounded-counter reads between the row tier and the
+// big-read tier: one WAVE per read (antidote_crdt_counter_b: orddict:update_counter on
+// P[{From,To}] and D[Id] is a keyed sum, folded by clocksi_materializer:apply_operations/4,
+// src/clocksi_materializer.erl:113-121).
+//
+// The LDS-sort tier (am_sets.hip) gives such a read a 256-thread workgroup and 78 KB of LDS
+// sized for set births/kills, so a CU holds two reads and most of a workgroup idles on a
+// few hundred ops.  A counter read needs only its D*D + D slot sums: here each wave of a
+// 256-thread block owns one read at a time with 20 B of LDS per slot (5.4 KB at D = 16):
+//   * slots start at the base value (bc_base: row r of the base arrays, or a snapshot-cache
+//     entry in the value pool);
+//   * the read's ops stream in 256-op tiles over the packed view (am_wave.h incl4; escaped
+//     ops from the full columns), payload words loaded with them (16-byte loads);
+//   * every included amount goes into its slot with an exact 128-bit LDS accumulation
+//     (64-bit atomics + carry, am_block.h acc128_atomic) and sets the slot's presence;
+//   * scalar outputs come from wave reductions, the slots leave with coalesced stores and an
+//     int64 overflow check (AM_ERR_OVERFLOW where Erlang would return a bignum).
+// Reads it does not take (longer than BCW_OPS, n_dc > 16, no packed view) go to `next`.
+#include "am_block.h"
+
+using namespace amk;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int NW = BLOCK / WAVE;
+constexpr int OPL = 4;
+constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
+constexpr uint64_t BCW_OPS = 32768;  // longer logs: the chunked big-read tier
+
+template <int DMAX>
+struct BcSmem {
+  static constexpr uint32_t NS = DMAX * DMAX + DMAX;
+  uint64_t lo[NS];
+  int64_t hi[NS];
+  uint32_t pres[NS];
+};
+
+template <int DMAX>
+__global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                   am_retry next) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  BcSmem<DMAX> &s = reinterpret_cast<BcSmem<DMAX> *>(smem_raw)[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint32_t nd = L.n_dc, np = nd * nd, ns = np + nd;
+  const uint64_t n = B.n_reads;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : n;
+  const uint64_t W = (uint64_t)gridDim.x * NW;
+  for (uint64_t i = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6); i < nsel; i += W) {
+    const uint64_t r = S.idx ? (uint64_t)uniform_u32(S.idx[sel0 + i]) : i;
+    const uint64_t key = uniform_u64(B.key[r]);
+    const uint32_t rtype = uniform_u32(B.type[r]);
+    int32_t status = AM_OK;
+    uint64_t off0 = 0, off1 = 0;
+    if (key >= L.n_keys) {
+      status = AM_ERR_INVALID;
+    } else {
+      off0 = uniform_u64(L.key_off[key]);
+      off1 = uniform_u64(L.key_off[key + 1]);
+      const uint32_t ktype = uniform_u32(L.key_type[key]);
+      const uint32_t kfl = L.key_flags ? uniform_u32(L.key_flags[key]) : 0u;
+      if (off1 > off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES))) status = AM_ERR_CORRUPTED_OPS_CACHE;
+      else if (rtype != (uint32_t)AM_BCOUNTER) status = AM_ERR_INVALID;
+    }
+    if (status != AM_OK) {
+      if (lane == 0) R.status[r] = status, R.flags[r] = 0;
+      continue;
+    }
+    if (off1 - off0 > BCW_OPS) {
+      if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
+      continue;
+    }
+    ReadU<DMAX> u;
+    {  // per-read inputs, wave-uniform (every lane reads the same read)
+      u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+      const uint64_t rstride = B.per_read_clock ? n : 1, ridx = B.per_read_clock ? r : 0;
+      u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
+      u.base_ignore = !B.base_ignore || B.base_ignore[r];
+      u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+        u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+      }
+      u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+      u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+    }
+    PkRead<DMAX> pk;
+    pk_setup(u, nd, uniform_u64(L.key_tbase[key]), pk);
+    // slots start at the base value (orddict entries present in the base stay present)
+    for (uint32_t k = lane; k < ns; k += WAVE) {
+      uint32_t bp = 0;
+      const int64_t bv = bc_base(B, r, np, nd, k, bp);
+      s.lo[k] = (uint64_t)bv;
+      s.hi[k] = bv < 0 ? -1 : 0;
+      s.pres[k] = bp;
+    }
+    wave_sync();
+
+    Acc<DMAX> a;
+    AccP<DMAX> ap;
+    a.reset();
+    ap.reset();
+    for (uint64_t t = off0 & ~(uint64_t)(OPL - 1); t < off1; t += TILE) {
+      const uint64_t g = t + (uint64_t)lane * OPL;
+      if (g >= off1) continue;
+      const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
+      const u64x2 a01 = *(const u64x2 *)(L.p0 + g), a23 = *(const u64x2 *)(L.p0 + g + 2);
+      const u64x2 f01 = *(const u64x2 *)(L.p1 + g), f23 = *(const u64x2 *)(L.p1 + g + 2);
+      const uint64_t amt[OPL] = {a01.x, a01.y, a23.x, a23.y}, ft[OPL] = {f01.x, f01.y, f23.x, f23.y};
+      const uint32_t ib = incl4<DMAX, true>(L, nd, stride, u, pk, g, off0, off1, ap, a);
+#pragma unroll
+      for (int k = 0; k < OPL; ++k) {
+        if (!((ib >> k) & 1u)) continue;
+        const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
+        if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
+        const uint32_t kind = AM_META_KIND(meta);
+        const uint32_t from = (uint32_t)(ft[k] & 0xFF), to = (uint32_t)((ft[k] >> 8) & 0xFF);
+        if (kind > AM_BC_TRANSFER || from >= nd || to >= nd) {  // Type:update/2 would raise
+          a.flags |= FLAG_BAD;
+          continue;
+        }
+        const uint32_t slot = kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
+        const int64_t v = (int64_t)amt[k];
+        acc128_atomic(&s.lo[slot], &s.hi[slot], v < 0 ? -1 : 0, (uint64_t)v);
+        atomicOr(&s.pres[slot], 1u);
+      }
+    }
+    pk_fold(ap, pk.K, u.allmask, a);
+    wave_sync();
+
+    // ---- scalar outputs (wave reductions, results in every lane) ----
+    const uint32_t count = wave_sum_u32_v(a.count), flags = wave_or_u32_v(a.flags), pres = wave_or_u32_v(a.pres);
+    const uint64_t min_excl = wave_min_u64_v(a.min_excl);
+    uint64_t myct = 0;  // lane d: max X[d] over the included ops
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d >= (int)nd) continue;
+      const uint64_t m = wave_max_u64_v(a.mx[d]);
+      if ((uint32_t)d == lane) myct = m;
+    }
+    status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+    if (status == AM_OK) {
+      bool ovf = false;
+      for (uint32_t k = lane; k < ns; k += WAVE) ovf |= s.hi[k] != ((int64_t)s.lo[k] < 0 ? -1 : 0);
+      if (__ballot(ovf)) status = AM_ERR_OVERFLOW;
+    }
+    if (status == AM_OK)
+      for (uint32_t k = lane; k < ns; k += WAVE) {
+        if (k < np) {
+          R.value.bc_p[r * np + k] = (int64_t)s.lo[k];
+          R.value.bc_p_pres[r * np + k] = s.pres[k] ? 1 : 0;
+        } else {
+          R.value.bc_d[r * nd + (k - np)] = (int64_t)s.lo[k];
+          R.value.bc_d_pres[r * nd + (k - np)] = s.pres[k] ? 1 : 0;
+        }
+      }
+    const bool ign = u.base_ignore && count == 0;
+    const uint32_t opres = ign ? 0u : (pres | u.cpres);
+    if (status == AM_OK && lane < nd) {
+      uint64_t c0 = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if ((uint32_t)d == lane) c0 = u.C0[d];
+      R.last_ct[(uint64_t)lane * n + r] = ((opres >> lane) & 1u) ? (myct > c0 ? myct : c0) : 0;
+    }
+    if (lane == 0) {
+      R.status[r] = status;
+      R.flags[r] = (uint8_t)(flags & 0xFFu);
+      if (status == AM_OK) {
+        const uint64_t idb = L.key_id_base ? L.key_id_base[key] : 1;
+        const uint64_t nops = off1 - off0;
+        int64_t nlo;
+        if (min_excl != NONE)
+          nlo = (L.op_id ? (int64_t)L.op_id[min_excl] : (int64_t)(idb + (min_excl - off0))) - 1;
+        else
+          nlo = nops == 0 ? 0 : (L.op_id ? (int64_t)L.op_id[off1 - 1] : (int64_t)(idb + nops - 1));
+        R.new_last_op[r] = nlo;
+        R.last_ct_ignore[r] = ign ? 1 : 0;
+        R.last_ct_pres[r] = opres;
+        R.is_new_ss[r] = count > 0;
+        R.count[r] = count;
+      }
+    }
+    wave_sync();  // the slots are rewritten by the wave's next read
+  }
+}
+
+template <int D>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
+  constexpr size_t smem = sizeof(BcSmem<D>) * NW;
+  static int occ = 0;
+  if (!occ) {
+    AM_HIP(hipFuncSetAttribute((const void *)k_bc_wave<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bc_wave<D>, BLOCK, smem) != hipSuccess || occ < 1) occ = 1;
+  }
+  uint64_t blocks = (B->n_reads + NW - 1) / NW, cap = (uint64_t)ctx->n_cu * occ;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return AM_OK;
+  hipLaunchKernelGGL((k_bc_wave<D>), dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, *B, *R, S, next);
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
+}  // namespace
+
+bool am_bcwave_applies(const am_op_log *L, const am_read_result *R) {
+  return am_log_packed(L) && L->n_dc <= 16 && L->op_meta && R->value.bc_p && R->value.bc_p_pres && R->value.bc_d &&
+         R->value.bc_d_pres;
+}
+
+int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                     am_retry next) {
+  const uint32_t nd = L->n_dc;
+  if (nd <= 1) return launch_d<1>(ctx, L, B, R, S, next);
+  if (nd <= 2) return launch_d<2>(ctx, L, B, R, S, next);
+  if (nd <= 3) return launch_d<3>(ctx, L, B, R, S, next);
+  if (nd <= 4) return launch_d<4>(ctx, L, B, R, S, next);
+  if (nd <= 8) return launch_d<8>(ctx, L, B, R, S, next);
+  return launch_d<16>(ctx, L, B, R, S, next);
+}

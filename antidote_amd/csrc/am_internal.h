@@ -103,6 +103,11 @@ int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_
 uint32_t am_lane_accept(const am_op_log *L, const am_read_result *R, uint32_t types);
 int am_launch_lanes(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                     am_retry next, uint32_t accept);
+// Bounded-counter wave tier (am_bcwave.hip): one wave per read with LDS slot sums, reads
+// up to 32768 ops over the packed view (n_dc <= 16); the rest go to `next`.
+bool am_bcwave_applies(const am_op_log *L, const am_read_result *R);
+int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                     am_retry next);
 // the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
                           uint32_t *key_ngrp);

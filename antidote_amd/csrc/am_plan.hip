@@ -123,7 +123,8 @@ int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
 // Set types over selection S.
 //   add-wins set / MV register: token-group tier, row kernel (short logs) -> wave kernel ->
 //     workgroup kernel -> (hand-off lists) LDS-sort tier k_sets -> (retry list) big-read tier
-//   bounded counter: row tier -> (hand-off list) k_sets -> (retry list) big-read tier
+//   bounded counter: row tier -> (hand-off lists) wave tier (am_bcwave.hip) -> k_sets ->
+//     (retry list) big-read tier
 // rows_buf / grp_buf (two lists): [0] = 0, [1] = hand-off count, list at +64.
 int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
              uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf, bool lanes_done) {
@@ -143,6 +144,16 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     if (rc) return rc;
     cur.idx = C.list;
     cur.range = rows_buf;
+    if (grp_buf && am_bcwave_applies(L, R)) {  // wave per read up to its limit (am_bcwave.hip)
+      AM_HIP(hipMemsetAsync(grp_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
+      am_retry nx;
+      nx.count = grp_buf + 1;
+      nx.list = grp_buf + 64;
+      rc = am_launch_bcwave(ctx, L, B, R, cur, nx);
+      if (rc) return rc;
+      cur.idx = nx.list;
+      cur.range = grp_buf;
+    }
   } else if (grp_buf && am_group_applies(L, R, type)) {
     // lane (or, off the packed view, row) -> wave -> workgroup kernels; each hands what it
     // does not take to the next.  The lane tier already ran over a mixed batch.
@@ -191,7 +202,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   void *rows_scr = nullptr, *grp_scr = nullptr;
   {
     int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
-    if (!rc && B->type_hint != AM_PN && B->type_hint != AM_LWW && B->type_hint != AM_BCOUNTER)
+    if (!rc && B->type_hint != AM_PN && B->type_hint != AM_LWW)
       rc = am_ctx_scratch(ctx, AM_SCR_GRP, 2 * (n + 64) * sizeof(uint32_t), &grp_scr);
     if (rc) return rc;
   }
