@@ -135,7 +135,7 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
       e = hipMemcpyAsync(outs[i].h, arena + out_off[i], outs[i].bytes, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   }
-  (void)hipFree(arena);
+  am_dev_release(c, arena);  // stream-ordered reuse by the next host batch
   if (e != hipSuccess) {
     am_set_error("host batch: %s", hipGetErrorString(e));
     return AM_ERR_HIP;

@@ -6,7 +6,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/antidote_mat.h"
@@ -21,6 +23,13 @@ struct am_ctx {
   void *scratch[AM_N_SCR] = {};  // grow-only device scratch slots (planner, row/group hand-offs, big-read path)
   size_t scratch_bytes[AM_N_SCR] = {};
   uint64_t *pinned = nullptr;    // small pinned host buffer for device -> host counters
+  // Device blocks of destroyed stores / caches kept for reuse by am_dev_alloc (a rebuilt
+  // store -- am_store_update every GC round -- asks for the same column sizes again), by
+  // size; block sizes of every am_dev_alloc block.  Reuse is stream-ordered: every kernel
+  // of the context runs on its one stream.
+  std::multimap<size_t, void *> free_blocks;
+  std::unordered_map<void *, size_t> block_size;
+  size_t free_bytes = 0;
   // Every entry point that touches the stream, the scratch slots or the pinned buffer holds
   // this lock, so concurrent callers on one context (a partition's READ_CONCURRENCY read
   // servers, include/antidote.hrl:28) serialize instead of sharing scratch; recursive
@@ -48,6 +57,9 @@ struct am_retry {
 int am_ctx_scratch(am_ctx *ctx, int slot, size_t bytes, void **out);
 // copy `n` u64 counters device -> host through the pinned buffer (synchronizes the stream)
 int am_ctx_fetch(am_ctx *ctx, const void *dev, uint32_t n_u64, uint64_t *host);
+
+// return an am_dev_alloc block to the context (kept for reuse, or freed past the cache cap)
+extern "C" void am_dev_release(am_ctx *ctx, void *p);
 
 struct am_store {
   am_ctx *ctx = nullptr;

@@ -104,9 +104,10 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
 }
 
 // Short-read limit of the row tier (am_rows.hip): at most 64 ops (one 16-lane row, 4 steps)
-// for PN / LWW; 127 for the bounded counter (the row's 64-bit LDS slot sums stay exact for
-// 127 amounts below 2^56; with n_dc > 16 a read with more than 64 entries is deferred).
-constexpr uint32_t ROWS_SCALAR = 64, ROWS_BC = 127;
+// for PN / LWW; 48 for the bounded counter (longer reads: the wave tier, am_bcwave.hip --
+// on C5 48 measured 1.5 % faster than 127 and 36 % faster than sending every read to the
+// wave tier).  The row's 64-bit LDS slot sums stay exact up to 127 amounts below 2^56.
+constexpr uint32_t ROWS_SCALAR = 64, ROWS_BC = 48;
 
 // PN / LWW over selection S: k_stream takes the long reads and marks the short ones in a
 // per-batch mask (rows_buf + 64) for the row tier, which skips batches without any.

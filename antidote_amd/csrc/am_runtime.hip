@@ -47,6 +47,8 @@ int am_ctx_close(am_ctx *c) {
   AM_HIP(hipStreamSynchronize(c->stream));
   for (void *&p : c->scratch)
     if (p) (void)hipFree(p), p = nullptr;
+  for (auto &kv : c->free_blocks) (void)hipFree(kv.second);
+  c->free_blocks.clear();
   if (c->pinned) (void)hipHostFree(c->pinned), c->pinned = nullptr;
   (void)hipEventDestroy(c->ev0);
   (void)hipEventDestroy(c->ev1);
@@ -117,22 +119,60 @@ int am_ctx_fetch(am_ctx *c, const void *dev, uint32_t n, uint64_t *host) {
 }
 
 extern "C" {
+// Caching device allocator: blocks are 2-MiB multiples (256-B multiples below 1 MiB); a
+// request reuses the smallest cached block that is at least as large and at most 1/8
+// larger, else hipMalloc.  Released blocks are cached up to AM_BLOCK_CACHE bytes per
+// context.
+static constexpr size_t AM_BLOCK_CACHE = (size_t)64 << 30;
+
 int am_dev_alloc(am_ctx *c, size_t bytes, void **out) {
   if (!c || !out) return AM_ERR_INVALID;
+  AM_LOCK(c);
   AM_HIP(hipSetDevice(c->device));
+  const size_t want = am_round_up(bytes ? bytes : 16, bytes >= ((size_t)1 << 20) ? ((size_t)2 << 20) : 256);
+  auto it = c->free_blocks.lower_bound(want);
+  if (it != c->free_blocks.end() && it->first <= want + want / 8) {
+    *out = it->second;
+    c->free_bytes -= it->first;
+    c->free_blocks.erase(it);
+    return AM_OK;
+  }
   void *p = nullptr;
-  hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+  hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess && !c->free_blocks.empty()) {  // out of memory: give the cache back, retry
+    (void)hipStreamSynchronize(c->stream);
+    for (auto &kv : c->free_blocks) (void)hipFree(kv.second);
+    c->free_blocks.clear();
+    c->free_bytes = 0;
+    e = hipMalloc(&p, want);
+  }
   if (e != hipSuccess) {
-    am_set_error("hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    am_set_error("hipMalloc(%zu): %s", want, hipGetErrorString(e));
     return AM_ERR_NOMEM;
   }
+  c->block_size[p] = want;
   *out = p;
   return AM_OK;
 }
 
+void am_dev_release(am_ctx *c, void *p) {
+  if (!c || !p) return;
+  AM_LOCK(c);
+  auto it = c->block_size.find(p);
+  if (it == c->block_size.end() || c->free_bytes + it->second > AM_BLOCK_CACHE) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (it != c->block_size.end()) c->block_size.erase(it);
+    (void)hipFree(p);
+    return;
+  }
+  c->free_blocks.emplace(it->second, p);
+  c->free_bytes += it->second;
+}
+
 int am_dev_free(am_ctx *c, void *p) {
   if (!c) return AM_ERR_INVALID;
-  if (p) AM_HIP(hipFree(p));
+  am_dev_release(c, p);
   return AM_OK;
 }
 
@@ -187,8 +227,7 @@ int am_store_destroy(am_store *st) {
   if (!st) return AM_OK;
   AM_LOCK(st->ctx);
   (void)hipSetDevice(st->ctx->device);
-  (void)hipStreamSynchronize(st->ctx->stream);
-  for (void *p : st->allocs) (void)hipFree(p);
+  for (void *p : st->allocs) am_dev_release(st->ctx, p);  // kept for the next store's columns
   delete st;
   return AM_OK;
 }

@@ -534,7 +534,7 @@ int am_snapcache_destroy(am_snapcache *c) {
   AM_LOCK(c->ctx);
   (void)hipSetDevice(c->ctx->device);
   (void)hipStreamSynchronize(c->ctx->stream);
-  for (void *p : c->allocs) (void)hipFree(p);
+  for (void *p : c->allocs) am_dev_release(c->ctx, p);
   if (c->pool_a) (void)hipFree(c->pool_a);
   if (c->pool_b) (void)hipFree(c->pool_b);
   if (c->pool_p) (void)hipFree(c->pool_p);
