@@ -178,18 +178,28 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
     uint32_t ns = 0;
     if (take && setr) {
       uint64_t born = 0, killed = 0;
-      for (uint64_t q = q0; q < rk1; q += 4) {
-        const u32x4 cv = rv;
-        if (q + 4 < rk1) rv = *(const u32x4 *)(L.rec_g + q + 4);
-        const uint32_t xs[4] = {cv.x, cv.y, cv.z, cv.w};
+      // 16 records per step: the first vector was prefetched with the ops, the other three
+      // are loaded together (an MV read of 16 ops has 31 records: two steps, not eight)
+      for (uint64_t q = q0; q < rk1; q += 16) {
+        u32x4 cv[4];
+        cv[0] = rv;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t x = xs[k];
-          if (q + k < rk0 || q + k >= rk1 || x == 0xFFFFFFFFu) continue;
-          if (!((incl >> (AM_REC_OP(x) + sh)) & 1ull)) continue;
-          const uint64_t bit = 1ull << AM_REC_GRP(x);
-          if (x & AM_REC_KILL) killed |= bit;
-          else born |= bit;
+        for (int j = 1; j < 4; ++j)
+          cv[j] = q + 4 * j < rk1 ? *(const u32x4 *)(L.rec_g + q + 4 * j) : u32x4{~0u, ~0u, ~0u, ~0u};
+        if (q + 16 < rk1) rv = *(const u32x4 *)(L.rec_g + q + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t xs[4] = {cv[j].x, cv[j].y, cv[j].z, cv[j].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint64_t qq = q + 4 * j + k;
+            const uint32_t x = xs[k];
+            if (qq < rk0 || qq >= rk1 || x == 0xFFFFFFFFu) continue;
+            if (!((incl >> (AM_REC_OP(x) + sh)) & 1ull)) continue;
+            const uint64_t bit = 1ull << AM_REC_GRP(x);
+            if (x & AM_REC_KILL) killed |= bit;
+            else born |= bit;
+          }
         }
       }
       if (status == AM_OK) {
@@ -199,11 +209,20 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
         if (ns > ocap) {
           status = AM_ERR_CAPACITY;
         } else {
-          for (uint32_t o = 0; alive; ++o, alive &= alive - 1) {
-            const uint32_t g = (uint32_t)__builtin_ctzll(alive);
-            const u64x2 ab = *(const u64x2 *)(L.grp + 2 * (rk0 + g));
-            R.value.set_a[ooff + o] = ab.x;
-            R.value.set_b[ooff + o] = ab.y;
+          // survivors in group order, four gathers in flight per step
+          for (uint32_t o = 0; alive; o += 4) {
+            u64x2 ab[4];
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (alive) {
+                ab[j] = *(const u64x2 *)(L.grp + 2 * (rk0 + (uint32_t)__builtin_ctzll(alive)));
+                alive &= alive - 1;
+                m = j + 1;
+              }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if ((uint32_t)j < m) R.value.set_a[ooff + o + j] = ab[j].x, R.value.set_b[ooff + o + j] = ab[j].y;
           }
         }
       }
