@@ -521,7 +521,7 @@ constexpr int vopl() {
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
 __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
-                                                                  am_sel S, am_retry next) {
+                                                                  am_sel S, am_retry next, uint32_t short_opl) {
   constexpr int OPL = vopl<DMAX, PACKED>();
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
   constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
@@ -551,8 +551,9 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       rr = mm.r;
       if (mm.st != AM_OK) {
         R.status[mm.r] = mm.st, R.flags[mm.r] = 0;
-      } else if (mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || has_base_pairs(B, mm.r)) {
-        hand = true;
+      } else if (mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || has_base_pairs(B, mm.r) ||
+                 (short_opl && mm.G <= 64 && mm.off1 - (mm.off0 & ~(uint64_t)(short_opl - 1)) <= 64)) {
+        hand = true;  // (short_opl: a short read the lane tier takes next)
       } else {
         elig = true;
         WSlot &w = s.slot[lane];
@@ -881,7 +882,8 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
 template <int D, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
 int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
              int tier) {
-  if (tier == AM_GRP_WAVE) {
+  if ((tier & 0xFF) == AM_GRP_WAVE) {
+    const uint32_t short_opl = (tier & AM_GRP_HAND_SHORT) ? (D <= 8 ? 8u : 4u) : 0u;  // am_lanes.hip lopl
     constexpr size_t smem = sizeof(WaveSmem) * NW;
     static int occ = 0;
     if (!occ) {
@@ -895,7 +897,7 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     if (blocks > cap) blocks = cap;
     if (blocks == 0) return AM_OK;
     hipLaunchKernelGGL((k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), smem,
-                       ctx->stream, *L, *B, *R, S, next);
+                       ctx->stream, *L, *B, *R, S, next, short_opl);
   } else if (tier == AM_GRP_ROW) {
     static int occ = 0;
     if (!occ) {

@@ -104,6 +104,8 @@ int am_launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_re
 // kernel does not take (ungrouped keys, base-snapshot pairs, logs beyond its limits) go to
 // `next`.
 enum { AM_GRP_ROW = 0, AM_GRP_WAVE = 1, AM_GRP_WG = 2 };
+// with AM_GRP_WAVE: hand the reads the lane tier takes (<= 64 ops, <= 64 groups) to `next`
+constexpr int AM_GRP_HAND_SHORT = 0x100;
 bool am_group_applies(const am_op_log *L, const am_read_result *R, uint32_t type);
 int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                     uint32_t type, am_retry next, int tier);

@@ -156,17 +156,21 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
       cur.range = grp_buf;
     }
   } else if (grp_buf && am_group_applies(L, R, type)) {
-    // lane (or, off the packed view, row) -> wave -> workgroup kernels; each hands what it
-    // does not take to the next.  The lane tier already ran over a mixed batch.
+    // wave -> lane (or, off the packed view, row) -> workgroup kernels; each hands what it
+    // does not take to the next.  The wave kernel goes first and hands the short reads on,
+    // so a batch of long logs (C3) is not passed over by the lane kernel, whose hand-off
+    // atomics then serialize (one per wave on one counter).  Over a mixed batch the lane
+    // tier already ran.
     uint32_t *bufs[3] = {rows_buf, grp_buf, grp_buf + (B->n_reads + 64)};
     for (int k = 0; k < 3; ++k) AM_HIP(hipMemsetAsync(bufs[k], 0, 2 * sizeof(uint32_t), ctx->stream));
     const uint32_t lanes = lanes_done ? 0u : am_lane_accept(L, R, 1u << type);
-    const int tiers[3] = {AM_GRP_ROW, AM_GRP_WAVE, AM_GRP_WG};
-    for (int k = lanes_done ? 1 : 0; k < 3; ++k) {
+    const int tiers[3] = {AM_GRP_WAVE | (lanes ? AM_GRP_HAND_SHORT : 0), AM_GRP_ROW, AM_GRP_WG};
+    for (int k = 0; k < 3; ++k) {
+      if (k == 1 && lanes_done) continue;  // the short reads were the lane tier's already
       am_retry nx;
       nx.count = bufs[k] + 1;
       nx.list = bufs[k] + 64;
-      rc = (k == 0 && lanes) ? am_launch_lanes(ctx, L, B, R, cur, nx, lanes)
+      rc = (k == 1 && lanes) ? am_launch_lanes(ctx, L, B, R, cur, nx, lanes)
                              : am_launch_group(ctx, L, B, R, cur, type, nx, tiers[k]);
       if (rc) return rc;
       cur.idx = nx.list;
