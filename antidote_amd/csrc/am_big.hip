@@ -178,11 +178,20 @@ struct ChunkSmem {
   uint64_t red[4];
 };
 
+// MV register chunks keep their kills in an LDS hash on the token (the MV kill key) holding
+// the latest kill position, instead of a list bitonic-sorted per chunk: insert = one 64-bit
+// LDS CAS + atomicMax, a birth's lookup = a few probes.  A kill that finds no slot goes
+// straight to the global records (resolved by the global pass, like an LDS overflow).
+constexpr uint64_t HKEY_EMPTY = ~0ull;
+constexpr uint32_t HPROBES = 64;
+__device__ __forceinline__ uint32_t tok_slot(uint64_t t) { return (uint32_t)(key_hash(t, 0) & (LK - 1)); }
+
 struct ChunkSink {
   ChunkSmem *s;
   BigRec G;
   BigAcc *acc;
   uint64_t rec0;
+  bool mvhash;  // MV register: kills into the LDS token hash
   __device__ void gbirth(uint64_t a, uint64_t b, int32_t pos, uint32_t sub) {
     const uint64_t i = rec0 + atomicAdd(&acc->nbirth, 1u);
     G.ba[i] = a, G.bb[i] = b, G.bp[i] = pos, G.bs[i] = sub;
@@ -201,8 +210,26 @@ struct ChunkSink {
     if (bi < LB) s->lb_a[bi] = a, s->lb_b[bi] = b, s->lb_p[bi] = pos, s->lb_s[bi] = sub;
     else gbirth(a, b, pos, sub);  // LDS full: unresolved, straight to the global records
   }
+  __device__ bool hash_kill(uint64_t t, int32_t pos) {
+    if (t == HKEY_EMPTY) return false;
+    const uint32_t h = tok_slot(t);
+    for (uint32_t pr = 0; pr < HPROBES; ++pr) {
+      const uint32_t sl = (h + pr) & (LK - 1);
+      const unsigned long long old =
+          atomicCAS((unsigned long long *)&s->lk_a[sl], (unsigned long long)HKEY_EMPTY, (unsigned long long)t);
+      if (old == HKEY_EMPTY || old == t) {
+        atomicMax(&s->lk_p[sl], pos);
+        return true;
+      }
+    }
+    return false;
+  }
   __device__ void kills(const uint64_t *tok, uint32_t n, uint64_t e, int32_t pos) {
     for (uint32_t i = 0; i < n; ++i) {
+      if (mvhash) {
+        if (!hash_kill(tok[i], pos)) gkill<AM_AWSET>(tok[i], e, pos);  // e is 0 for MV kills
+        continue;
+      }
       const uint32_t ki = atomicAdd(&s->ctr[0], 1u);
       if (ki < LK) s->lk_a[ki] = tok[i], s->lk_b[ki] = e, s->lk_p[ki] = pos;
       else gkill<AM_AWSET>(tok[i], e, pos);  // e is 0 for MV kills already
@@ -246,7 +273,10 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
     u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
 
     if (tid < 8) s.ctr[tid] = 0;
-    ChunkSink sink{&s, G, acc, R0.rec0};
+    constexpr bool MVH = TYPE == AM_MVREG;
+    if (MVH)
+      for (uint32_t i = tid; i < LK; i += BLOCK) s.lk_a[i] = HKEY_EMPTY, s.lk_p[i] = (int32_t)0x80000000;
+    ChunkSink sink{&s, G, acc, R0.rec0, MVH};
     uint64_t *slo = s.lk_a;  // bounded counter: LDS slot sums of this chunk
     int64_t *shi = (int64_t *)s.lk_b;
     uint32_t *spres = (uint32_t *)s.lk_p;
@@ -348,6 +378,30 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
       continue;
     }
     // ---- local resolution, then export ----
+    if constexpr (MVH) {  // kills are in the LDS token hash
+      const uint32_t nb = s.ctr[1] < LB ? s.ctr[1] : LB;
+      for (uint32_t i = tid; i < nb; i += BLOCK) {
+        const uint64_t t = s.lb_b[i];  // MV kill key of the birth (value, token): its token
+        bool dead = false;
+        if (t != HKEY_EMPTY) {
+          const uint32_t h = tok_slot(t);
+          for (uint32_t pr = 0; pr < HPROBES; ++pr) {
+            const uint32_t sl = (h + pr) & (LK - 1);
+            const uint64_t k = s.lk_a[sl];
+            if (k == t) {
+              dead = s.lk_p[sl] > s.lb_p[i];
+              break;
+            }
+            if (k == HKEY_EMPTY) break;
+          }
+        }
+        if (!dead) sink.gbirth(s.lb_a[i], s.lb_b[i], s.lb_p[i], s.lb_s[i]);
+      }
+      for (uint32_t sl = tid; sl < LK; sl += BLOCK)  // the latest kill of each token
+        if (s.lk_a[sl] != HKEY_EMPTY) sink.gkill<AM_AWSET>(s.lk_a[sl], 0ull, s.lk_p[sl]);
+      __syncthreads();
+      continue;
+    }
     const uint32_t nk = s.ctr[0] < LK ? s.ctr[0] : LK;
     const uint32_t nb = s.ctr[1] < LB ? s.ctr[1] : LB;
     block_sort(s.lk_a, s.lk_b, s.lk_p, nk, LK);  // by (kill key, pos)
