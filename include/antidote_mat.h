@@ -57,8 +57,10 @@
  *     0..n_dc-1 in ascending Erlang term order (so sorted [{Dc, T}] renderings
  *     match).  n_dc <= AM_MAX_DC.
  *   - "ignore" (an atom in the reference) is an explicit flag.
- *   - Device entry points take DEVICE pointers and run asynchronously on the
- *     context's HIP stream; the *_host variants take host memory and block.
+ *   - Device entry points take DEVICE pointers and run on the context's HIP
+ *     stream, asynchronously but for the data-dependent counter readbacks each
+ *     one documents (am_materialize: at most two); the *_host variants take host
+ *     memory and block.
  */
 #ifndef ANTIDOTE_MAT_H
 #define ANTIDOTE_MAT_H
@@ -287,7 +289,10 @@ int am_store_log(const am_store *st, am_op_log *out);
 int am_store_destroy(am_store *st);
 
 /* ---- the hot path ---- */
-/* Device pointers; asynchronous on the ctx stream. */
+/* Device pointers; runs on the ctx stream.  Asynchronous except for two data-dependent
+ * counter readbacks: a mixed-type batch reads the lane tier's hand-off count once (and
+ * returns there when every read was short), and a batch whose set / bounded-counter reads
+ * reach the big-read tier reads that tier's count once to size its scratch. */
 int am_materialize(am_ctx *ctx, const am_op_log *dev_log, const am_read_batch *dev_batch,
                    am_read_result *dev_res);
 /* Host pointers for batch/result; the log is the store's device log.  Blocks. */
