@@ -168,6 +168,13 @@ SIGNATURES = [
     ("am_codec_size", c_uint64, [c_void_p]),
     ("am_codec_take_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     ("am_codec_compare", c_int, [c_char_p, c_uint64, c_char_p, c_uint64, POINTER(c_int)]),
+    ("am_txid_create", c_int, [POINTER(c_void_p)]),
+    ("am_txid_destroy", c_int, [c_void_p]),
+    ("am_txid_intern", c_int, [c_void_p, c_char_p, c_uint64, POINTER(c_uint64)]),
+    ("am_txid_lookup", c_int, [c_void_p, c_char_p, c_uint64, POINTER(c_uint64)]),
+    ("am_txid_forget", c_int, [c_void_p, c_char_p, c_uint64]),
+    ("am_txid_size", c_uint64, [c_void_p]),
+    ("am_txid_canonical", c_int, [c_char_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]),
     ("am_store_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]),
     ("am_snapcache_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]),
     ("am_vnode_relabel", c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),

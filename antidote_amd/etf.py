@@ -2,15 +2,36 @@
 enif_binary_to_term do in the NIF, for the Python mirror and its tests.
 
 Python terms: int (any size), float, Atom (str subclass) / str as atom, tuple, list
-(proper), bytes (binary).  The codec (am_codec) interns these encodings."""
+(proper), bytes (binary), Pid / Ref (the server_pid of a #tx_id{}; only the TxId map,
+am_txid, accepts them).  The codec (am_codec) interns these encodings."""
 from __future__ import annotations
 
 import struct
-from typing import Any
+from dataclasses import dataclass, field
+from typing import Any, Tuple
 
 
 class Atom(str):
     """An Erlang atom."""
+
+
+@dataclass(frozen=True)
+class Pid:
+    """An Erlang pid: NEW_PID_EXT (88), or PID_EXT (103, 8-bit creation) when legacy."""
+    node: str
+    id: int
+    serial: int
+    creation: int
+    legacy: bool = field(default=False, compare=False)
+
+
+@dataclass(frozen=True)
+class Ref:
+    """An Erlang reference: NEWER_REFERENCE_EXT (90), or NEW_REFERENCE_EXT (114) when legacy."""
+    node: str
+    creation: int
+    ids: Tuple[int, ...]
+    legacy: bool = field(default=False, compare=False)
 
 
 def encode(t: Any) -> bytes:
@@ -62,6 +83,26 @@ def _enc(t: Any, out: bytearray) -> None:
             out.append(106)
     elif isinstance(t, (bytes, bytearray)):
         out += bytes([109]) + struct.pack(">I", len(t)) + bytes(t)
+    elif isinstance(t, Pid):
+        if t.legacy:
+            out.append(103)
+            _enc(Atom(t.node), out)
+            out += struct.pack(">IIB", t.id, t.serial, t.creation & 0xFF)
+        else:
+            out.append(88)
+            _enc(Atom(t.node), out)
+            out += struct.pack(">III", t.id, t.serial, t.creation)
+    elif isinstance(t, Ref):
+        if t.legacy:
+            out += bytes([114]) + struct.pack(">H", len(t.ids))
+            _enc(Atom(t.node), out)
+            out.append(t.creation & 0xFF)
+        else:
+            out += bytes([90]) + struct.pack(">H", len(t.ids))
+            _enc(Atom(t.node), out)
+            out += struct.pack(">I", t.creation)
+        for x in t.ids:
+            out += struct.pack(">I", x)
     else:
         raise TypeError(f"no external term format for {type(t)}")
 
@@ -128,4 +169,20 @@ def _dec(b: bytes, i: int):
     if tag == 109:
         n = struct.unpack(">I", b[i:i + 4])[0]
         return bytes(b[i + 4:i + 4 + n]), i + 4 + n
+    if tag in (88, 103):
+        node, i = _dec(b, i)
+        if tag == 88:
+            pid_id, serial, creation = struct.unpack(">III", b[i:i + 12])
+            return Pid(str(node), pid_id, serial, creation), i + 12
+        pid_id, serial, creation = struct.unpack(">IIB", b[i:i + 9])
+        return Pid(str(node), pid_id, serial, creation, legacy=True), i + 9
+    if tag in (90, 114):
+        n = struct.unpack(">H", b[i:i + 2])[0]
+        node, i = _dec(b, i + 2)
+        if tag == 90:
+            creation, i = struct.unpack(">I", b[i:i + 4])[0], i + 4
+        else:
+            creation, i = b[i], i + 1
+        ids = struct.unpack(">" + "I" * n, b[i:i + 4 * n])
+        return Ref(str(node), creation, tuple(ids), legacy=tag == 114), i + 4 * n
     raise ValueError(f"unsupported tag {tag}")

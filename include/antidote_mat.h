@@ -488,6 +488,26 @@ int am_snapcache_relabel(am_ctx *ctx, am_snapcache *c, const uint8_t *key_type, 
 /* both, for a vnode's ops cache and snapshot cache */
 int am_vnode_relabel(am_vnode *v, const uint64_t *old_labels, const uint64_t *new_labels, uint64_t n);
 
+/* ---- transaction ids (am_txid.hip) ----
+ * is_op_in_snapshot/7 compares TxIds for equality only: TxId == Op#clocksi_payload.txid
+ * (src/clocksi_materializer.erl:232).  #tx_id{local_start_time, server_pid}
+ * (include/antidote.hrl:192-195) holds a pid, so TxIds are NOT labelled by the ordered codec:
+ * am_txid_intern maps the external term format of a TxId (enif_term_to_binary, pids, ports and
+ * references included) to a dense u64 id, the op_txid / am_read_batch.txid words.  Every
+ * encoding of one term gets one id (the bytes are canonicalised first); ids start at 1, are
+ * never reordered, relabeled or reused.  am_txid_forget drops an ended transaction's entry.
+ * Thread-safe.  Maps and funs: AM_ERR_UNSUPPORTED. */
+typedef struct am_txids am_txids;
+int am_txid_create(am_txids **out);
+int am_txid_destroy(am_txids *t);
+int am_txid_intern(am_txids *t, const uint8_t *term, uint64_t len, uint64_t *id);
+/* AM_CODEC_ABSENT when the TxId was never interned (or was forgotten) */
+int am_txid_lookup(am_txids *t, const uint8_t *term, uint64_t len, uint64_t *id);
+int am_txid_forget(am_txids *t, const uint8_t *term, uint64_t len);
+uint64_t am_txid_size(am_txids *t);
+/* the canonical encoding the map keys on (131-prefixed); *out_len always set */
+int am_txid_canonical(const uint8_t *term, uint64_t len, uint8_t *buf, uint64_t cap, uint64_t *out_len);
+
 /* ---- synthetic op logs (bench + parity; counter-based, regenerable per key) ---- */
 typedef struct am_synth_params {
   uint64_t seed;
