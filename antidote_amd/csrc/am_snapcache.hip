@@ -95,6 +95,31 @@ __device__ __forceinline__ uint64_t clk(const uint64_t *vc, uint32_t pres, uint3
 }
 __device__ __forceinline__ uint32_t n_slots(uint32_t nd) { return nd * nd + nd; }
 
+// snapshot_insert_gc/4's prune threshold (src/materializer_vnode.erl:523-527) over the kept
+// entries [s0, s0 + keep) (newest first): Acc = the oldest kept clock, then for every entry
+// newest -> oldest Acc = vectorclock:min([CT1, Acc]), i.e. each DC of CT1 lowered to
+// min(CT1[dc], Acc[dc]) with a DC missing from Acc read as 0 (a DC only in Acc keeps its entry;
+// oracle/ref_materializer.py vc_min2 gives the evidence for this rule).  Writes thr[d * stride]
+// (0 for absent DCs) and returns the presence mask.
+__device__ uint32_t gc_threshold(const ScView &C, uint64_t s0, uint32_t keep, uint64_t *thr, uint64_t stride) {
+  const uint32_t nd = C.n_dc;
+  const uint64_t last = s0 + keep - 1;
+  uint32_t pres = 0;
+  for (uint32_t d = 0; d < nd; ++d) {
+    bool have = (C.pres[last] >> d) & 1u;
+    uint64_t acc = have ? C.vc[last * nd + d] : 0;
+    for (uint32_t e = 0; e < keep; ++e) {
+      if (!((C.pres[s0 + e] >> d) & 1u)) continue;
+      const uint64_t a = C.vc[(s0 + e) * nd + d], b = have ? acc : 0;
+      acc = a < b ? a : b;
+      have = true;
+    }
+    thr[(uint64_t)d * stride] = have ? acc : 0;
+    pres |= (have ? 1u : 0u) << d;
+  }
+  return pres;
+}
+
 __global__ void k_sc_claim(ScView C, am_read_batch B) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < B.n_reads; r += (uint64_t)gridDim.x * blockDim.x)
     if (B.key[r] < C.n_keys) atomicMin(&C.owner[B.key[r]], (uint32_t)r);
@@ -276,16 +301,8 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       C.plen[s0] = off ? w : 0;
     }
     C.cnt[key] = (uint8_t)keep;
-    if (gc && G.mask) {  // CommitTime = vectorclock:min over the kept entries (dict merge)
-      uint32_t pr = 0;
-      for (uint32_t e = 0; e < keep; ++e) pr |= C.pres[s0 + e];
-      for (uint32_t d = 0; d < nd; ++d) {
-        uint64_t m = ~0ull;
-        for (uint32_t e = 0; e < keep; ++e)
-          if ((C.pres[s0 + e] >> d) & 1u) m = min(m, C.vc[(s0 + e) * nd + d]);
-        G.thr_vc[(uint64_t)d * C.n_keys + key] = ((pr >> d) & 1u) ? m : 0;
-      }
-      G.thr_pres[key] = pr;
+    if (gc && G.mask) {  // the prune threshold over the kept entries
+      G.thr_pres[key] = gc_threshold(C, s0, keep, G.thr_vc + key, C.n_keys);
       G.mask[key] = 1;
     }
   }
@@ -298,26 +315,16 @@ ScView view(const am_snapcache *c) {
 unsigned grid(uint64_t n) { return (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096); }
 
 // forced snapshot_insert_gc/4 on every cached key (src/materializer_vnode.erl:519-536): the
-// dict keeps its newest SNAPSHOT_MIN entries and CommitTime = vectorclock:min over them
-// (dict merge: a DC present in any of the clocks is kept, with the min over those having it)
+// dict keeps its newest SNAPSHOT_MIN entries and the prune threshold is gc_threshold over them
 __global__ void k_sc_threshold(ScView C, uint8_t *mask, uint64_t *thr_vc, uint32_t *thr_pres) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < C.n_keys;
        k += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t cnt = C.cnt[k];
     const uint32_t m = (cnt == ABSENT) ? 0 : (cnt < SMIN ? cnt : SMIN);
     if (cnt != ABSENT) C.cnt[k] = (uint8_t)m;
-    uint32_t pres = 0;
-    for (uint32_t e = 0; e < m; ++e) pres |= C.pres[k * CAP + e];
-    for (uint32_t d = 0; d < C.n_dc; ++d) {
-      uint64_t t = ~0ull;
-      for (uint32_t e = 0; e < m; ++e)
-        if ((C.pres[k * CAP + e] >> d) & 1u) {
-          const uint64_t v = C.vc[(k * CAP + e) * C.n_dc + d];
-          t = v < t ? v : t;
-        }
-      thr_vc[(uint64_t)d * C.n_keys + k] = ((pres >> d) & 1u) ? t : 0;
-    }
-    thr_pres[k] = pres;
+    thr_pres[k] = m ? gc_threshold(C, k * CAP, m, thr_vc + k, C.n_keys) : 0u;
+    if (!m)
+      for (uint32_t d = 0; d < C.n_dc; ++d) thr_vc[(uint64_t)d * C.n_keys + k] = 0;
     mask[k] = m ? 1 : 0;
   }
 }

@@ -345,8 +345,11 @@ int am_snapcache_get_value(am_ctx *ctx, const am_snapcache *cache, uint64_t key,
                            uint32_t *n_words, uint64_t *a, uint64_t *b, uint8_t *pres);
 
 /* A forced snapshot_insert_gc/4 on every cached key (src/materializer_vnode.erl:519-536): the
- * dict keeps its newest min(n, SNAPSHOT_MIN) entries and Thr = vectorclock:min (dict merge: a
- * DC present in any clock is kept) over them.  Device outputs: mask[n_keys] (1 = the key has
+ * dict keeps its newest min(n, SNAPSHOT_MIN) entries and Thr = the reference's fold over them
+ * (:523-527): Acc = the oldest kept clock, then Acc = vectorclock:min([CT1, Acc]) for each entry
+ * newest first, where min([V1, V2]) lowers each DC of V1 to min(V1[dc], V2[dc]) with a DC
+ * missing from V2 read as 0 (so while the initial {} snapshot is kept nothing is pruned; evidence
+ * in oracle/ref_materializer.py vc_min2).  Device outputs: mask[n_keys] (1 = the key has
  * a threshold), thr_vc[n_dc][n_keys], thr_pres[n_keys] -- exactly the prune arguments of
  * am_store_update (so ops are only pruned below snapshots that stay cached).  n_keys is the
  * cache's: hand the outputs only to am_store_update of a store with the same key count (the

@@ -160,13 +160,45 @@ def vc_all_dots_greater(v1, v2):
     return all(vc_get(v1, d) > vc_get(v2, d) for d in list(v1) + list(v2))
 
 
-def vc_min(vcs):
-    """vectorclock:min/1 -- dict:merge keeps keys present in only one clock."""
-    out: dict = {}
-    for v in vcs:
-        for k, t in v.items():
-            out[k] = min(out[k], t) if k in out else t
+def vc_min2(v1: dict, v2: dict) -> dict:
+    """vectorclock:min([V1, V2]): V2 with every DC of V1 lowered to min(V1[dc], V2[dc]), a DC
+    missing from V2 read as 0 (a DC only in V2 keeps V2's entry).
+
+    Pinned by the reference's own suites, not by a KAT: with dict:merge semantics (a DC missing
+    from one clock keeps the other's entry) the first GC read of a key that was never read
+    before -- op_insert_gc/3's read at NewId rem 50 == 0 (src/materializer_vnode.erl:633-640),
+    whose dict then holds the new snapshot and the initial {} one (:394-397) -- gets a prune
+    threshold equal to the new snapshot's clock, prunes every op, and prune_ops/2 leaves
+    element(FIRST_OP+Len) = 0 as an op (:580-583), on which the next materialize/4 walk fails
+    (src/clocksi_materializer.erl:173).  test/multidc/multiple_dcs_SUITE.erl:243-266 replicates
+    100 adds to a key no one reads before op 99 and passes, so min({}, X) must not be X: with a
+    missing DC read as 0 the threshold is all-zero while {} is kept and nothing is pruned."""
+    out = dict(v2)
+    for d, a in v1.items():
+        b = v2.get(d, 0)
+        out[d] = a if a < b else b
     return out
+
+
+def vc_min(vcs):
+    """vectorclock:min/1: min([V]) = V, min([V1, V2 | T]) = min([min2(V1, V2) | T])."""
+    if not vcs:
+        return {}
+    acc = dict(vcs[0])
+    for v in vcs[1:]:
+        acc = vc_min2(acc, v)
+    return acc
+
+
+def gc_threshold(pruned) -> dict:
+    """snapshot_insert_gc/4's prune threshold (src/materializer_vnode.erl:523-527):
+    {CT, _} = vector_orddict:last(Pruned), then foldl over the entries (newest first) of
+    Acc = vectorclock:min([CT1, Acc])."""
+    ct, _s = vo_last(pruned)
+    acc = ct
+    for ct1, _st in pruned[0]:
+        acc = vc_min([ct1, acc])
+    return acc
 
 
 # ---------------------------------------------------------------------------
@@ -619,10 +651,7 @@ def snapshot_insert_gc(key, sdict, should_gc, st: VnodeState):
     """:515-563."""
     if sdict[1] >= SNAPSHOT_THRESHOLD or should_gc:
         pruned = vo_sublist(sdict, 1, SNAPSHOT_MIN)
-        ct, _s = vo_last(pruned)
-        commit_time = ct
-        for ct1, _st in pruned[0]:
-            commit_time = vc_min([ct1, commit_time])
+        commit_time = gc_threshold(pruned)
         t = st.ops_cache.get(key)
         if t is None:
             length, op_id, list_len, tup = 0, 0, 0, None

@@ -228,7 +228,7 @@ def test_gpu_gc_from_snapshot_cache(mat):
                 assert _key_ops(D1, k) == _key_ops(D0, k)
                 continue
             sub = R.vo_sublist(st.snapshot_cache[k], 1, R.SNAPSHOT_MIN)
-            thr = R.vc_min([ct for ct, _s in sub[0]])
+            thr = R.gc_threshold(sub)
             st.snapshot_cache[k] = sub  # snapshot_insert_gc stores PrunedSnapshots (:536)
             t = st.ops_cache.get(k)
             if t is None:
