@@ -23,6 +23,12 @@
 using namespace amk;
 using namespace amk_grp;
 
+// experiment switch (phase costs; default off): bit 0 skips the PN / LWW payload loads, bit 1
+// the set records, bit 2 the survivor gathers
+#ifndef AMK_LANE_SKIP
+#define AMK_LANE_SKIP 0
+#endif
+
 namespace {
 
 constexpr uint32_t LBITS = 64;  // inclusion bits of a lane read: ops [off0 & ~(OPL-1), off1)
@@ -34,6 +40,54 @@ constexpr int LBLOCK = 256;
 template <int DMAX>
 constexpr int lopl() {
   return DMAX <= 8 ? 8 : 4;
+}
+
+// position of the k-th (0-based) set bit of m (k < popcount(m))
+__device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t k) {
+  uint32_t pos = 0, c = (uint32_t)__popc((uint32_t)m);
+  if (k >= c) k -= c, m >>= 32, pos += 32;
+  c = (uint32_t)__popc((uint32_t)m & 0xFFFFu);
+  if (k >= c) k -= c, m >>= 16, pos += 16;
+  c = (uint32_t)__popc((uint32_t)m & 0xFFu);
+  if (k >= c) k -= c, m >>= 8, pos += 8;
+  c = (uint32_t)__popc((uint32_t)m & 0xFu);
+  if (k >= c) k -= c, m >>= 4, pos += 4;
+  c = (uint32_t)__popc((uint32_t)m & 0x3u);
+  if (k >= c) k -= c, m >>= 2, pos += 2;
+  return pos + (k >= ((uint32_t)m & 1u) ? 1u : 0u);
+}
+
+// The wave's survivor gather: lane l contributes n survivors (alive bits of its read's groups,
+// pairs at grp[2 (src + g)], output slots dst, dst + 1, ...).  Entry j of the wave's list is
+// taken by lane j % 64: its owner is the last lane whose exclusive prefix is <= j, its group the
+// (j - prefix)-th set bit of the owner's mask.  All 64 lanes must be active.
+__device__ __forceinline__ void wave_gather(const am_op_log &L, const am_read_result &R, uint32_t n, uint64_t alive,
+                                            uint64_t src, uint64_t dst, uint32_t lane) {
+  const uint32_t incl = wave_incl_scan_u32(n, lane), excl = incl - n;
+  const uint32_t T = lane_u32(incl, WAVE - 1);
+  constexpr int K = 4;
+  for (uint32_t base = 0; base < T; base += K * WAVE) {
+    u64x2 ab[K];
+    uint64_t to[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t j = base + (uint32_t)k * WAVE + lane;
+      const uint32_t jj = j < T ? j : T - 1;
+      uint32_t own = 0;
+#pragma unroll
+      for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t c = own + step;
+        if (c < (uint32_t)WAVE && shfl_u32(excl, c) <= jj) own = c;
+      }
+      const uint32_t rank = jj - shfl_u32(excl, own);
+      const uint64_t m = shfl_u64(alive, own), s0 = shfl_u64(src, own), d0 = shfl_u64(dst, own);
+      to[k] = j < T ? d0 + rank : ~0ull;
+      if (j < T) ab[k] = *(const u64x2 *)(L.grp + 2 * (s0 + select64(m, rank)));
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (to[k] != ~0ull) R.value.set_a[to[k]] = ab[k].x, R.value.set_b[to[k]] = ab[k].y;
+  }
 }
 
 template <int DMAX, int OPL>
@@ -111,7 +165,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
     // the first record vector of a set read is in flight with the ops
     const uint64_t q0 = rk0 & ~3ull;
     u32x4 rv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    if (take && setr && rk1 > rk0) rv = *(const u32x4 *)(L.rec_g + q0);
+    if (!(AMK_LANE_SKIP & 2) && take && setr && rk1 > rk0) rv = *(const u32x4 *)(L.rec_g + q0);
 
     auto load = [&](LTile<DMAX, OPL> &T, uint64_t g) {
 #pragma unroll
@@ -124,8 +178,8 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
 #pragma unroll
       for (int k = 0; k < OPL; ++k) T.tx[k] = 0, T.v0[k] = 0, T.v1[k] = 0;
       if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, T.tx);
-      if (scal) ld_n64<OPL>(L.p0 + g, T.v0);
-      if (t == AM_LWW) ld_n64<OPL>(L.p1 + g, T.v1);
+      if (!(AMK_LANE_SKIP & 1) && scal) ld_n64<OPL>(L.p0 + g, T.v0);
+      if (!(AMK_LANE_SKIP & 1) && t == AM_LWW) ld_n64<OPL>(L.p1 + g, T.v1);
     };
     AccP<DMAX> ap;
     Acc<DMAX> a;
@@ -176,11 +230,12 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
 
     // ---- set reads: records of included ops -> born / killed groups -> survivors ----
     uint32_t ns = 0;
+    uint64_t galive = 0, gsrc = 0, gdst = 0;  // this lane's survivors for the wave's gather
     if (take && setr) {
       uint64_t born = 0, killed = 0;
       // 16 records per step: the first vector was prefetched with the ops, the other three
       // are loaded together (an MV read of 16 ops has 31 records: two steps, not eight)
-      for (uint64_t q = q0; q < rk1; q += 16) {
+      for (uint64_t q = q0; !(AMK_LANE_SKIP & 2) && q < rk1; q += 16) {
         u32x4 cv[4];
         cv[0] = rv;
 #pragma unroll
@@ -203,30 +258,22 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
         }
       }
       if (status == AM_OK) {
-        uint64_t alive = born & ~killed;
+        const uint64_t alive = born & ~killed;
         ns = (uint32_t)__popcll(alive);
         const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
         if (ns > ocap) {
           status = AM_ERR_CAPACITY;
-        } else {
-          // survivors in group order, four gathers in flight per step
-          for (uint32_t o = 0; alive; o += 4) {
-            u64x2 ab[4];
-            uint32_t m = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (alive) {
-                ab[j] = *(const u64x2 *)(L.grp + 2 * (rk0 + (uint32_t)__builtin_ctzll(alive)));
-                alive &= alive - 1;
-                m = j + 1;
-              }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if ((uint32_t)j < m) R.value.set_a[ooff + o + j] = ab[j].x, R.value.set_b[ooff + o + j] = ab[j].y;
-          }
+        } else if (!(AMK_LANE_SKIP & 4)) {
+          galive = alive, gsrc = rk0, gdst = ooff;
         }
       }
     }
+    // survivors of every set read of the wave in one gather: the wave's concatenated survivor
+    // list (read order, group order within a read) is split over all 64 lanes, so a wave issues
+    // up to 256 independent 16-byte group loads at once and writes each read's pairs with
+    // adjacent lanes (one lane per read looping over its survivors serialized a memory
+    // latency per four survivors)
+    wave_gather(L, R, (uint32_t)__popcll(galive), galive, gsrc, gdst, lane);
 
     // ---- outputs ----
     if (take) {
