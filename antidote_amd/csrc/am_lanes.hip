@@ -24,7 +24,7 @@ using namespace amk;
 using namespace amk_grp;
 
 // experiment switch (phase costs; default off): bit 0 skips the PN / LWW payload loads, bit 1
-// the set records, bit 2 the survivor gathers
+// the set records, bit 2 the survivor gathers, bit 3 every output but the status
 #ifndef AMK_LANE_SKIP
 #define AMK_LANE_SKIP 0
 #endif
@@ -40,6 +40,44 @@ constexpr int LBLOCK = 256;
 template <int DMAX>
 constexpr int lopl() {
   return DMAX <= 8 ? 8 : 4;
+}
+
+// ---- quad all-reductions (DPP quad_perm 1032, 2301): every lane of a quad ends with the
+// quad's value.  All 64 lanes must be active (DPP reads an inactive lane as 0).
+__device__ __forceinline__ uint32_t quad_or_u32(uint32_t v) {
+  v |= dpp32<0xB1>(v);
+  return v | dpp32<0x4E>(v);
+}
+__device__ __forceinline__ uint64_t quad_or_u64(uint64_t v) {
+  v |= dpp64<0xB1>(v);
+  return v | dpp64<0x4E>(v);
+}
+__device__ __forceinline__ uint32_t quad_sum_u32(uint32_t v) {
+  v += dpp32<0xB1>(v);
+  return v + dpp32<0x4E>(v);
+}
+__device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
+  v = max(v, dpp32<0xB1>(v));
+  return max(v, dpp32<0x4E>(v));
+}
+__device__ __forceinline__ uint64_t quad_min_u64(uint64_t v) {
+  v = umin64(v, dpp64<0xB1>(v));
+  return umin64(v, dpp64<0x4E>(v));
+}
+template <int C>
+__device__ __forceinline__ void quad_step_i128(int64_t &hi, uint64_t &lo) {
+  const uint64_t wlo = dpp64<C>(lo);
+  const int64_t whi = (int64_t)dpp64<C>((uint64_t)hi);
+  add128(hi, lo, whi, wlo);
+}
+template <int C>
+__device__ __forceinline__ void quad_step_lww(LwwVal &v) {
+  const uint64_t ts = dpp64<C>(v.ts), val = dpp64<C>(v.val);
+  const uint32_t has = dpp32<C>(v.has);
+  const bool gt = has && (!v.has || ts > v.ts || (ts == v.ts && val > v.val));
+  v.ts = gt ? ts : v.ts;
+  v.val = gt ? val : v.val;
+  v.has |= has;
 }
 
 // position of the k-th (0-based) set bit of m (k < popcount(m))
@@ -191,7 +229,90 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
     lv.reset();
     bool esc = false;
     uint64_t incl = 0;
-    {
+    if constexpr (!GENERAL) {
+      // The scan in QUAD shape: the wave's 64 reads in 4 phases of 16; in phase ph quad q
+      // (lanes 4q..4q+3) scans read 16 ph + q, lane j of the quad holding ops [4j, 4j+4) of each
+      // 16-op tile, so each packed column / payload load is 64 / 128 contiguous bytes per quad
+      // (one lane per read reading its own 64-byte segments: 5.0 TB/s on C4's columns, this
+      // shape 6.3, scripts/bw_probe_c4.hip).  The quad's partials are combined by DPP and handed
+      // to the read's own lane (ds_bpermute), which carries on as before.
+      const uint32_t qj = lane & 3u;
+      const uint32_t tk = take ? (t | 0x100u) : 0u;
+#pragma unroll 1
+      for (uint32_t ph = 0; ph < 4; ++ph) {
+        const uint32_t src = 16u * ph + (lane >> 2);
+        const uint32_t qt = shfl_u32(tk, src);
+        const uint64_t qo0 = shfl_u64(off0, src), qo1 = shfl_u64(off1, src), qK = shfl_u64(pk.K, src);
+        const bool qtake = (qt >> 8) & 1u;
+        const uint32_t qty = qt & 0xFFu;
+        PkRead<DMAX> qpk;
+        pk_setup(u, nd, qK, qpk);
+        const uint64_t qt0 = qo0 & ~(uint64_t)(OPL - 1);  // the owner's inclusion-bit window
+        AccP<DMAX> qap;
+        qap.reset();
+        PnVal qpv;
+        LwwVal qlv;
+        qpv.reset();
+        qlv.reset();
+        bool qesc = false;
+        uint64_t qincl = 0;
+        for (uint64_t g = (qo0 & ~3ull) + 4 * qj; qtake && g < qo1; g += 16) {
+          uint32_t x[4][DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            u32x4 q = {0, 0, 0, 0};
+            if (d < (int)nd) q = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
+            x[0][d] = q.x, x[1][d] = q.y, x[2][d] = q.z, x[3][d] = q.w;
+          }
+          u64x2 a0 = {0, 0}, a1 = {0, 0}, c0 = {0, 0}, c1 = {0, 0};
+          if (!(AMK_LANE_SKIP & 1) && (qty == AM_PN || qty == AM_LWW))
+            a0 = *(const u64x2 *)(L.p0 + g), a1 = *(const u64x2 *)(L.p0 + g + 2);
+          if (!(AMK_LANE_SKIP & 1) && qty == AM_LWW) c0 = *(const u64x2 *)(L.p1 + g), c1 = *(const u64x2 *)(L.p1 + g + 2);
+          const uint64_t tx[4] = {0, 0, 0, 0};
+          const uint32_t ib = pk_tile<DMAX, 4, false>(u, qpk, x, tx, g, qo0, qo1, qap, qesc);
+          qincl |= (uint64_t)ib << (g - qt0);
+          const uint64_t pv0[4] = {a0.x, a0.y, a1.x, a1.y}, pv1[4] = {c0.x, c0.y, c1.x, c1.y};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if ((ib >> k) & 1u) {
+              if (qty == AM_PN) qpv.add(pv0[k], 0);
+              else if (qty == AM_LWW) qlv.add(pv0[k], pv1[k]);
+            }
+        }
+        qincl = quad_or_u64(qincl);
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) qap.mx[d] = quad_max_u32(qap.mx[d]);
+        qap.count = quad_sum_u32(qap.count);
+        qap.flags = quad_or_u32(qap.flags | (qesc ? 0x200u : 0u));
+        qap.min_excl = quad_min_u64(qap.min_excl);
+        quad_step_i128<0xB1>(qpv.hi, qpv.lo);
+        quad_step_i128<0x4E>(qpv.hi, qpv.lo);
+        quad_step_lww<0xB1>(qlv);
+        quad_step_lww<0x4E>(qlv);
+        // PN and LWW reads are exclusive: one payload pair travels
+        const uint64_t w0 = qty == AM_LWW ? qlv.ts : (uint64_t)qpv.hi, w1 = qty == AM_LWW ? qlv.val : qpv.lo;
+        const uint32_t fl = qap.flags | (qlv.has ? 0x400u : 0u);
+        // the read's own lane (16 ph + q) takes its quad's values from quad lane 0
+        const uint32_t from = (lane >> 4) == ph ? 4u * (lane & 15u) : lane;
+        const uint64_t r_incl = shfl_u64(qincl, from), r_me = shfl_u64(qap.min_excl, from);
+        const uint64_t r_w0 = shfl_u64(w0, from), r_w1 = shfl_u64(w1, from);
+        const uint32_t r_cnt = shfl_u32(qap.count, from), r_fl = shfl_u32(fl, from);
+        uint32_t r_mx[DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) r_mx[d] = d < (int)nd ? shfl_u32(qap.mx[d], from) : 0u;
+        if ((lane >> 4) == ph) {
+          incl = r_incl;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) ap.mx[d] = r_mx[d];
+          ap.count = r_cnt;
+          ap.flags = r_fl & ~0x600u;
+          ap.min_excl = r_me;
+          esc = (r_fl & 0x200u) != 0;
+          if (t == AM_PN) pv.hi = (int64_t)r_w0, pv.lo = r_w1;
+          if (t == AM_LWW) lv.ts = r_w0, lv.val = r_w1, lv.has = (r_fl & 0x400u) ? 1u : 0u;
+        }
+      }
+    } else {
       LTile<DMAX, OPL> cur;
       for (uint64_t g = t0; take && g < off1; g += OPL) {
         load(cur, g);
@@ -300,6 +421,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
         vflag = win ? 0 : bbin;
       }
       R.status[r] = status;
+      if (AMK_LANE_SKIP & 8) continue;
       R.flags[r] = (uint8_t)(a.flags & 0xFFu);
       if (status == AM_OK) {
         R.new_last_op[r] = new_last_op(L, key, off0, off1, a.min_excl);

@@ -253,7 +253,20 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       const uint64_t x = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
       le = x <= clk(C.vc + s0 * nd, fp, d);
     }
-    const bool ins = !le;
+    bool ins = !le;
+    // the value words' room in the pool (sized on the host before the batch; offset 0 is never
+    // handed out): if it is ever missing the snapshot is not cached at all -- the read's own
+    // result stands -- rather than cached with an empty value (ctr[1] records the event)
+    const uint32_t w = ins ? value_words(R, r, t, nd) : 0u;
+    uint64_t off = 0;
+    if (w) {
+      off = atomicAdd((unsigned long long *)C.ctr, (unsigned long long)w);
+      if (off == 0 || off + w > C.pool_cap) {
+        atomicOr((unsigned long long *)(C.ctr + 1), 1ull);
+        ins = false;
+        off = 0;
+      }
+    }
     // snapshot_insert_gc/4: at SNAPSHOT_THRESHOLD entries (or ShouldGC) keep the newest
     // SNAPSHOT_MIN and prune the ops below their vectorclock:min
     const uint32_t grown = ne + (ins ? 1u : 0u);
@@ -277,14 +290,8 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       C.v0[s0] = (t == AM_PN || t == AM_LWW) ? R.value.v0[r] : 0;
       C.v1[s0] = t == AM_LWW ? R.value.v1[r] : 0;
       C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
-      // the value words into the pool (sized on the host before the batch: never overflows)
-      const uint32_t w = value_words(R, r, t, nd);
-      uint64_t off = 0;
+      // the value words into the pool
       if (w) {
-        off = atomicAdd((unsigned long long *)C.ctr, (unsigned long long)w);
-        if (off + w > C.pool_cap) off = 0, atomicOr((unsigned long long *)(C.ctr + 1), 1ull);  // host sizing bug
-      }
-      if (w && off) {
         if (t == AM_BCOUNTER) {
           const uint32_t q = nd * nd;
           for (uint32_t i = 0; i < w; ++i) {

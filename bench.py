@@ -6,18 +6,24 @@ One step = one batched snapshot read of every key this GPU owns:
      all-reduce over all ranks (am_gst_allreduce) -> am_gst_finalize; the stable
      snapshot lands in HBM and is the read's MinSnapshotTime (as a ClockSI
      transaction reads at the GST, src/clocksi_interactive_coord.erl:907-912);
-  2. am_materialize of all keys at that snapshot (clocksi_materializer:materialize/4
-     per key, fresh base: the first read of each key).  Mixed-type configs (c4, c5) are
-     one mixed batch: the library's planner splits it by type on the device.
-Default workload (BASELINE.json configs[1], "c2"): antidote_crdt_register_lww, 1M keys x
-256 ops per GPU, 3-DC vectorclocks, synthetic counter-based logs generated in HBM.
---config c1..c5 selects the other BASELINE.json configs (see CONFIGS).
+  2. --base fresh (default): am_materialize of all keys at that snapshot
+     (clocksi_materializer:materialize/4 per key, base ignore: the first read of each key);
+     --base cached: am_snapcache_read of all keys (materializer_vnode:read/6 ->
+     internal_read/7: base snapshot from the device snapshot cache, materialize/4, write-back),
+     the cache holding each key's q = 0.5 snapshot (SURVEY.md 8(d)'s cached mode).  The cache
+     is rebuilt at q = 0.5 between steps outside the timed region; each step's GST + read is
+     timed with HIP events on the library's stream.
+  Mixed-type configs (c4, c5) are one mixed batch: the library's planner splits it by type on
+  the device.
+Default workload: c3 (BASELINE.json configs[2], the largest single-GPU configuration):
+antidote_crdt_set_aw, 1M keys x 1024 ops per GPU, 8-DC vectorclocks, synthetic counter-based
+logs generated in HBM.  --config c1..c5 selects the other BASELINE.json configs (see CONFIGS).
 Weak scaling: each rank owns its own keys (keys shard by riak_core partition:
 partition = key mod 64, GPU = partition mod N; rank r's log holds exactly the keys with
 am_key_partition(key, 64) % N == r), so value = N * ops per GPU / step time.
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W --config c2]; for N > 1 under
-torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR from the env).
+Launch: python bench.py [--gpus 1 --steps K --warmup W --config c3 --base fresh]; for N > 1
+under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR from the env).
 """
 from __future__ import annotations
 
@@ -132,9 +138,32 @@ def workload_bytes(cfg, dlog, ko, kt, reads, packed):
     return total
 
 
-def cpu_baseline(cfg, p, budget_s=10.0):
+def cached_bytes(cfg, pre, reads):
+    """Extra algorithmic bytes of a cached-base read (am_snapcache_read) per read: the base
+    entry (clock 8*D + presence 4 + last_op 8 + value: PN / LWW 17, set pairs 16 each from the
+    value pool), the snapshot-cache dict header (count 1 + owner 4), and the write-back of a
+    stored snapshot (the same entry sizes, its pairs 16 each into the pool)."""
+    nd = cfg["n_dc"]
+    ent = 8 * nd + 4 + 8
+    n = reads.n
+    total = n * (ent + 5)
+    base_pairs = float(pre.set_len.sum().item()) if pre.set_len is not None else 0.0
+    total += base_pairs * 16 + (0 if pre.set_len is not None else n * 17)
+    stored = ((reads.is_new_ss != 0) & (reads.count >= 5)).cpu().numpy()
+    n_st = int(stored.sum())
+    total += n_st * ent
+    if reads.set_len is not None:
+        total += float(reads.set_len.cpu().numpy()[stored].sum()) * 16
+    else:
+        total += n_st * 17
+    return total
+
+
+def cpu_baseline(cfg, p, budget_s=10.0, cached=False):
     """The C restatement (oracle/am_oracle.c, a port of clocksi_materializer) on the host
-    cores, on a bounded sample of the same workload (host-regenerated keys).  Rank 0, N=1."""
+    cores, on a bounded sample of the same workload (host-regenerated keys).  Rank 0, N=1.
+    cached: every read starts from its q = 0.5 result as the base snapshot (materialize/4 with
+    a cached base; the snapshot-cache bookkeeping around it is not part of the port)."""
     from antidote_amd.oplog import HostBatch, Read
     from oracle import amo
     import threading
@@ -154,6 +183,21 @@ def cpu_baseline(cfg, p, budget_s=10.0):
         reads = [Read(k, int(kt[k]), {d: clock[d] for d in range(p.n_dc)}) for k in range(per)]
         hb = HostBatch(p.n_dc, reads, [max(cfg["set_cap"], 1)] * per)
         s = log.as_struct()
+        if cached:
+            half = synth.read_clock(p, 0.5)
+            h0 = HostBatch(p.n_dc, [Read(k, int(kt[k]), {d: half[d] for d in range(p.n_dc)}) for k in range(per)],
+                           [max(cfg["set_cap"], 1)] * per)
+            b0, r0 = h0.structs()
+            amo.lib().amo_materialize_range(ctypes.byref(s), ctypes.byref(b0), 0, per, ctypes.byref(r0))
+            assert (h0.status[:per] == 0).all(), "cpu baseline: q=0.5 reads failed"
+            hb.base_ignore[:] = h0.last_ct_ignore
+            hb.base_vc[:] = h0.last_ct
+            hb.base_pres[:] = h0.last_ct_pres
+            hb.base_last_op[:] = h0.new_last_op
+            hb.b_v0[:], hb.b_v1[:], hb.b_vflag[:] = h0.v0, h0.v1, h0.vflag
+            hb.b_set_off, hb.b_set_len, hb.b_set_a, hb.b_set_b = h0.o_set_off, h0.o_set_len, h0.o_set_a, h0.o_set_b
+            hb.b_bc_p, hb.b_bc_pp, hb.b_bc_d, hb.b_bc_dp = h0.o_bc_p, h0.o_bc_pp, h0.o_bc_d, h0.o_bc_dp
+            hb._h0 = h0
         b, r = hb.structs()
         parts.append((s, b, r, per, int(log.n_ops), log, hb))
     n_ops = sum(x[4] for x in parts)
@@ -181,7 +225,8 @@ def cpu_baseline(cfg, p, budget_s=10.0):
             break
     dt = time.perf_counter() - t0
     return {"value": passes * n_ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
-            "sample": f"{len(k0s) * per} keys ({n_ops} ops) of the same workload, {passes} passes in {dt:.1f}s, "
+            "sample": f"{len(k0s) * per} keys ({n_ops} ops) of the same workload"
+                      f"{' with q=0.5 cached bases' if cached else ''}, {passes} passes in {dt:.1f}s, "
                       f"C restatement of clocksi_materializer (oracle/am_oracle.c), not BEAM"}
 
 
@@ -207,6 +252,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--base", default="fresh", choices=["fresh", "cached"],
+                    help="fresh: base ignore (first read); cached: base from the snapshot cache at q = 0.5")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -272,13 +319,16 @@ def main():
                         types=types)
     read_vc, read_pres = reads.read_vc, reads.read_pres   # the GST result is written here
 
-    def step():
+    def gst():
         abi.check(mat.L.am_gst_local_min(mat.ctx, n_dc, len(parts), d_pvc.data_ptr(), d_ppres.data_ptr(), None,
                                          lanes.data_ptr()), "gst_local_min")
         abi.check(mat.L.am_gst_allreduce(comm, lanes.data_ptr(), n_dc), "gst_allreduce")
         abi.check(mat.L.am_gst_finalize(mat.ctx, n_dc, lanes.data_ptr(), last_vc.data_ptr(), last_pres.data_ptr(),
                                         0, read_vc.data_ptr(), read_pres.data_ptr(), changed.data_ptr()),
                   "gst_finalize")
+
+    def step():
+        gst()
         materialize(mat, dlog, reads)
 
     def barrier():
@@ -287,15 +337,55 @@ def main():
         if pg is not None:
             pg.barrier()
 
-    torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    dt = time.perf_counter() - t0
+    cache = [None]
+    if args.base == "cached":
+        # the q = 0.5 reads that fill the snapshot cache (each key's first read caches its
+        # snapshot: is_newest, >= MIN_OP_STORE_SS ops, src/materializer_vnode.erl:469-509)
+        pre = DeviceReads(n_keys, n_dc, type_ if type_ in range(1, 6) else 0, synth.read_clock(p, 0.5),
+                          set_cap=max(cfg["set_cap"], 1), types=types)
+
+        def populate():
+            if cache[0] is not None:
+                abi.check(mat.L.am_snapcache_destroy(cache[0]), "am_snapcache_destroy")
+            h = ctypes.c_void_p()
+            abi.check(mat.L.am_snapcache_create(mat.ctx, n_dc, n_keys, ctypes.byref(h)), "am_snapcache_create")
+            cache[0] = h
+            b, r = pre.structs()
+            abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(dlog), ctypes.byref(b), ctypes.byref(r)),
+                      "am_snapcache_read (populate)")
+
+        def cached_read():
+            b, r = reads.structs()
+            abi.check(mat.L.am_snapcache_read(mat.ctx, cache[0], ctypes.byref(dlog), ctypes.byref(b),
+                                              ctypes.byref(r)), "am_snapcache_read")
+
+        def timed_steps(k):
+            tot = 0.0
+            for _ in range(k):
+                populate()
+                barrier()
+                abi.check(mat.L.am_timer_start(mat.ctx), "timer")
+                gst()
+                cached_read()
+                ms_ = ctypes.c_float()
+                abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms_)), "timer")
+                tot += ms_.value * 1e-3
+            return tot
+
+        timed_steps(args.warmup)
+        barrier()
+        dt = timed_steps(args.steps)
+        barrier()
+    else:
+        torch.cuda.synchronize()
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        barrier()
+        dt = time.perf_counter() - t0
     if pg is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
@@ -304,20 +394,34 @@ def main():
     # sanity: the snapshot read used the GST and every read succeeded
     st = reads.status.cpu().numpy()
     assert (st == 0).all(), f"materialize returned errors: {np.unique(st, return_counts=True)}"
-    gst = read_vc.cpu().numpy().view(np.uint64)
-    assert [int(x) for x in gst] == [int(clock[d]) for d in range(n_dc)], "GST mismatch"
+    gst_vc = read_vc.cpu().numpy().view(np.uint64)
+    assert [int(x) for x in gst_vc] == [int(clock[d]) for d in range(n_dc)], "GST mismatch"
 
-    # ---- the materialize batch, timed alone with HIP events on the library's stream ----
+    # ---- the read batch, timed alone with HIP events on the library's stream ----
     kern_iters = max(5, args.steps)
-    barrier()
-    abi.check(mat.L.am_timer_start(mat.ctx), "timer")
-    for _ in range(kern_iters):
-        materialize(mat, dlog, reads)
-    ms = ctypes.c_float()
-    abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
-    kern_ms = ms.value / kern_iters
+    if args.base == "cached":
+        kern_s = 0.0
+        for _ in range(kern_iters):
+            populate()
+            barrier()
+            abi.check(mat.L.am_timer_start(mat.ctx), "timer")
+            cached_read()
+            ms = ctypes.c_float()
+            abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
+            kern_s += ms.value
+        kern_ms = kern_s / kern_iters
+    else:
+        barrier()
+        abi.check(mat.L.am_timer_start(mat.ctx), "timer")
+        for _ in range(kern_iters):
+            materialize(mat, dlog, reads)
+        ms = ctypes.c_float()
+        abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
+        kern_ms = ms.value / kern_iters
     packed = bool(dlog.pk_vc)
     alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed)
+    if args.base == "cached":
+        alg_bytes += cached_bytes(cfg, pre, reads)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
     total_ops = world * n_ops * args.steps
@@ -340,10 +444,16 @@ def main():
         "config": {"workload": workload, "keys_per_gpu": n_keys, "ops_per_gpu": n_ops, "n_dc": n_dc,
                    "snapshot_quantile": Q, "partitions": N_PARTITIONS, "parallelism": f"partition-sharded x{world}",
                    "key_placement": "rank r holds the keys with am_key_partition(key, 64) % N == r",
-                   "step": "GST min all-reduce (RCCL) + materialize all keys"},
+                   "step": "GST min all-reduce (RCCL) + materialize all keys" if args.base == "fresh" else
+                           "GST min all-reduce (RCCL) + am_snapcache_read of all keys (read/6: cached base at "
+                           "q=0.5, materialize/4, write-back); cache rebuilt between steps, untimed; HIP-event "
+                           "timing of each step",
+                   "base": args.base},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config, workload),
-                     "kernel": "k_stream" if single else "am_materialize (all tiers: k_stream, k_rows, k_grp_*, k_sets, k_big_*)",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config if args.base == "fresh" else args.config + "_cached", workload),
+                     "kernel": ("am_snapcache_read (select + materialize tiers + store)" if args.base == "cached"
+                                else "k_stream" if single else
+                                "am_materialize (all tiers: k_stream, k_rows, k_grp_*, k_sets, k_big_*)"),
                      "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "layout": "packed (u32 commit vectors relative to a per-key time base); set effects as u32 token-group records"
@@ -351,10 +461,12 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, p, budget_s=args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(cfg, p, budget_s=args.cpu_budget, cached=args.base == "cached")
     if rank == 0:
         print(json.dumps(out), flush=True)
     mat.L.am_comm_destroy(comm)
+    if cache[0] is not None:
+        mat.L.am_snapcache_destroy(cache[0])
     store.close()
     mat.close()
     if pg is not None:
