@@ -131,6 +131,9 @@ SIGNATURES = [
     ("am_gst_allreduce", c_int, [c_void_p, c_void_p, c_uint32]),
     ("am_gst_finalize", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                                 c_void_p]),
+    ("am_gst_local_min_host", c_int, [c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("am_gst_merge_lanes_host", c_int, [c_uint32, c_void_p, c_void_p]),
+    ("am_gst_finalize_host", c_int, [c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     ("am_key_partition", c_uint32, [c_int64, c_uint32]),
     ("am_key_partition_bytes", c_uint32, [c_void_p, c_uint64, c_int, c_uint32]),
     ("am_chash_key", c_int, [c_void_p, c_uint64, c_void_p]),

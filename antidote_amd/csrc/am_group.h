@@ -503,9 +503,12 @@ constexpr int VRPT = 8;                    // records per lane per chunk (512 pe
 // starts with no dependent global load (key -> key_off / records / time base / output range)
 constexpr uint32_t WB = 32;
 struct WSlot {
-  uint64_t off0, rk0, ooff, K, idb;
-  uint32_t r, nops, nrec, G, ocap, _pad;
+  uint64_t off0, rk0, ooff, K, idb, boff;
+  uint32_t r, nops, nrec, G, ocap, nb;
 };
+// base-snapshot reads (cached AW / MV bases): at most KB base pairs and KB new survivors,
+// merged in LDS (the survivor list area; see k_grp_wave step 4b)
+constexpr uint32_t KB = 120;
 struct WaveSmem {
   uint32_t born[VG / 32], killed[VG / 32];
   uint32_t incl[VWORDS];
@@ -517,6 +520,159 @@ struct WaveSmem {
 template <int DMAX, bool PACKED>
 constexpr int vopl() {
   return PACKED ? (AMK_VOPL8 && DMAX <= 8 ? 8 : DMAX <= 8 ? 4 : DMAX <= 16 ? 2 : 1) : (DMAX < 8 ? 4 : DMAX <= 16 ? 2 : 1);
+}
+
+// A read the wave kernel can take with its base snapshot: no base pairs, or at most KB of
+// them and TxId ignore (an op of the reading transaction is a candidate even when the base
+// holds it, and re-applying it duplicates tokens outside the closed form)
+__device__ __forceinline__ bool base_ok(const am_op_log &L, const am_read_batch &B, uint64_t r) {
+  if (!has_base_pairs(B, r)) return true;
+  const bool txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+  return !txid && B.base.set_len[r] <= KB;
+}
+
+// key order of the merge: AW elem (a); MV (value, token) (a, b)
+template <int TYPE>
+__device__ __forceinline__ bool key_lt(uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1) {
+  return TYPE == AM_AWSET ? a0 < a1 : (a0 < a1 || (a0 == a1 && b0 < b1));
+}
+
+// The group of a base pair (AW (elem, token); MV token, under its value or ~0 when the log
+// holds no birth of it), or ~0u.  Groups are ordered AW: elem, then newest birth first, unborn
+// last; MV: (value | ~0, token).
+template <int TYPE>
+__device__ __forceinline__ uint32_t base_group(const am_op_log &L, uint64_t rk0, uint32_t G, uint64_t a, uint64_t b) {
+  auto ga = [&](uint32_t g) { return L.grp[2 * (rk0 + g)]; };
+  auto gb = [&](uint32_t g) { return L.grp[2 * (rk0 + g) + 1]; };
+  if (TYPE == AM_AWSET) {
+    uint32_t lo = 0, hi = G;  // first group with elem >= a
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ga(mid) < a) lo = mid + 1;
+      else hi = mid;
+    }
+    for (uint32_t g = lo; g < G; g += 4) {  // the elem's groups, four loads in flight
+      u64x2 q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = g + k < G ? *(const u64x2 *)(L.grp + 2 * (rk0 + g + k)) : u64x2{~0ull, 0};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (q[k].x != a) return ~0u;
+        if (q[k].y == b) return g + k;
+      }
+    }
+    return ~0u;
+  }
+  for (int pass = 0; pass < 2; ++pass) {  // (value, token), then (~0, token)
+    const uint64_t ka = pass ? ~0ull : a;
+    uint32_t lo = 0, hi = G;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint64_t x = ga(mid), y = gb(mid);
+      if (x < ka || (x == ka && y < b)) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < G && ga(lo) == ka && gb(lo) == b) return lo;
+  }
+  return ~0u;
+}
+
+// Step 4b of k_grp_wave: the read's value from a cached base.  materialize/4 folds the
+// included candidates (ops not in the base, src/clocksi_materializer.erl:216-268) over the
+// base state in log order; in closed form (causal logs: a remove follows the add it observed)
+//   AW  per elem: [new tokens alive, newest first] ++ [base tokens not killed]   (ToAdd ++ (Current -- ToRemove))
+//   MV  sorted union of the new pairs alive and the base pairs not overridden   (insert_sorted)
+// where a base token is killed by an included candidate kill of its group (the builder keeps
+// the kills of groups with no birth in the log: tokens a base holds from pruned ops).  The
+// new survivors (<= KB) and the base pairs (<= KB) are listed in LDS (keys only) and each
+// output position is its rank in its own list plus a binary-search count in the other.
+// Returns false (nothing written) when the new survivors exceed KB.
+template <int TYPE>
+__device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_result &R, WaveSmem &s, uint64_t rk0,
+                           uint32_t G, uint32_t nb, uint64_t boff, uint64_t ooff, uint32_t ocap, uint32_t lane,
+                           uint32_t &nout, int32_t &status) {
+  const uint32_t nwd = (G + 31) / 32;
+  const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
+  const uint32_t c = (uint32_t)__popc(aw);
+  const uint32_t inc = wave_incl_scan_u32(c, lane);
+  const uint32_t ns = (uint32_t)__shfl((int)inc, 63, WAVE);
+  if (ns > KB) return false;
+  // LDS: the survivor list area holds list[KB] u16 | nka[KB] nkb[KB] bka[KB] bkb[KB] u64
+  uint16_t *list = s.list;
+  uint64_t *nka = reinterpret_cast<uint64_t *>(s.list + KB), *nkb = nka + KB, *bka = nkb + KB, *bkb = bka + KB;
+  static_assert(KB * 2 + 4 * KB * 8 <= VG * 2 && (KB * 2) % 8 == 0, "base-merge lists fit the survivor list area");
+  uint64_t *balive = reinterpret_cast<uint64_t *>(s.incl);  // 2 words: base pairs alive
+  {
+    uint32_t o = inc - c;
+    for (uint32_t bits = aw; bits; bits &= bits - 1) list[o++] = (uint16_t)(lane * 32 + __builtin_ctz(bits));
+  }
+  wave_sync();
+  // new survivors' pairs (lanes i, i + 64) and keys
+  u64x2 np[2] = {{0, 0}, {0, 0}};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = lane + 64u * h;
+    if (i < ns) {
+      np[h] = *(const u64x2 *)(L.grp + 2 * (rk0 + list[i]));
+      nka[i] = np[h].x, nkb[i] = np[h].y;
+    }
+  }
+  // base pairs (lanes j, j + 64): alive unless an included candidate killed their group
+  u64x2 bp[2] = {{0, 0}, {0, 0}};
+  uint64_t am[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t jb = lane + 64u * h;
+    bool alive = false;
+    if (jb < nb) {
+      bp[h].x = B.base.set_a[boff + jb], bp[h].y = B.base.set_b[boff + jb];
+      bka[jb] = bp[h].x, bkb[jb] = bp[h].y;
+      const uint32_t g = base_group<TYPE>(L, rk0, G, bp[h].x, bp[h].y);
+      alive = g == ~0u || !((s.killed[g >> 5] >> (g & 31)) & 1u);
+    }
+    am[h] = __ballot(alive);
+  }
+  if (lane == 0) balive[0] = am[0], balive[1] = am[1];
+  const uint32_t nbs = (uint32_t)(__popcll(am[0]) + __popcll(am[1]));
+  wave_sync();
+  nout = ns + nbs;
+  if (nout > ocap) {
+    status = AM_ERR_CAPACITY;
+    return true;
+  }
+  // alive base pairs among the first x
+  auto alive_below = [&](uint32_t x) -> uint32_t {
+    const uint64_t a0 = balive[0], a1 = balive[1];
+    if (x <= 64) return (uint32_t)__popcll(x == 64 ? a0 : (a0 & ((1ull << x) - 1ull)));
+    return (uint32_t)__popcll(a0) + (uint32_t)__popcll(x - 64 == 64 ? a1 : (a1 & ((1ull << (x - 64)) - 1ull)));
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = lane + 64u * h;
+    if (i < ns) {  // + alive base pairs with a smaller key (AW ties: the new tokens first)
+      uint32_t lo = 0, hi = nb;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (key_lt<TYPE>(bka[mid], bkb[mid], np[h].x, np[h].y)) lo = mid + 1;
+        else hi = mid;
+      }
+      const uint64_t o = ooff + i + alive_below(lo);
+      R.value.set_a[o] = np[h].x, R.value.set_b[o] = np[h].y;
+    }
+    const uint32_t jb = lane + 64u * h;
+    if (jb < nb && ((am[h] >> lane) & 1ull)) {  // + new survivors with a key not above it
+      uint32_t lo = 0, hi = ns;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (!key_lt<TYPE>(bp[h].x, bp[h].y, nka[mid], nkb[mid])) lo = mid + 1;
+        else hi = mid;
+      }
+      const uint64_t o = ooff + alive_below(jb) + lo;
+      R.value.set_a[o] = bp[h].x, R.value.set_b[o] = bp[h].y;
+    }
+  }
+  wave_sync();
+  return true;
 }
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
@@ -551,8 +707,9 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       rr = mm.r;
       if (mm.st != AM_OK) {
         R.status[mm.r] = mm.st, R.flags[mm.r] = 0;
-      } else if (mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || has_base_pairs(B, mm.r) ||
-                 (short_opl && mm.G <= 64 && mm.off1 - (mm.off0 & ~(uint64_t)(short_opl - 1)) <= 64)) {
+      } else if (mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || !base_ok(L, B, mm.r) ||
+                 (short_opl && mm.G <= 64 && mm.off1 - (mm.off0 & ~(uint64_t)(short_opl - 1)) <= 64 &&
+                  !has_base_pairs(B, mm.r))) {
         hand = true;  // (short_opl: a short read the lane tier takes next)
       } else {
         elig = true;
@@ -563,6 +720,9 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
         w.idb = L.key_id_base ? L.key_id_base[mm.key] : 1;
         w.r = (uint32_t)mm.r, w.nops = (uint32_t)(mm.off1 - mm.off0), w.nrec = (uint32_t)(mm.rk1 - mm.rk0);
         w.G = mm.G, w.ocap = o1 - o0 < 0xFFFFFFFFull ? (uint32_t)(o1 - o0) : 0xFFFFFFFFu;
+        const bool hb = has_base_pairs(B, mm.r);
+        w.nb = hb ? B.base.set_len[mm.r] : 0u;
+        w.boff = hb ? B.base.set_off[mm.r] : 0;
       }
     }
     const uint64_t hm = __ballot(hand);
@@ -672,7 +832,18 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       //      2048 = 64 words): a scan of the popcounts places every survivor, the group ids
       //      are listed in LDS and the pairs gathered 128 at a time, all loads in flight ----
       uint32_t ns = 0;
-      if (status == AM_OK && !(AMK_SKIP & 2)) {
+      const uint32_t nb = uniform_u32(s.slot[j].nb);
+      if (nb && status == AM_OK) {
+        // 4b. a cached base (vector_orddict snapshot): merge its pairs not killed by an
+        //     included candidate with the new survivors (base_merge); a read that outgrows the
+        //     LDS lists goes to the next tier untouched
+        if (!base_merge<TYPE>(L, B, R, s, rk0, G, nb, uniform_u64(s.slot[j].boff), uniform_u64(s.slot[j].ooff),
+                              uniform_u32(s.slot[j].ocap), lane, ns, status)) {
+          if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
+          wave_sync();
+          continue;
+        }
+      } else if (status == AM_OK && !(AMK_SKIP & 2)) {
         const uint32_t nwd = (G + 31) / 32;
         const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
         const uint32_t c = (uint32_t)__popc(aw);

@@ -169,14 +169,16 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
     grp[2 * (r0 + j) + 1] = TYPE == AM_AWSET ? s.tok[s.rep[rg]] : s.kb[j];
   }
   __syncthreads();
-  // records; a kill is EFFECTIVE only after its group's birth (a kill in the birth's own op
-  // or before it never removes the token, and a group without a birth is never output):
-  // the others become empty slots (0xFFFFFFFF)
+  // records; a kill of a born group is EFFECTIVE only after the birth (a kill in the birth's
+  // own op or before it never removes the token): the others become empty slots
+  // (0xFFFFFFFF).  Kills of a group with no birth in the log are kept: such a group is never
+  // output from the log alone, but a cached base snapshot may hold its token (born by an op
+  // pruned since), which an included kill removes (k_grp_wave's base merge)
   for (uint32_t r = tid; r < n; r += BLOCK) {
     const uint32_t g = s.grpof[r], b = s.bfirst[g];
     const uint32_t op = s.info[r] & 0xFFFFu;
     const bool kill = (s.info[r] & KILL31) != 0;
-    const bool keep = !kill || (b != 0xFFFFFFFFu && op > (s.info[b] & 0xFFFFu));
+    const bool keep = !kill || b == 0xFFFFFFFFu || op > (s.info[b] & 0xFFFFu);
     rec_g[r0 + r] = keep ? (op | ((kill ? 1u : 0u) << 16) | (s.fin[g] << 17)) : 0xFFFFFFFFu;
   }
   if (tid == 0) ngrp[k] = G;

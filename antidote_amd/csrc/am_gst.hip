@@ -23,9 +23,11 @@ namespace {
 
 constexpr uint64_t ABSENT = ~0ull;
 
-__global__ void k_gst_local_min(uint32_t n_dc, uint32_t n_part, const uint64_t *vc, const uint32_t *pres,
-                                const uint8_t *undef, uint64_t *lanes) {
-  const uint32_t d = threadIdx.x;
+// The per-DC steps, shared by the kernels and their CPU twins (am_gst_*_host): one source for
+// the device path and the host path the multi-process tests drive.
+// get_min_time/1 over one node's partitions, DC d (src/stable_time_functions.erl:51-85)
+__host__ __device__ inline uint64_t local_min_dc(uint32_t d, uint32_t n_dc, uint32_t n_part, const uint64_t *vc,
+                                                 const uint32_t *pres, const uint8_t *undef) {
   bool any_undef = false, present = false;
   uint64_t m = ABSENT;
   for (uint32_t p = 0; p < n_part; ++p) {
@@ -33,19 +35,19 @@ __global__ void k_gst_local_min(uint32_t n_dc, uint32_t n_part, const uint64_t *
       any_undef = true;
       continue;
     }
-    if (d < n_dc && ((pres[p] >> d) & 1u)) {
+    if ((pres[p] >> d) & 1u) {
       const uint64_t t = vc[(uint64_t)p * n_dc + d];
       m = (present && m <= t) ? m : t;   // PrevTime >= Time -> store Time
       present = true;
     }
   }
-  if (d < n_dc) lanes[d] = present ? (any_undef ? 0 : m) : ABSENT;
-  if (d == 0) lanes[n_dc] = 1;
+  return present ? (any_undef ? 0 : m) : ABSENT;
 }
 
-__global__ void k_gst_finalize(uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres, int gr,
-                               uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed) {
-  if (threadIdx.x != 0) return;
+// meta_data_sender:update_stable/3 with update_func_min/2 (src/meta_data_sender.erl:342-356,
+// src/stable_time_functions.erl:42-48), then the gr broadcast (src/dc_utilities.erl:259-277)
+__host__ __device__ inline void finalize(uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres,
+                                         int gr, uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed) {
   const bool undef = lanes[n_dc] == 0;
   uint32_t lp = *last_pres;
   bool ch = false;
@@ -66,6 +68,18 @@ __global__ void k_gst_finalize(uint32_t n_dc, const uint64_t *lanes, uint64_t *l
     if ((lp >> d) & 1u) gmin = last_vc[d] < gmin ? last_vc[d] : gmin;
   for (uint32_t d = 0; d < n_dc; ++d) out_vc[d] = ((lp >> d) & 1u) ? (gr ? gmin : last_vc[d]) : 0;
   *out_pres = lp;
+}
+
+__global__ void k_gst_local_min(uint32_t n_dc, uint32_t n_part, const uint64_t *vc, const uint32_t *pres,
+                                const uint8_t *undef, uint64_t *lanes) {
+  const uint32_t d = threadIdx.x;
+  if (d < n_dc) lanes[d] = local_min_dc(d, n_dc, n_part, vc, pres, undef);
+  if (d == 0) lanes[n_dc] = 1;
+}
+
+__global__ void k_gst_finalize(uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres, int gr,
+                               uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed) {
+  if (threadIdx.x == 0) finalize(n_dc, lanes, last_vc, last_pres, gr, out_vc, out_pres, changed);
 }
 
 }  // namespace
@@ -133,6 +147,27 @@ int am_comm_destroy(am_comm *c) {
   if (!c) return AM_OK;
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
+  return AM_OK;
+}
+
+int am_gst_local_min_host(uint32_t n_dc, uint32_t n_part, const uint64_t *part_vc, const uint32_t *part_pres,
+                          const uint8_t *part_undef, uint64_t *lanes) {
+  if (!lanes || n_dc > AM_MAX_DC || (n_part && (!part_vc || !part_pres))) return AM_ERR_INVALID;
+  for (uint32_t d = 0; d < n_dc; ++d) lanes[d] = local_min_dc(d, n_dc, n_part, part_vc, part_pres, part_undef);
+  lanes[n_dc] = 1;
+  return AM_OK;
+}
+
+int am_gst_merge_lanes_host(uint32_t n_dc, const uint64_t *in, uint64_t *inout) {
+  if (!in || !inout || n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  for (uint32_t d = 0; d <= n_dc; ++d) inout[d] = in[d] < inout[d] ? in[d] : inout[d];  // ncclMin on ncclUint64
+  return AM_OK;
+}
+
+int am_gst_finalize_host(uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres, int gr,
+                         uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed) {
+  if (!lanes || !last_vc || !last_pres || !out_vc || !out_pres || n_dc > AM_MAX_DC) return AM_ERR_INVALID;
+  finalize(n_dc, lanes, last_vc, last_pres, gr, out_vc, out_pres, changed);
   return AM_OK;
 }
 

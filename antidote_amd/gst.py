@@ -53,3 +53,56 @@ def allreduce_lanes(lanes: np.ndarray, group=None) -> np.ndarray:
 def owned_partitions(n_partitions: int, rank: int, world: int) -> Sequence[int]:
     """riak_core partition p is served by GPU p mod N (one process per GPU)."""
     return [p for p in range(n_partitions) if p % world == rank]
+
+
+# ---- the C-ABI host twins of the device GST path (am_gst_*_host, one source with the kernels)
+def local_min_host(table: Dict[int, Optional[Dict[int, int]]], n_dc: int) -> np.ndarray:
+    """am_gst_local_min_host over a node's partitions {partition: dict | UNDEFINED} -> lanes."""
+    from . import abi
+    parts = sorted(table)
+    vc = np.zeros((max(len(parts), 1), n_dc), np.uint64)
+    pres = np.zeros(max(len(parts), 1), np.uint32)
+    undef = np.zeros(max(len(parts), 1), np.uint8)
+    for i, p in enumerate(parts):
+        d = table[p]
+        if d is UNDEFINED or d == "undefined":  # None, or the oracle's atom
+            undef[i] = 1
+            continue
+        for dc, t in d.items():
+            vc[i, dc] = t
+            pres[i] |= np.uint32(1 << dc)
+    lanes = np.zeros(n_dc + 1, np.uint64)
+    abi.check(abi.lib().am_gst_local_min_host(n_dc, len(parts), vc.ctypes.data, pres.ctypes.data, undef.ctypes.data,
+                                              lanes.ctypes.data), "am_gst_local_min_host")
+    return lanes
+
+
+def merge_host(lanes: np.ndarray, into: np.ndarray, n_dc: int) -> np.ndarray:
+    """am_gst_merge_lanes_host: the all-reduce's element-wise min of two nodes' lanes."""
+    from . import abi
+    out = np.ascontiguousarray(into, np.uint64).copy()
+    a = np.ascontiguousarray(lanes, np.uint64)
+    abi.check(abi.lib().am_gst_merge_lanes_host(n_dc, a.ctypes.data, out.ctypes.data), "am_gst_merge_lanes_host")
+    return out
+
+
+class StableHost:
+    """meta_data_sender's stable state for one node (am_gst_finalize_host): the monotone update
+    of the merged lanes, and the snapshot a reader gets (gr: min broadcast to every DC)."""
+
+    def __init__(self, n_dc: int):
+        self.n_dc = n_dc
+        self.last_vc = np.zeros(n_dc, np.uint64)
+        self.last_pres = np.zeros(1, np.uint32)
+
+    def update(self, lanes: np.ndarray, gr: bool = False):
+        from . import abi
+        out = np.zeros(self.n_dc, np.uint64)
+        pres = np.zeros(1, np.uint32)
+        ch = np.zeros(1, np.uint8)
+        ln = np.ascontiguousarray(lanes, np.uint64)
+        abi.check(abi.lib().am_gst_finalize_host(self.n_dc, ln.ctypes.data, self.last_vc.ctypes.data,
+                                                 self.last_pres.ctypes.data, 1 if gr else 0, out.ctypes.data,
+                                                 pres.ctypes.data, ch.ctypes.data), "am_gst_finalize_host")
+        snap = {d: int(out[d]) for d in range(self.n_dc) if (int(pres[0]) >> d) & 1}
+        return bool(ch[0]), snap

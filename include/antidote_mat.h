@@ -173,7 +173,8 @@ typedef struct am_op_log {
    * reference's output order: AW by elem, then newest birth first (ToAdd ++ Current), MV by
    * (Value, Token) (insert_sorted); groups without a birth last.  One u32 record per
    * birth / EFFECTIVE kill (one that follows its group's birth: a kill in the birth's own op
-   * or earlier never removes the token), a key's records contiguous and in op order,
+   * or earlier never removes the token; every kill of a group with no birth in the log, whose
+   * token only a cached base can hold), a key's records contiguous and in op order,
    * [rec_key_off[k], rec_key_off[k+1]):
    *   rec_g = op index within the key (bits 0-15) | kill << 16 | group << 17, or 0xFFFFFFFF
    *           for a kill slot that is not effective
@@ -437,6 +438,16 @@ int am_gst_allreduce(am_comm *comm, uint64_t *lanes, uint32_t n_dc);
 int am_gst_finalize(am_ctx *ctx, uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc,
                     uint32_t *last_pres, int gr, uint64_t *out_vc, uint32_t *out_pres,
                     uint8_t *changed);
+
+/* CPU twins of am_gst_local_min / the all-reduce's element-wise min / am_gst_finalize, compiled
+ * from the same per-DC code as the kernels (am_gst.hip): host pointers, no device.  A node
+ * whose GST merge runs on the host (and the multi-process tests, which exchange lanes over
+ * gloo) gets the device path's exact encoding and rules. */
+int am_gst_local_min_host(uint32_t n_dc, uint32_t n_part, const uint64_t *part_vc, const uint32_t *part_pres,
+                          const uint8_t *part_undef, uint64_t *lanes);
+int am_gst_merge_lanes_host(uint32_t n_dc, const uint64_t *in, uint64_t *inout);  /* inout = min(in, inout), n_dc+1 lanes */
+int am_gst_finalize_host(uint32_t n_dc, const uint64_t *lanes, uint64_t *last_vc, uint32_t *last_pres, int gr,
+                         uint64_t *out_vc, uint32_t *out_pres, uint8_t *changed);
 
 /* ---- sharding ---- */
 /* 0-based partition position for integer keys: abs(K) rem n_partitions. */

@@ -1,6 +1,9 @@
-"""world_size-2 gloo tests of the multi-GPU layout (CPU): partition ownership, key
-sharding, and the GST node-level exchange (lane encoding + MIN all-reduce) against the
-reference's two-level get_min_time (src/meta_data_sender.erl:237-245)."""
+"""world_size-2/4 gloo tests of the multi-GPU layout (CPU): partition ownership, key sharding,
+and the GST node-level exchange against the reference's two-level get_min_time + update_stable
+(src/meta_data_sender.erl:237-245, 342-356).  The GST path goes through the C ABI's host twins
+of the device kernels (am_gst_local_min_host / am_gst_merge_lanes_host / am_gst_finalize_host,
+one source with k_gst_local_min / ncclMin / k_gst_finalize in am_gst.hip); gloo carries the
+lanes between the processes as RCCL does between GPUs."""
 import os
 import random
 import socket
@@ -22,9 +25,9 @@ def _port():
     return p
 
 
-def _scenario(seed, world):
+def _scenario(seed, world, n_dc=None):
     rng = random.Random(seed)
-    n_dc = rng.randint(1, 5)
+    n_dc = rng.randint(1, 5) if n_dc is None else n_dc
     table = {}
     for p in range(N_PART):
         r = rng.random()
@@ -36,6 +39,7 @@ def _scenario(seed, world):
 
 
 def _worker(rank, world, port, seed, q):
+    import torch
     import torch.distributed as dist
 
     from antidote_amd import gst
@@ -43,43 +47,57 @@ def _worker(rank, world, port, seed, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        n_dc, table = _scenario(seed, world)
-        mine = gst.owned_partitions(N_PART, rank, world)
-        local = R.get_min_time({p: table[p] for p in mine})       # this node's merge
-        lanes = gst.encode_node(local, n_dc)
-        merged = gst.decode(gst.allreduce_lanes(lanes), n_dc)
+        stable = None
+        snaps = []
+        for rnd in range(3):  # three GST rounds: the monotone update_stable across rounds
+            n_dc, table = _scenario(seed * 10 + rnd, world, n_dc=1 + seed % 5)
+            if stable is None:
+                stable = gst.StableHost(n_dc)
+            mine = gst.owned_partitions(N_PART, rank, world)
+            lanes = gst.local_min_host({p: table[p] for p in mine}, n_dc)   # this node's merge (C ABI)
+            got = [None] * world
+            dist.all_gather_object(got, lanes.tolist())                     # the RCCL exchange, over gloo
+            merged = np.full(n_dc + 1, gst.ABSENT, np.uint64)
+            for other in got:
+                merged = gst.merge_host(np.asarray(other, np.uint64), merged, n_dc)
+            changed, snap = stable.update(merged, gr=(rnd == 2))
+            snaps.append((gst.decode(merged, n_dc), changed, snap))
         owned = [0] * N_PART
-        for p in mine:
+        for p in gst.owned_partitions(N_PART, rank, world):
             owned[p] = 1
-        import torch
         t = torch.tensor(owned)
         dist.all_reduce(t)
-        q.put((rank, merged, t.tolist()))
+        q.put((rank, snaps, t.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_gst_two_rank_matches_reference_two_level_merge(seed):
-    world = 2
+@pytest.mark.parametrize("world,seed", [(2, 1), (2, 2), (2, 3), (4, 4)])
+def test_gst_multi_rank_matches_reference_two_level_merge(world, seed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, seed, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=180) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    n_dc, table = _scenario(seed, world)
     from antidote_amd import gst
-    # reference: per-node local merge, then get_min_time over the node dicts
-    nodes = {r: R.get_min_time({p: table[p] for p in gst.owned_partitions(N_PART, r, world)})
-             for r in range(world)}
-    expect = R.get_min_time(nodes)
-    for rank, merged, owned in res:
-        assert merged == expect, (rank, merged, expect)
+    # reference: per-node local merge, get_min_time over the node dicts, update_stable against
+    # the previous round's result (update_func_min), gr broadcast in the last round
+    last = {}
+    expect = []
+    for rnd in range(3):
+        n_dc, table = _scenario(seed * 10 + rnd, world, n_dc=1 + seed % 5)
+        nodes = {r: R.get_min_time({p: table[p] for p in gst.owned_partitions(N_PART, r, world)})
+                 for r in range(world)}
+        merged = R.get_min_time(nodes)
+        changed, last = R.update_stable(last, merged)
+        expect.append((merged, changed, R.gst_gr(last) if rnd == 2 else dict(last)))
+    for rank, snaps, owned in res:
+        assert snaps == expect, (rank, snaps, expect)
         assert owned == [1] * N_PART          # every partition served by exactly one rank
 
 
