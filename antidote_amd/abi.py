@@ -57,7 +57,7 @@ class am_op_log(ctypes.Structure):
         ("var_off", c_void_p), ("var_data", c_void_p),
         ("key_tbase", c_void_p), ("pk_vc", c_void_p),
         ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp", c_void_p),
-        ("key_ngrp", c_void_p),
+        ("key_ngrp", c_void_p), ("key_end", c_void_p), ("rec_key_end", c_void_p),
     ]
 
 
@@ -156,8 +156,12 @@ SIGNATURES = [
     ("am_vnode_read_host", c_int, [c_void_p, POINTER(am_read_batch), c_void_p, POINTER(am_read_result)]),
     ("am_vnode_parts", c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     ("am_vnode_key_info", c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
+    ("am_vnode_stats", c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     ("am_store_update", c_int, [c_void_p, c_void_p, POINTER(am_op_log), c_void_p, c_void_p, c_void_p, c_void_p,
                                 POINTER(c_void_p)]),
+    ("am_store_reserve", c_int, [c_void_p, c_void_p, POINTER(c_void_p)]),
+    ("am_store_apply", c_int, [c_void_p, c_void_p, c_uint64, c_void_p, POINTER(am_op_log), c_void_p, c_void_p, c_void_p,
+                               c_void_p, POINTER(c_int)]),
     ("am_read_objects_host", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, POINTER(am_read_batch),
                                      POINTER(am_read_result)]),
     ("am_read_objects_submit", c_int, [c_void_p, c_uint32, c_void_p, c_void_p, POINTER(am_read_batch),
@@ -207,7 +211,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 3:
+        if L.am_abi_version() != 4:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

@@ -1,0 +1,372 @@
+// am_apply.hip -- op-cache ingestion + GC in place, for the keys a batch touches:
+// materializer_vnode:op_insert_gc/3 appends (src/materializer_vnode.erl:622-647) and
+// snapshot_insert_gc/4's prune_ops/2 of one key (:515-604) at O(the touched keys' ops), not a
+// whole-store rebuild.
+//
+// A vnode store keeps room for appends per key (key_end / rec_key_end in am_op_log: the ETS
+// tuple's ListLen slack, :540-560).  am_store_apply:
+//   1. k_view: the touched keys as a log of m keys over the store's OWN op columns (key ranges
+//      and per-key columns gathered; no op is copied);
+//   2. the ordinary rebuild on that view (am_store_update_ex: prune, append with ids
+//      OpCounter+1.., packed view, token-group view) -> a small dense store of the touched keys;
+//   3. k_fit: every touched key still fits its room (ops + one free slot, variable words,
+//      records); one u32 readback.  If a key does not fit nothing is written and the caller
+//      rebuilds the whole store, regrowing every key's room (the reference doubles ListLen);
+//   4. k_writeback, one wave per key: every op column, the packed view under the key's new time
+//      base, the variable words (offsets rebased), the records and group pairs, the key's
+//      header (end, OpCounter, id base, type, flags, group count).
+// Readers take a key's end from key_end (am_kend), so the free slots behind it are never read.
+#include "am_internal.h"
+
+namespace {
+
+constexpr int WAVE_SZ = 64;
+
+struct ViewCols {
+  uint64_t *off, *end, *idb, *ctr;
+  uint8_t *type, *flags;
+};
+
+// per touched key: its range and header in the store -> the view's columns
+__global__ void k_view(am_op_log L, const uint64_t *counter, const uint64_t *keys, uint64_t m, ViewCols V) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    V.off[i] = L.key_off[k];
+    V.end[i] = am_kend(L, k);
+    V.idb[i] = L.key_id_base ? L.key_id_base[k] : 1;
+    V.type[i] = L.key_type[k];
+    V.flags[i] = L.key_flags ? L.key_flags[k] : 0;
+    if (counter) V.ctr[i] = counter[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) V.off[m] = 0;
+}
+
+// thr_vc [n_dc][n_keys] / thr_pres [n_keys] of the store's keys -> [n_dc][m] / [m]
+__global__ void k_thr_gather(const uint64_t *keys, uint64_t m, uint32_t n_dc, uint64_t n_keys, const uint8_t *mask,
+                             const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *omask, uint64_t *ovc,
+                             uint32_t *opres) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    omask[i] = mask[k];
+    opres[i] = thr_pres[k];
+    for (uint32_t d = 0; d < n_dc; ++d) ovc[(uint64_t)d * m + i] = thr_vc[(uint64_t)d * n_keys + k];
+  }
+}
+
+__device__ __forceinline__ bool set_type(uint32_t t) { return t == AM_AWSET || t == AM_MVREG; }
+
+// does key i of the rebuilt view S fit key keys[i]'s room in L?
+__global__ void k_fit(am_op_log L, am_op_log S, const uint64_t *keys, uint64_t m, uint32_t *nofit) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    const uint64_t c0 = L.key_off[k], c1 = L.key_off[k + 1];
+    const uint64_t s0 = S.key_off[i], s1 = S.key_off[i + 1];
+    bool ok = s1 - s0 + 1 <= c1 - c0;
+    if (ok && L.var_off) ok = (S.var_off ? S.var_off[s1] - S.var_off[s0] : 0) <= L.var_off[c1] - L.var_off[c0];
+    if (ok && L.rec_key_off && S.rec_key_off && set_type(S.key_type[i]))
+      ok = am_rkend(S, i) - S.rec_key_off[i] <= L.rec_key_off[k + 1] - L.rec_key_off[k];
+    if (!ok) atomicOr(nofit, 1u);
+  }
+}
+
+// one wave per touched key: S's key i -> the store's key keys[i]
+__global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter, uint64_t *counter,
+                            const uint64_t *keys, uint64_t m) {
+  const uint32_t lane = threadIdx.x & (WAVE_SZ - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
+  const uint64_t ls = L.snap_stride ? L.snap_stride : L.n_ops, ss = S.snap_stride ? S.snap_stride : S.n_ops;
+  uint8_t *op_meta = const_cast<uint8_t *>(L.op_meta);
+  uint64_t *commit_time = const_cast<uint64_t *>(L.commit_time), *snap_vc = const_cast<uint64_t *>(L.snap_vc);
+  uint64_t *p0 = const_cast<uint64_t *>(L.p0), *p1 = const_cast<uint64_t *>(L.p1);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / WAVE_SZ) + threadIdx.x / WAVE_SZ; i < m; i += waves) {
+    const uint64_t k = keys[i];
+    const uint64_t d0 = L.key_off[k], cap_end = L.key_off[k + 1];
+    const uint64_t s0 = S.key_off[i], n = S.key_off[i + 1] - s0;
+    const uint64_t idb = S.key_id_base ? S.key_id_base[i] : 1;
+    const uint64_t vb = L.var_off ? L.var_off[d0] : 0, sv0 = S.var_off ? S.var_off[s0] : 0;
+    const uint64_t nv = S.var_off ? S.var_off[s0 + n] - sv0 : 0;
+    for (uint64_t j = lane; j < n; j += WAVE_SZ) {
+      const uint64_t p = s0 + j, q = d0 + j;
+      op_meta[q] = S.op_meta[p];
+      commit_time[q] = S.commit_time[p];
+      for (uint32_t d = 0; d < L.n_dc; ++d) snap_vc[(uint64_t)d * ls + q] = S.snap_vc[(uint64_t)d * ss + p];
+      if (L.snap_pres) const_cast<uint32_t *>(L.snap_pres)[q] = S.snap_pres ? S.snap_pres[p] : 0xFFFFFFFFu;
+      if (L.op_txid) const_cast<uint64_t *>(L.op_txid)[q] = S.op_txid ? S.op_txid[p] : ~0ull;
+      if (L.op_id) const_cast<uint64_t *>(L.op_id)[q] = S.op_id ? S.op_id[p] : idb + j;
+      p0[q] = S.p0[p];
+      p1[q] = S.p1 ? S.p1[p] : 0;
+      if (L.pk_vc && S.pk_vc)
+        for (uint32_t d = 0; d < L.n_dc; ++d)
+          const_cast<uint32_t *>(L.pk_vc)[(uint64_t)d * ls + q] = S.pk_vc[(uint64_t)d * ss + p];
+      if (L.var_off) const_cast<uint64_t *>(L.var_off)[q] = vb + (S.var_off ? S.var_off[p] - sv0 : 0);
+    }
+    if (L.var_off) {
+      uint64_t *vo = const_cast<uint64_t *>(L.var_off);
+      for (uint64_t q = d0 + n + lane; q < cap_end; q += WAVE_SZ) vo[q] = vb + nv;  // the free slots
+      uint64_t *vd = const_cast<uint64_t *>(L.var_data);
+      for (uint64_t w = lane; w < nv; w += WAVE_SZ) vd[vb + w] = S.var_data[sv0 + w];
+    }
+    const uint32_t t = S.key_type[i];
+    uint32_t ng = set_type(t) ? 0u : AM_NGRP_NONE;
+    if (L.rec_key_off) {
+      const uint64_t r0 = L.rec_key_off[k];
+      uint64_t nr = 0;
+      if (S.rec_key_off && S.key_ngrp) {
+        const uint64_t sr0 = S.rec_key_off[i];
+        nr = am_rkend(S, i) - sr0;
+        ng = S.key_ngrp[i];
+        uint32_t *rg = const_cast<uint32_t *>(L.rec_g);
+        for (uint64_t r = lane; r < nr; r += WAVE_SZ) rg[r0 + r] = S.rec_g[sr0 + r];
+        uint64_t *gp = const_cast<uint64_t *>(L.grp);
+        const uint32_t ngc = ng == AM_NGRP_NONE ? 0u : ng;
+        for (uint32_t g = lane; g < ngc; g += WAVE_SZ) {
+          gp[2 * (r0 + g)] = S.grp[2 * (sr0 + g)];
+          gp[2 * (r0 + g) + 1] = S.grp[2 * (sr0 + g) + 1];
+        }
+      }
+      if (lane == 0) {
+        const_cast<uint64_t *>(L.rec_key_end)[k] = r0 + nr;
+        const_cast<uint32_t *>(L.key_ngrp)[k] = ng;
+      }
+    }
+    if (lane == 0) {
+      const_cast<uint64_t *>(L.key_end)[k] = d0 + n;
+      if (L.key_tbase) const_cast<uint64_t *>(L.key_tbase)[k] = S.key_tbase ? S.key_tbase[i] : 0;
+      const_cast<uint8_t *>(L.key_type)[k] = (uint8_t)t;
+      if (L.key_flags) const_cast<uint8_t *>(L.key_flags)[k] = S.key_flags ? S.key_flags[i] : 0;
+      if (L.key_id_base) const_cast<uint64_t *>(L.key_id_base)[k] = idb;
+      if (counter) counter[k] = s_counter[i];
+    }
+  }
+}
+
+// dense op ids (key_id_base + position) / "no TxId" words for every used slot of a store
+// that had no such column: the first gap in a key's ids (a GC that kept non-consecutive ops) or
+// the first TxId turns the column on, once, for the whole store
+__global__ void k_fill_ids(am_op_log L, uint64_t *op_id, uint64_t *op_txid) {
+  const uint32_t lane = threadIdx.x & (WAVE_SZ - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
+  for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE_SZ) + threadIdx.x / WAVE_SZ; k < L.n_keys; k += waves) {
+    const uint64_t o0 = L.key_off[k], o1 = am_kend(L, k), idb = L.key_id_base ? L.key_id_base[k] : 1;
+    for (uint64_t p = o0 + lane; p < o1; p += WAVE_SZ) {
+      if (op_id) op_id[p] = idb + (p - o0);
+      if (op_txid) op_txid[p] = ~0ull;
+    }
+  }
+}
+
+unsigned grid_threads(uint64_t n) { return (unsigned)((n + 255) / 256 < 65536 ? ((n + 255) / 256 ? (n + 255) / 256 : 1) : 65536); }
+unsigned grid_waves(uint64_t n) { return (unsigned)((n + 3) / 4 < 65536 ? ((n + 3) / 4 ? (n + 3) / 4 : 1) : 65536); }
+
+}  // namespace
+
+int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_keys, const am_op_log *dev_new,
+                   const uint8_t *d_mask_full, const uint64_t *d_thr_vc_full, const uint32_t *d_thr_pres_full,
+                   uint8_t *d_gc_flags, uint64_t *h_new_len, int *applied) {
+  AM_LOCK(c);
+  *applied = 0;
+  am_op_log &L = st->dev;
+  // in place needs the slack layout with its per-key header columns and OpCounter
+  if (!L.key_end || !L.key_id_base || !st->counter || (L.rec_key_off && !L.rec_key_end) || m == 0) return AM_OK;
+  if (dev_new && (dev_new->n_keys != m || (dev_new->snap_pres && !L.snap_pres) || (dev_new->var_off && !L.var_off)))
+    return AM_OK;
+  AM_HIP(hipSetDevice(c->device));
+  const uint64_t nd = L.n_dc;
+  // scratch: the view's columns, the gathered prune arguments, the fit flag
+  const size_t o_end = am_round_up((m + 1) * 8, 256), o_idb = o_end + am_round_up(m * 8, 256);
+  const size_t o_ctr = o_idb + am_round_up(m * 8, 256), o_type = o_ctr + am_round_up(m * 8, 256);
+  const size_t o_flags = o_type + am_round_up(m, 256), o_mask = o_flags + am_round_up(m, 256);
+  const size_t o_tvc = o_mask + am_round_up(m, 256), o_tpres = o_tvc + am_round_up(nd * m * 8, 256);
+  const size_t o_fit = o_tpres + am_round_up(m * 4, 256), total = o_fit + 256;
+  void *scr = nullptr;
+  if (int rc = am_dev_alloc(c, total, &scr)) return rc;
+  char *b = (char *)scr;
+  ViewCols V{(uint64_t *)b, (uint64_t *)(b + o_end), (uint64_t *)(b + o_idb), (uint64_t *)(b + o_ctr),
+             (uint8_t *)(b + o_type), (uint8_t *)(b + o_flags)};
+  uint8_t *mask = d_mask_full ? (uint8_t *)(b + o_mask) : nullptr;
+  uint64_t *tvc = (uint64_t *)(b + o_tvc);
+  uint32_t *tpres = (uint32_t *)(b + o_tpres), *nofit = (uint32_t *)(b + o_fit);
+  auto done = [&](int rc) {
+    (void)hipStreamSynchronize(c->stream);
+    am_dev_release(c, scr);
+    return rc;
+  };
+  hipLaunchKernelGGL(k_view, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, (const uint64_t *)st->counter, d_keys,
+                     m, V);
+  if (mask)
+    hipLaunchKernelGGL(k_thr_gather, dim3(grid_threads(m)), dim3(256), 0, c->stream, d_keys, m, L.n_dc, L.n_keys,
+                       d_mask_full, d_thr_vc_full, d_thr_pres_full, mask, tvc, tpres);
+  if (hipGetLastError() != hipSuccess || hipMemsetAsync(nofit, 0, 4, c->stream) != hipSuccess) {
+    am_set_error("am_store_apply: view failed");
+    return done(AM_ERR_HIP);
+  }
+  am_op_log view = L;  // the touched keys over the store's own op columns
+  view.n_keys = m;
+  view.key_off = V.off, view.key_end = V.end, view.key_id_base = V.idb, view.key_type = V.type, view.key_flags = V.flags;
+  view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
+  am_store *sub = nullptr;
+  int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
+                              false, nullptr, &sub);
+  if (rc) return done(rc);
+  const am_op_log &S = sub->dev;
+  bool cols = !(S.snap_pres && !L.snap_pres) && !(S.var_off && !L.var_off) && !(L.pk_vc && !S.pk_vc) &&
+              !(S.rec_key_off && !L.rec_key_off);
+  if (cols && ((S.op_id && !L.op_id) || (S.op_txid && !L.op_txid))) {  // turn the column on (O(store), once)
+    const size_t na = L.snap_stride ? L.snap_stride : L.n_ops;
+    void *ids = nullptr, *tx = nullptr;
+    if (S.op_id && !L.op_id && !rc) rc = am_dev_alloc(c, na * 8 + 8, &ids);
+    if (S.op_txid && !L.op_txid && !rc) rc = am_dev_alloc(c, na * 8 + 8, &tx);
+    if (!rc && L.n_keys)
+      hipLaunchKernelGGL(k_fill_ids, dim3(grid_waves(L.n_keys)), dim3(256), 0, c->stream, L, (uint64_t *)ids,
+                         (uint64_t *)tx);
+    if (!rc && hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
+    if (rc) {
+      am_dev_release(c, ids);
+      am_dev_release(c, tx);
+      am_store_destroy(sub);
+      return done(rc);
+    }
+    if (ids) st->allocs.push_back(ids), L.op_id = (const uint64_t *)ids;
+    if (tx) st->allocs.push_back(tx), L.op_txid = (const uint64_t *)tx;
+  }
+  uint64_t fit = 0;
+  if (cols) {
+    hipLaunchKernelGGL(k_fit, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, S, d_keys, m, nofit);
+    if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
+    uint64_t w = 0;
+    if (!rc) rc = am_ctx_fetch(c, nofit, 1, &w);
+    fit = (w & 0xFFFFFFFFull) == 0;
+  }
+  if (!rc && fit) {
+    hipLaunchKernelGGL(k_writeback, dim3(grid_waves(m)), dim3(256), 0, c->stream, L, S,
+                       (const uint64_t *)sub->counter, st->counter, d_keys, m);
+    if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
+    if (!rc && h_new_len) {
+      std::vector<uint64_t> so(m + 1);
+      if (hipMemcpyAsync(so.data(), S.key_off, (m + 1) * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+          hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = AM_ERR_HIP;
+      for (uint64_t i = 0; !rc && i < m; ++i) h_new_len[i] = so[i + 1] - so[i];
+    }
+    if (!rc) *applied = 1;
+  }
+  if (rc == AM_ERR_HIP) am_set_error("am_store_apply: device pass failed");
+  rc = done(rc);
+  am_store_destroy(sub);
+  return rc;
+}
+
+namespace {
+__global__ void k_key_lens(am_op_log L, const uint64_t *keys, uint64_t m, const uint8_t *flags_full, uint64_t *len,
+                           uint8_t *flags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    len[i] = am_kend(L, k) - L.key_off[k];
+    if (flags_full) flags[i] = flags_full[k];
+  }
+}
+}  // namespace
+
+// the op counts of keys[0..m) (device list) and, if flags_full [n_keys] is given, their entries
+// -> host arrays
+int am_store_key_lens(am_ctx *c, const am_store *st, uint64_t m, const uint64_t *d_keys, const uint8_t *flags_full,
+                      uint64_t *h_len, uint8_t *h_flags) {
+  AM_LOCK(c);
+  if (m == 0) return AM_OK;
+  void *scr = nullptr;
+  if (int rc = am_dev_alloc(c, m * 9 + 64, &scr)) return rc;
+  uint64_t *len = (uint64_t *)scr;
+  uint8_t *fl = (uint8_t *)scr + m * 8;
+  hipLaunchKernelGGL(k_key_lens, dim3(grid_threads(m)), dim3(256), 0, c->stream, st->dev, d_keys, m, flags_full, len,
+                     fl);
+  bool ok = hipGetLastError() == hipSuccess &&
+            hipMemcpyAsync(h_len, len, m * 8, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+            (!flags_full || hipMemcpyAsync(h_flags, fl, m, hipMemcpyDeviceToHost, c->stream) == hipSuccess) &&
+            hipStreamSynchronize(c->stream) == hipSuccess;
+  am_dev_release(c, scr);
+  if (!ok) {
+    am_set_error("am_store_key_lens failed");
+    return AM_ERR_HIP;
+  }
+  return AM_OK;
+}
+
+namespace {
+// the store's keys [0, n_old) and new empty keys [n_old, n_new) as one view's key columns
+__global__ void k_grow_view(am_op_log L, const uint64_t *counter, uint64_t n_new, uint64_t *off, uint64_t *end,
+                            uint64_t *idb, uint64_t *ctr, uint8_t *type, uint8_t *flags) {
+  const uint64_t n_old = L.n_keys, tail = L.key_off[n_old];
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= n_new; k += (uint64_t)gridDim.x * blockDim.x) {
+    const bool old = k < n_old;
+    off[k] = old ? L.key_off[k] : tail;
+    if (k == n_new) continue;
+    end[k] = old ? am_kend(L, k) : tail;
+    idb[k] = old ? (L.key_id_base ? L.key_id_base[k] : 1) : 1;
+    ctr[k] = old ? (counter ? counter[k] : 0) : 0;
+    type[k] = old ? L.key_type[k] : (uint8_t)AM_PN;
+    flags[k] = old ? (L.key_flags ? L.key_flags[k] : 0) : 0;
+  }
+}
+}  // namespace
+
+// a copy of st over n_new >= n_keys keys (the new keys empty: ets:insert of their tuple comes
+// with their first op, src/materializer_vnode.erl:624-629), with room for appends
+int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint64_t *cap_hint, am_store **out) {
+  AM_LOCK(c);
+  const am_op_log &L = st->dev;
+  if (n_new < L.n_keys) return AM_ERR_INVALID;
+  if (!st->counter) {
+    am_set_error("am_store_grow_keys: the store keeps no OpCounter column");
+    return AM_ERR_INVALID;
+  }
+  const size_t o_end = am_round_up((n_new + 1) * 8, 256), o_idb = o_end + am_round_up(n_new * 8, 256);
+  const size_t o_ctr = o_idb + am_round_up(n_new * 8, 256), o_type = o_ctr + am_round_up(n_new * 8, 256);
+  const size_t o_flags = o_type + am_round_up(n_new, 256), total = o_flags + am_round_up(n_new, 256);
+  void *scr = nullptr;
+  if (int rc = am_dev_alloc(c, total, &scr)) return rc;
+  char *b = (char *)scr;
+  am_op_log view = L;
+  view.n_keys = n_new;
+  view.key_off = (uint64_t *)b, view.key_end = (uint64_t *)(b + o_end), view.key_id_base = (uint64_t *)(b + o_idb);
+  view.key_type = (uint8_t *)(b + o_type), view.key_flags = (uint8_t *)(b + o_flags);
+  view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
+  hipLaunchKernelGGL(k_grow_view, dim3(grid_threads(n_new + 1)), dim3(256), 0, c->stream, L,
+                     (const uint64_t *)st->counter, n_new, (uint64_t *)view.key_off, (uint64_t *)view.key_end,
+                     (uint64_t *)view.key_id_base, (uint64_t *)(b + o_ctr), (uint8_t *)view.key_type,
+                     (uint8_t *)view.key_flags);
+  int rc = hipGetLastError() == hipSuccess ? AM_OK : AM_ERR_HIP;
+  if (!rc)
+    rc = am_store_update_ex(c, view, (const uint64_t *)(b + o_ctr), nullptr, nullptr, nullptr, nullptr, nullptr, true,
+                            cap_hint, out);
+  (void)hipStreamSynchronize(c->stream);
+  am_dev_release(c, scr);
+  return rc;
+}
+
+extern "C" {
+
+int am_store_reserve(am_ctx *c, const am_store *st, am_store **out) {
+  if (!c || !st || !out) return AM_ERR_INVALID;
+  AM_LOCK(c);
+  AM_HIP(hipSetDevice(c->device));
+  return am_store_update_ex(c, st->dev, st->counter, nullptr, nullptr, nullptr, nullptr, nullptr, true, nullptr, out);
+}
+
+int am_store_apply(am_ctx *c, am_store *st, uint64_t n_touched, const uint64_t *keys, const am_op_log *dev_new,
+                   const uint8_t *prune_mask, const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags,
+                   int *applied) {
+  if (!c || !st || !applied || (n_touched && !keys) || (prune_mask && (!thr_vc || !thr_pres))) return AM_ERR_INVALID;
+  AM_LOCK(c);
+  *applied = 0;
+  if (n_touched == 0) {
+    *applied = 1;
+    return AM_OK;
+  }
+  if (dev_new && (dev_new->n_dc != st->dev.n_dc || !dev_new->key_off)) {
+    am_set_error("am_store_apply: the new-op log must be CSR over the touched keys with the store's n_dc");
+    return AM_ERR_INVALID;
+  }
+  return am_store_apply_ex(c, st, n_touched, keys, dev_new, prune_mask, thr_vc, thr_pres, gc_flags, nullptr, applied);
+}
+
+}  // extern "C"

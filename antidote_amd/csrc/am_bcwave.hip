@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
       status = AM_ERR_INVALID;
     } else {
       off0 = uniform_u64(L.key_off[key]);
-      off1 = uniform_u64(L.key_off[key + 1]);
+      off1 = uniform_u64(am_kend(L, key));
       const uint32_t ktype = uniform_u32(L.key_type[key]);
       const uint32_t kfl = L.key_flags ? uniform_u32(L.key_flags[key]) : 0u;
       if (off1 > off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES))) status = AM_ERR_CORRUPTED_OPS_CACHE;

@@ -106,7 +106,7 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
   for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbig; b += gridDim.x * blockDim.x) {
     const uint64_t r = list[b];
     const uint64_t key = B.key[r];
-    const uint64_t off0 = L.key_off[key], off1 = L.key_off[key + 1];
+    const uint64_t off0 = L.key_off[key], off1 = am_kend(L, key);
     const uint64_t W = L.var_off ? L.var_off[off1] - L.var_off[off0] : 0;
     const uint64_t nbase = B.base.set_off ? B.base.set_len[r] : 0;
     const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);

@@ -488,7 +488,7 @@ __global__ void k_store_relabel(am_op_log L, uint64_t *p0, uint64_t *p1, uint64_
   for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; k < L.n_keys; k += waves) {
     const uint32_t t = L.key_type[k];
     if (t != AM_LWW && t != AM_AWSET && t != AM_MVREG) continue;
-    for (uint64_t p = L.key_off[k] + lane; p < L.key_off[k + 1]; p += 64) {
+    for (uint64_t p = L.key_off[k] + lane; p < am_kend(L, k); p += 64) {
       if (t == AM_LWW) {
         relabel_word(p1 + p, old, nw, n);  // {Ts, Value}: the value
         continue;

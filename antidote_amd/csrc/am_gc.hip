@@ -42,7 +42,23 @@ struct UpdArgs {
   const uint64_t *thr_vc;      // [n_dc][n_keys]
   const uint32_t *thr_pres;    // [n_keys]
   uint64_t *keep_bits;         // [n_ops/64 + 2] survivor bitmap of pruned keys (count -> scatter)
+  uint64_t *used;              // slack layout: [n_keys] ops / [n_keys] var words the key holds
+  uint64_t *vused;             //   (cnt / vcnt then hold the key's capacities); null => exact
+  const uint64_t *cap_hint;    // slack layout: [n_keys] op capacity wanted per key, or null
 };
+
+// Room for appends of a slack store (the ETS tuple's ListLen slack,
+// src/materializer_vnode.erl:540-560): a quarter of the key's ops and at least 4 free slots
+// (one slot always stays free: var_off[key_end] ends the last op's words); variable words in
+// proportion to the key's own words per op.
+__device__ __forceinline__ uint64_t slack_cap(uint64_t n) {
+  const uint64_t room = n / 4 > 4 ? n / 4 : 4;
+  return n + room;
+}
+__device__ __forceinline__ uint64_t slack_vcap(uint64_t n, uint64_t nv, uint64_t cap) {
+  const uint64_t per = n ? (nv + n - 1) / n : 0;
+  return nv + (cap - n) * (per > 2 ? per : 2) + 4;
+}
 
 __device__ __forceinline__ uint32_t lane() { return threadIdx.x & (WAVE_SZ - 1); }
 
@@ -89,7 +105,7 @@ __device__ __forceinline__ uint64_t var_len(const am_op_log &L, uint64_t p) {
 __global__ void k_upd_count(UpdArgs A, uint64_t *cnt, uint64_t *vcnt) {
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
   for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE_SZ) + threadIdx.x / WAVE_SZ; k < A.L.n_keys; k += waves) {
-    const uint64_t o0 = A.L.key_off[k], o1 = A.L.key_off[k + 1];
+    const uint64_t o0 = A.L.key_off[k], o1 = am_kend(A.L, k);
     const bool prune = A.mask && A.mask[k];
     const uint32_t tpres = prune ? A.thr_pres[k] : 0;
     uint64_t kept = 0, vk = 0;
@@ -114,8 +130,17 @@ __global__ void k_upd_count(UpdArgs A, uint64_t *cnt, uint64_t *vcnt) {
       if (A.N.var_off) nv = A.N.var_off[n1] - A.N.var_off[n0];
     }
     if (lane() == 0) {
-      cnt[k] = kept + nn;
-      vcnt[k] = vk + nv;
+      const uint64_t n = kept + nn, v = vk + nv;
+      if (A.used) {
+        uint64_t cap = slack_cap(n);
+        if (A.cap_hint && A.cap_hint[k] > cap) cap = A.cap_hint[k];
+        A.used[k] = n, A.vused[k] = v;
+        cnt[k] = cap;
+        vcnt[k] = slack_vcap(n, v, cap);
+      } else {
+        cnt[k] = n;
+        vcnt[k] = v;
+      }
     }
   }
 }
@@ -156,6 +181,7 @@ struct OutCols {
   uint64_t *op_txid, *op_id, *p0, *p1, *var_off, *var_data;
   uint64_t *key_tbase;          // packed view of the new log (am_packop.h), or null
   uint32_t *pk_vc;
+  uint64_t *key_end;            // slack layout: [n_keys] end of the key's ops, or null
   uint64_t stride;
 };
 
@@ -192,7 +218,7 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
   const uint64_t lt = (1ull << lane()) - 1ull;
   for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE_SZ) + threadIdx.x / WAVE_SZ; k < A.L.n_keys; k += waves) {
-    const uint64_t o0 = A.L.key_off[k], o1 = A.L.key_off[k + 1];
+    const uint64_t o0 = A.L.key_off[k], o1 = am_kend(A.L, k);
     const uint64_t idb = A.L.key_id_base ? A.L.key_id_base[k] : 1;
     const uint64_t counter = A.counter ? A.counter[k]
                              : o1 > o0 ? (A.L.op_id ? A.L.op_id[o1 - 1] : idb + (o1 - o0) - 1)
@@ -279,6 +305,11 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
         vq += wave_bcast(vincl, 63);
       }
     }
+    if (O.key_end) {  // slack: the free slots' var_off all end the key's words
+      const uint64_t cap_end = cnt[k + 1];
+      for (uint64_t p = q + lane(); O.var_off && p < cap_end; p += WAVE_SZ) O.var_off[p] = vq;
+      if (lane() == 0) O.key_end[k] = q;
+    }
     if (lane() == 0) {
       const uint64_t nops_old = o1 - o0;
       const uint32_t otype = A.L.key_type[k];
@@ -311,7 +342,14 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   if (!c) return AM_ERR_INVALID;
   AM_LOCK(c);
   if (!c || !st || !out) return AM_ERR_INVALID;
-  const am_op_log &L = st->dev;
+  return am_store_update_ex(c, st->dev, st->counter, dev_new, prune_mask, thr_vc, thr_pres, gc_flags, false, nullptr,
+                            out);
+}
+
+int am_store_update_ex(am_ctx *c, const am_op_log &L, const uint64_t *counter, const am_op_log *dev_new,
+                       const uint8_t *prune_mask, const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags,
+                       bool slack, const uint64_t *cap_hint, am_store **out) {
+  AM_LOCK(c);
   if (prune_mask && (!thr_vc || !thr_pres)) {
     am_set_error("am_store_update: prune_mask needs thr_vc and thr_pres");
     return AM_ERR_INVALID;
@@ -326,7 +364,7 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
   UpdArgs A{};
   A.L = L;
   if (dev_new) A.N = *dev_new;
-  A.counter = st->counter;
+  A.counter = counter;
   A.mask = prune_mask;
   A.thr_vc = thr_vc;
   A.thr_pres = thr_pres;
@@ -348,7 +386,8 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
     const size_t o_vcnt = am_round_up((nk + 1) * 8, 256), o_gap = o_vcnt + am_round_up((nk + 1) * 8, 256);
     const size_t o_gmax = o_gap + am_round_up(nk + 1, 256), o_tmp = o_gmax + 256;
     const size_t o_keep = o_tmp + am_round_up(tmp_b + 16, 256);
-    const size_t total = o_keep + (prune_mask ? am_round_up((L.n_ops / 64 + 2) * 8, 256) : 0);
+    const size_t o_used = o_keep + (prune_mask ? am_round_up((L.n_ops / 64 + 2) * 8, 256) : 0);
+    const size_t total = o_used + (slack ? 2 * am_round_up(nk * 8 + 8, 256) : 0);
     void *scr = nullptr;
     if (int rc = am_ctx_scratch(c, AM_SCR_GC, total, &scr)) return rc;
     char *b = (char *)scr;
@@ -358,6 +397,9 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
     gap_max = (uint8_t *)(b + o_gmax);
     tmp = b + o_tmp;
     A.keep_bits = prune_mask ? (uint64_t *)(b + o_keep) : nullptr;
+    A.used = slack ? (uint64_t *)(b + o_used) : nullptr;
+    A.cap_hint = slack ? cap_hint : nullptr;
+    A.vused = slack ? (uint64_t *)(b + o_used + am_round_up(nk * 8 + 8, 256)) : nullptr;
   }
   uint64_t tot[2] = {0, 0};
   bool ok = hipMemsetAsync(cnt + nk, 0, 8, c->stream) == hipSuccess &&
@@ -427,6 +469,7 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
     O.pk_vc = (uint32_t *)alloc((size_t)L.n_dc * na * 4, (size_t)L.n_dc * na * 4);  // DC tails zeroed below
   }
   uint64_t *key_off = (uint64_t *)alloc((nk + 1) * 8, (nk + 1) * 8);
+  O.key_end = slack ? (uint64_t *)alloc(nk * 8 + 8, nk * 8) : nullptr;
   for (uint32_t dd = 0; !rc && dd < L.n_dc && na > n_out; ++dd)
     if (hipMemsetAsync(O.snap_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 8, c->stream) != hipSuccess ||
         (O.pk_vc && hipMemsetAsync(O.pk_vc + (uint64_t)dd * na + n_out, 0, (na - n_out) * 4, c->stream) != hipSuccess))
@@ -460,6 +503,7 @@ extern "C" int am_store_update(am_ctx *c, const am_store *st, const am_op_log *d
     return AM_ERR_HIP;
   }
   d.key_off = key_off;
+  d.key_end = O.key_end;
   d.key_id_base = O.key_id_base;
   d.key_type = O.key_type;
   d.key_flags = O.key_flags;

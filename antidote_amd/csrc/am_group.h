@@ -95,14 +95,14 @@ __device__ __forceinline__ void read_meta(const am_op_log &L, const am_read_batc
     return;
   }
   m.off0 = L.key_off[m.key];
-  m.off1 = L.key_off[m.key + 1];
+  m.off1 = am_kend(L, m.key);
   const uint32_t ktype = L.key_type[m.key];
   const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[m.key] : 0u;
   if (m.off1 > m.off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES))) m.st = AM_ERR_CORRUPTED_OPS_CACHE;
   else if (rtype != type) m.st = AM_ERR_INVALID;
   if (m.st != AM_OK) return;
   m.rk0 = L.rec_key_off[m.key];
-  m.rk1 = L.rec_key_off[m.key + 1];
+  m.rk1 = am_rkend(L, m.key);
   m.G = L.key_ngrp[m.key];
 }
 

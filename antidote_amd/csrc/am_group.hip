@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t
   for (uint64_t k = blockIdx.x; k < L.n_keys; k += gridDim.x) {
     const uint32_t type = uniform_u32(L.key_type[k]);
     const uint32_t kfl = L.key_flags ? uniform_u32(L.key_flags[k]) : 0u;
-    const uint64_t off0 = uniform_u64(L.key_off[k]), off1 = uniform_u64(L.key_off[k + 1]);
+    const uint64_t off0 = uniform_u64(L.key_off[k]), off1 = uniform_u64(am_kend(L, k));
     const uint64_t r0 = uniform_u64(rcnt[off0]), r1 = uniform_u64(rcnt[off1]);
     const uint64_t n = r1 - r0;
     const bool set = type == AM_AWSET || type == AM_MVREG;

@@ -71,6 +71,15 @@ struct am_store {
 
 void am_set_error(const char *fmt, ...);
 
+// the end of key k's ops / records (include/antidote_mat.h: key_end / rec_key_end, the room
+// for appends of a vnode store; without them the CSR's next offset)
+__host__ __device__ __forceinline__ uint64_t am_kend(const am_op_log &L, uint64_t k) {
+  return L.key_end ? L.key_end[k] : L.key_off[k + 1];
+}
+__host__ __device__ __forceinline__ uint64_t am_rkend(const am_op_log &L, uint64_t k) {
+  return L.rec_key_end ? L.rec_key_end[k] : L.rec_key_off[k + 1];
+}
+
 #define AM_HIP(call)                                                                  \
   do {                                                                                \
     hipError_t e_ = (call);                                                           \
@@ -126,6 +135,25 @@ int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
                           uint32_t *key_ngrp);
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
+// am_store_update over a log view (am_gc.hip): counter = OpCounter per key or null; slack =>
+// the new store has room for appends (key_end / rec_key_end set, am_store_apply), at least
+// cap_hint[k] op slots for key k when cap_hint (device [n_keys]) is given
+int am_store_update_ex(am_ctx *c, const am_op_log &L, const uint64_t *counter, const am_op_log *dev_new,
+                       const uint8_t *prune_mask, const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags,
+                       bool slack, const uint64_t *cap_hint, am_store **out);
+// in-place ingestion + GC of the m keys d_keys (device list, distinct) of a slack store
+// (am_apply.hip): dev_new = new ops as CSR over the m keys (or null); d_mask_full / thr over the
+// store's n_keys (or null); d_gc_flags [m] receives AM_GC_*; h_new_len [m] (host, or null) the
+// keys' op counts after.  *applied = 0: some key does not fit its room (nothing written) --
+// rebuild the whole store instead.
+int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_keys, const am_op_log *dev_new,
+                   const uint8_t *d_mask_full, const uint64_t *d_thr_vc_full, const uint32_t *d_thr_pres_full,
+                   uint8_t *d_gc_flags, uint64_t *h_new_len, int *applied);
+int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint64_t *cap_hint, am_store **out);  // am_apply.hip
+struct am_snapcache;
+extern "C" int am_snapcache_grow(am_snapcache *c, uint64_t new_n);  // am_snapcache.hip (not exported in the header)
+int am_store_key_lens(am_ctx *c, const am_store *st, uint64_t m, const uint64_t *d_keys, const uint8_t *flags_full,
+                      uint64_t *h_len, uint8_t *h_flags);
 
 // Short-read tier (am_rows.hip): reads with at most short_max ops (and error reads) are
 // materialized by one 16-lane row each.  list/count (set types only): reads the tier

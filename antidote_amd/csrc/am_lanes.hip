@@ -135,8 +135,13 @@ struct LTile {
   uint64_t v0[OPL], v1[OPL];
 };
 
+// waves per SIMD the register allocation must allow (experiment switch; 1 = the compiler's choice)
+#ifndef AMK_LANE_MINW
+#define AMK_LANE_MINW 1
+#endif
+
 template <int DMAX, bool GENERAL>
-__global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+__global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                  am_retry next, uint32_t accept) {
   constexpr int OPL = lopl<DMAX>();
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -164,7 +169,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
         st = AM_ERR_INVALID;
       } else {
         off0 = L.key_off[key];
-        off1 = L.key_off[key + 1];
+        off1 = am_kend(L, key);
         const uint32_t ktype = L.key_type[key];
         const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;
         if (off1 > off0 && (ktype != t || (kfl & AM_KEY_MIXED_TYPES))) st = AM_ERR_CORRUPTED_OPS_CACHE;
@@ -174,7 +179,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane(am_op_log L, am_read_batch B, a
         if (ok && (t == AM_AWSET || t == AM_MVREG)) {
           G = L.key_ngrp[key];
           rk0 = L.rec_key_off[key];
-          rk1 = L.rec_key_off[key + 1];
+          rk1 = am_rkend(L, key);
           ok = G != AM_NGRP_NONE && G <= LGRP && !has_base_pairs(B, r);
         }
         take = ok;

@@ -63,12 +63,28 @@ __device__ __forceinline__ bool op_effects(const am_op_log &L, uint64_t p, uint3
   return set_effects<AM_MVREG>(L, p, meta, 0, sk);
 }
 
+// records reserved per free op slot of a slack store (an AW add with one token and a remove,
+// an MV assign overriding one token); a key whose appends need more is rebuilt
+constexpr uint64_t REC_SLACK = 2;
+
 __global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, uint32_t *pk_vc, uint8_t *op_meta) {
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < L.n_ops; p += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t type = L.key_type[okey[p]];
+    const uint32_t k = okey[p];
+    const uint32_t type = L.key_type[k];
+    const bool setk = type == AM_AWSET || type == AM_MVREG;
+    if (L.key_end && p >= L.key_end[k]) {  // a free slot: room for its records, as many as the
+      uint64_t per = REC_SLACK;            // key's ops average (records <= effect words + 1)
+      if (setk && L.var_off) {
+        const uint64_t o0 = L.key_off[k], e = L.key_end[k];
+        const uint64_t w = e > o0 ? (L.var_off[e] - L.var_off[o0] + (e - o0) - 1) / (e - o0) + 1 : 0;
+        per = w > per ? w : per;
+      }
+      cnt[p] = setk ? per : 0;
+      continue;
+    }
     const uint32_t meta = L.op_meta[p];
     uint64_t c = 0;
-    if ((type == AM_AWSET || type == AM_MVREG) && !(meta & AM_META_BAD)) {
+    if (setk && !(meta & AM_META_BAD)) {
       CountSink cs;
       if (op_effects(L, p, type, meta, cs)) {
         c = cs.n;
@@ -81,9 +97,12 @@ __global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, ui
   }
 }
 
-__global__ void k_rec_key_off(const uint64_t *key_off, uint64_t n_keys, const uint64_t *off, uint64_t *rko) {
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= n_keys; k += (uint64_t)gridDim.x * blockDim.x)
+__global__ void k_rec_key_off(const uint64_t *key_off, const uint64_t *key_end, uint64_t n_keys, const uint64_t *off,
+                              uint64_t *rko, uint64_t *rke) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= n_keys; k += (uint64_t)gridDim.x * blockDim.x) {
     rko[k] = off[key_off[k]];
+    if (key_end && k < n_keys) rke[k] = off[key_end[k]];
+  }
 }
 
 struct MaxOp {
@@ -105,9 +124,9 @@ int build_records(am_store *st) {
   int rc = AM_OK;
   auto cleanup = [&]() {
     (void)hipStreamSynchronize(c->stream);
-    if (okey) (void)hipFree(okey);
-    if (cnt) (void)hipFree(cnt);
-    if (tmp) (void)hipFree(tmp);
+    am_dev_release(c, okey);  // temporaries from the context's caching allocator (stream-ordered reuse)
+    am_dev_release(c, cnt);
+    am_dev_release(c, tmp);
   };
   if (hipcub::DeviceScan::InclusiveScan(nullptr, tmp_b, okey, okey, MaxOp(), n, c->stream) != hipSuccess ||
       hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cnt, cnt, n + 1, c->stream) != hipSuccess) {
@@ -115,8 +134,8 @@ int build_records(am_store *st) {
     return AM_ERR_HIP;
   }
   if (t2 > tmp_b) tmp_b = t2;
-  if (hipMalloc((void **)&okey, n * 4) != hipSuccess || hipMalloc((void **)&cnt, (n + 1) * 8) != hipSuccess ||
-      hipMalloc(&tmp, tmp_b + 16) != hipSuccess) {
+  if (am_dev_alloc(c, n * 4, (void **)&okey) || am_dev_alloc(c, (n + 1) * 8, (void **)&cnt) ||
+      am_dev_alloc(c, tmp_b + 16, &tmp)) {
     cleanup();
     am_set_error("record view: out of device memory");
     return AM_ERR_NOMEM;
@@ -140,17 +159,23 @@ int build_records(am_store *st) {
     return AM_ERR_HIP;
   }
   rc = AM_OK;
-  void *rko = nullptr, *rg = nullptr, *gp = nullptr, *ng = nullptr;
+  void *rko = nullptr, *rke = nullptr, *rg = nullptr, *gp = nullptr, *ng = nullptr;
   rc = am_dev_alloc(c, (d.n_keys + 1) * 8, &rko);
-  if (!rc) st->allocs.push_back(rko), rc = am_dev_alloc(c, (n_rec + 4) * 4, &rg);
+  if (!rc) st->allocs.push_back(rko);
+  if (!rc && d.key_end) {
+    rc = am_dev_alloc(c, (d.n_keys + 1) * 8, &rke);
+    if (!rc) st->allocs.push_back(rke);
+  }
+  if (!rc) rc = am_dev_alloc(c, (n_rec + 4) * 4, &rg);
   if (!rc) st->allocs.push_back(rg), rc = am_dev_alloc(c, (n_rec + 4) * 16, &gp);
   if (!rc) st->allocs.push_back(gp), rc = am_dev_alloc(c, (d.n_keys + 1) * 4, &ng);
   if (!rc) st->allocs.push_back(ng);
   if (!rc) {
-    hipLaunchKernelGGL(k_rec_key_off, dim3(grid_of(d.n_keys + 1)), dim3(256), 0, c->stream, d.key_off, d.n_keys, cnt,
-                       (uint64_t *)rko);
+    hipLaunchKernelGGL(k_rec_key_off, dim3(grid_of(d.n_keys + 1)), dim3(256), 0, c->stream, d.key_off, d.key_end,
+                       d.n_keys, cnt, (uint64_t *)rko, (uint64_t *)rke);
     am_op_log v = d;
     v.rec_key_off = (const uint64_t *)rko;
+    v.rec_key_end = (const uint64_t *)rke;
     rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng);
     if (!rc && (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)) {
       am_set_error("token-group view: build pass failed");
@@ -161,6 +186,7 @@ int build_records(am_store *st) {
   if (rc) return rc;
   d.n_rec = n_rec;
   d.rec_key_off = (const uint64_t *)rko;
+  d.rec_key_end = (const uint64_t *)rke;
   d.rec_g = (const uint32_t *)rg;
   d.grp = (const uint64_t *)gp;
   d.key_ngrp = (const uint32_t *)ng;

@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         st = AM_ERR_INVALID;
       } else {
         off0 = L.key_off[key];
-        off1 = L.key_off[key + 1];
+        off1 = am_kend(L, key);
         const uint32_t ktype = L.key_type[key];
         const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;
         if (off1 > off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES)))

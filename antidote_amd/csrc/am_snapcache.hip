@@ -25,6 +25,8 @@
 // base.bc_off), so a cached base is never copied.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "am_wave.h"
 
 using namespace amk;
@@ -239,7 +241,7 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
     }
     // materialize_snapshot/7: number_of_ops == 0 returns the base; errors and
     // CommitTime == ignore return without caching
-    if (R.status[r] != AM_OK || L.key_off[key + 1] == L.key_off[key] || R.last_ct_ignore[r]) continue;
+    if (R.status[r] != AM_OK || am_kend(L, key) == L.key_off[key] || R.last_ct_ignore[r]) continue;
     const bool sg = should_gc && should_gc[r];
     if (!((R.is_new_ss[r] && S.newest[r] && R.count[r] >= MIN_OP_STORE_SS) || sg)) continue;
     // internal_store_ss/4: ShouldInsert = NewLastOp - first.last_op_id >= MIN_OP_STORE_SS
@@ -364,9 +366,14 @@ uint64_t reserved_words(uint32_t nd) { return (uint64_t)nd * nd + nd + 1; }
 // does not free enough (synchronizes the stream)
 int pool_reserve(am_snapcache *c, uint64_t need) {
   am_ctx *ctx = c->ctx;
-  uint64_t used = 0;
-  int rc = am_ctx_fetch(ctx, c->ctr, 1, &used);
+  uint64_t w[2] = {0, 0};
+  int rc = am_ctx_fetch(ctx, c->ctr, 2, w);
   if (rc) return rc;
+  if (w[1]) {  // an earlier batch found its room missing (k_sc_store did not cache that snapshot)
+    am_set_error("am_snapcache: a snapshot was not cached for lack of value-pool room (pool sizing)");
+    return AM_ERR_NOMEM;
+  }
+  const uint64_t used = w[0];
   if (used + need <= c->pool_cap) return AM_OK;
   const uint64_t ne = c->n_keys * CAP;
   uint64_t *len = nullptr;
@@ -507,6 +514,51 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
     return rc;
   }
   *out = c;
+  return AM_OK;
+}
+
+// a larger key space for the cache (keys [n_keys, new_n) start without a snapshot dict); the
+// pool and every existing entry are kept
+int am_snapcache_grow(am_snapcache *c, uint64_t new_n) {
+  am_ctx *ctx = c->ctx;
+  AM_LOCK(ctx);
+  if (new_n <= c->n_keys) return AM_OK;
+  const uint64_t nd = c->n_dc, ne0 = c->n_keys * CAP, ne = new_n * CAP + 1;
+  std::vector<void *> fresh;
+  int rc = AM_OK;
+  auto grow = [&](void **field, size_t old_b, size_t new_b, int fill) {
+    void *p = nullptr;
+    if (rc || (rc = am_dev_alloc(ctx, new_b, &p))) return;
+    fresh.push_back(p);
+    if (hipMemsetAsync(p, fill, new_b, ctx->stream) != hipSuccess ||
+        (old_b && hipMemcpyAsync(p, *field, old_b, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess))
+      rc = AM_ERR_HIP;
+    *field = p;
+  };
+  void *old[10] = {c->cnt, c->owner, c->vc, c->pres, c->last_op, c->v0, c->v1, c->vflag, c->poff, c->plen};
+  grow((void **)&c->cnt, c->n_keys, new_n + 16, ABSENT);
+  grow((void **)&c->owner, c->n_keys * 4, (new_n + 1) * 4, 0xFF);
+  grow((void **)&c->vc, ne0 * nd * 8, ne * nd * 8, 0);
+  grow((void **)&c->pres, ne0 * 4, ne * 4, 0);
+  grow((void **)&c->last_op, ne0 * 8, ne * 8, 0);
+  grow((void **)&c->v0, ne0 * 8, ne * 8, 0);
+  grow((void **)&c->v1, ne0 * 8, ne * 8, 0);
+  grow((void **)&c->vflag, ne0, ne, 0);
+  grow((void **)&c->poff, ne0 * 8, ne * 8, 0);
+  grow((void **)&c->plen, ne0 * 4, ne * 4, 0);
+  if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
+  if (rc) {
+    for (void *p : fresh) c->allocs.push_back(p);  // freed with the cache
+    am_set_error("am_snapcache_grow failed");
+    return rc;
+  }
+  for (void *p : old) {
+    auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
+    if (it != c->allocs.end()) c->allocs.erase(it);
+    am_dev_release(ctx, p);
+  }
+  for (void *p : fresh) c->allocs.push_back(p);
+  c->n_keys = new_n;
   return AM_OK;
 }
 

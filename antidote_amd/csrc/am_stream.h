@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
         M.st = AM_ERR_INVALID;
       } else {
         M.off0 = L.key_off[key];
-        M.off1 = L.key_off[key + 1];
+        M.off1 = am_kend(L, key);
         if (PACKED) M.K = L.key_tbase[key];
         const uint32_t ktype = L.key_type[key];
         const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;

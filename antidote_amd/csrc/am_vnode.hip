@@ -17,6 +17,7 @@
 // keys), run the triggered keys' GC reads as one batch, prune them (one rebuild), repeat.
 // The host keeps the per-key tuple header (Length, ListLen, OpCounter) the rounds plan with.
 #include <algorithm>
+#include <atomic>
 #include <thread>
 
 #include "am_internal.h"
@@ -48,6 +49,9 @@ struct am_vnode {
   uint64_t *thr_vc = nullptr;   // device [n_dc][n_keys]
   uint32_t *thr_pres = nullptr; // device [n_keys]
   uint8_t *gc_flags = nullptr;  // device [n_keys]
+  uint64_t rebuilds = 0;        // whole-store rebuilds (a key outgrew its room) ...
+  uint64_t applies = 0;         // ... and in-place applies of touched keys
+  std::atomic<int> in_flight{0};  // am_read_objects_submit tickets not yet finished
 };
 
 namespace {
@@ -55,46 +59,138 @@ namespace {
 // the reference's Length of key k
 uint64_t ref_len(const am_vnode *v, uint64_t k) { return v->len[k] + v->quirk[k]; }
 
-// refreshes the Length mirror from the device log
-int pull_lengths(am_vnode *v) {
-  std::vector<uint64_t> ko(v->n_keys + 1);
-  AM_HIP(hipMemcpyAsync(ko.data(), v->st->dev.key_off, (v->n_keys + 1) * 8, hipMemcpyDeviceToHost, v->ctx->stream));
-  AM_HIP(hipStreamSynchronize(v->ctx->stream));
-  for (uint64_t k = 0; k < v->n_keys; ++k) v->len[k] = ko[k + 1] - ko[k];
-  return AM_OK;
-}
-
 int swap_store(am_vnode *v, am_store *ns) {
   am_store_destroy(v->st);
   v->st = ns;
   return AM_OK;
 }
 
-// snapshot_insert_gc's op prune for the keys in gc_mask (thresholds on the device), then
+// a device copy of a host key list (caching allocator; am_dev_release after use)
+struct DevKeys {
+  am_ctx *c;
+  uint64_t *p = nullptr;
+  explicit DevKeys(am_ctx *c_) : c(c_) {}
+  int upload(const std::vector<uint64_t> &keys) {
+    if (int rc = am_dev_alloc(c, keys.size() * 8 + 8, (void **)&p)) return rc;
+    AM_HIP(hipMemcpyAsync(p, keys.data(), keys.size() * 8, hipMemcpyHostToDevice, c->stream));
+    return AM_OK;
+  }
+  ~DevKeys() {
+    if (p) {
+      (void)hipStreamSynchronize(c->stream);
+      am_dev_release(c, p);
+    }
+  }
+};
+
+// per-key op capacity for a rebuild (device [n], am_dev_release after use): room for the tuple's
+// ListLen slots doubled once (snapshot_insert_gc/4's resize, src/materializer_vnode.erl:540-560:
+// Length never exceeds ListLen, and a GC doubles ListLen when the tuple is nearly full), so a
+// key outgrows its room only at its second doubling; keys without a tuple get the default room
+struct CapHint {
+  am_ctx *c;
+  uint64_t *p = nullptr;
+  explicit CapHint(am_ctx *c_) : c(c_) {}
+  int upload(const am_vnode *v, uint64_t n) {
+    std::vector<uint64_t> h(n, 0);
+    for (uint64_t k = 0; k < n && k < v->list_len.size(); ++k)
+      if (v->list_len[k]) h[k] = 2 * v->list_len[k] + 2;
+    if (int rc = am_dev_alloc(c, n * 8 + 8, (void **)&p)) return rc;
+    AM_HIP(hipMemcpyAsync(p, h.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    AM_HIP(hipStreamSynchronize(c->stream));
+    return AM_OK;
+  }
+  ~CapHint() {
+    if (p) {
+      (void)hipStreamSynchronize(c->stream);
+      am_dev_release(c, p);
+    }
+  }
+};
+
+// NewListLen of snapshot_insert_gc/4 (src/materializer_vnode.erl:540-560) for key k
+void resize_list_len(am_vnode *v, uint64_t k) {
+  const uint64_t nl = ref_len(v, k), ll = v->list_len[k];
+  uint64_t nll = ll;
+  if (nl + RESIZE_THRESHOLD > ll) {  // NewLength > ListLen - RESIZE_THRESHOLD
+    nll = ll * 2;
+  } else {
+    const uint64_t half = ll / 2;
+    if (half > OPS_THRESHOLD && half > nl + RESIZE_THRESHOLD) nll = half;
+  }
+  v->list_len[k] = nll;
+}
+
+// snapshot_insert_gc's op prune for `keys` (gc_mask set, thresholds on the device): in place
+// (am_store_apply), or a whole-store rebuild when a key's room no longer fits; then
 // NewListLen by the reference's resize rule
-int prune(am_vnode *v, const std::vector<uint8_t> &mask) {
+int prune(am_vnode *v, const std::vector<uint64_t> &keys) {
+  const uint64_t m = keys.size();
+  DevKeys dk(v->ctx);
+  if (int rc = dk.upload(keys)) return rc;
+  std::vector<uint64_t> nl(m);
+  std::vector<uint8_t> fl(m);
+  int applied = 0;
+  int rc = am_store_apply_ex(v->ctx, v->st, m, dk.p, nullptr, v->gc_mask, v->thr_vc, v->thr_pres, v->gc_flags, nl.data(),
+                          &applied);
+  if (rc) return rc;
+  if (applied) {
+    ++v->applies;
+    AM_HIP(hipMemcpyAsync(fl.data(), v->gc_flags, m, hipMemcpyDeviceToHost, v->ctx->stream));
+    AM_HIP(hipStreamSynchronize(v->ctx->stream));
+  } else {
+    am_store *ns = nullptr;
+    CapHint ch(v->ctx);
+    if ((rc = ch.upload(v, v->n_keys))) return rc;
+    rc = am_store_update_ex(v->ctx, v->st->dev, v->st->counter, nullptr, v->gc_mask, v->thr_vc, v->thr_pres,
+                            v->gc_flags, true, ch.p, &ns);
+    if (rc) return rc;
+    swap_store(v, ns);
+    ++v->rebuilds;
+    rc = am_store_key_lens(v->ctx, v->st, m, dk.p, v->gc_flags, nl.data(), fl.data());
+    if (rc) return rc;
+  }
+  for (uint64_t i = 0; i < m; ++i) {
+    const uint64_t k = keys[i];
+    v->len[k] = nl[i];
+    v->quirk[k] = (fl[i] & AM_GC_PRUNED_ALL) ? 1 : 0;
+    resize_list_len(v, k);
+  }
+  return AM_OK;
+}
+
+// a larger key space (keys [n_keys, new_n) have no tuple yet: ets:insert on their first op,
+// src/materializer_vnode.erl:624-629): the store and snapshot cache grow, the device GC
+// arrays are reallocated, the host mirrors extended
+int grow_keys(am_vnode *v, uint64_t new_n) {
+  if (new_n <= v->n_keys) return AM_OK;
   am_store *ns = nullptr;
-  int rc = am_store_update(v->ctx, v->st, nullptr, v->gc_mask, v->thr_vc, v->thr_pres, v->gc_flags, &ns);
+  CapHint ch(v->ctx);
+  int rc = ch.upload(v, new_n);
+  if (!rc) rc = am_store_grow_keys(v->ctx, v->st, new_n, ch.p, &ns);
   if (rc) return rc;
   swap_store(v, ns);
-  std::vector<uint8_t> fl(v->n_keys);
-  AM_HIP(hipMemcpyAsync(fl.data(), v->gc_flags, v->n_keys, hipMemcpyDeviceToHost, v->ctx->stream));
-  AM_HIP(hipStreamSynchronize(v->ctx->stream));
-  rc = pull_lengths(v);
-  if (rc) return rc;
-  for (uint64_t k = 0; k < v->n_keys; ++k) {
-    if (!mask[k]) continue;
-    v->quirk[k] = (fl[k] & AM_GC_PRUNED_ALL) ? 1 : 0;
-    const uint64_t nl = ref_len(v, k), ll = v->list_len[k];
-    uint64_t nll = ll;
-    if (nl + RESIZE_THRESHOLD > ll) {  // NewLength > ListLen - RESIZE_THRESHOLD
-      nll = ll * 2;
-    } else {
-      const uint64_t half = ll / 2;
-      if (half > OPS_THRESHOLD && half > nl + RESIZE_THRESHOLD) nll = half;
-    }
-    v->list_len[k] = nll;
+  ++v->rebuilds;
+  if ((rc = am_snapcache_grow(v->sc, new_n))) return rc;
+  uint8_t *gm = nullptr, *gf = nullptr;
+  uint64_t *tv = nullptr;
+  uint32_t *tp = nullptr;
+  if (!rc) rc = am_dev_alloc(v->ctx, new_n + 16, (void **)&gm);
+  if (!rc) rc = am_dev_alloc(v->ctx, new_n + 16, (void **)&gf);
+  if (!rc) rc = am_dev_alloc(v->ctx, (size_t)v->n_dc * new_n * 8 + 16, (void **)&tv);
+  if (!rc) rc = am_dev_alloc(v->ctx, new_n * 4 + 16, (void **)&tp);
+  if (rc) {
+    for (void *p : {(void *)gm, (void *)gf, (void *)tv, (void *)tp}) am_dev_release(v->ctx, p);
+    return rc;
   }
+  AM_HIP(hipMemsetAsync(gm, 0, new_n + 16, v->ctx->stream));
+  AM_HIP(hipStreamSynchronize(v->ctx->stream));
+  am_dev_release(v->ctx, v->gc_mask), am_dev_release(v->ctx, v->gc_flags);
+  am_dev_release(v->ctx, v->thr_vc), am_dev_release(v->ctx, v->thr_pres);
+  v->gc_mask = gm, v->gc_flags = gf, v->thr_vc = tv, v->thr_pres = tp;
+  v->len.resize(new_n, 0), v->list_len.resize(new_n, 0), v->counter.resize(new_n, 0);
+  v->quirk.resize(new_n, 0), v->type.resize(new_n, 0);
+  v->n_keys = new_n;
   return AM_OK;
 }
 
@@ -110,35 +206,53 @@ int run_round(void *arg, const am_read_batch *db, am_read_result *dr, const void
 // one round of reads over distinct keys (host arrays), then the GCs they triggered
 int read_round(am_vnode *v, const am_read_batch *hb, const uint8_t *should_gc, am_read_result *hr) {
   ReadArg a{v};
-  std::vector<uint8_t> sg(hb->n_reads, 0);
-  if (should_gc) std::copy(should_gc, should_gc + hb->n_reads, sg.begin());
+  const uint64_t n = hb->n_reads;
+  std::vector<uint8_t> sg(n, 0);
+  if (should_gc) std::copy(should_gc, should_gc + n, sg.begin());
   int rc = am_run_host_batch(v->ctx, v->st, hb, hr, sg.data(), sg.size(), run_round, &a);
   if (rc) return rc;
-  std::vector<uint8_t> mask(v->n_keys);
-  AM_HIP(hipMemcpyAsync(mask.data(), v->gc_mask, v->n_keys, hipMemcpyDeviceToHost, v->ctx->stream));
-  AM_HIP(hipStreamSynchronize(v->ctx->stream));
-  if (std::any_of(mask.begin(), mask.end(), [](uint8_t x) { return x != 0; })) return prune(v, mask);
-  return AM_OK;
+  // the GC mask of the batch's keys only (keys past the vnode's are invalid reads)
+  std::vector<uint64_t> keys;
+  keys.reserve(n);
+  for (uint64_t i = 0; i < n; ++i)
+    if (hb->key[i] < v->n_keys) keys.push_back(hb->key[i]);
+  if (keys.empty()) return AM_OK;
+  DevKeys dk(v->ctx);
+  if ((rc = dk.upload(keys))) return rc;
+  std::vector<uint64_t> lens(keys.size());
+  std::vector<uint8_t> mask(keys.size());
+  rc = am_store_key_lens(v->ctx, v->st, keys.size(), dk.p, v->gc_mask, lens.data(), mask.data());
+  if (rc) return rc;
+  std::vector<uint64_t> gc;
+  for (uint64_t i = 0; i < keys.size(); ++i)
+    if (mask[i]) gc.push_back(keys[i]);
+  return gc.empty() ? AM_OK : prune(v, gc);
 }
 
-// host op log holding, per key k, the ops [beg[k], end[k]) of src (same columns)
+// host op log holding the ops [beg_i, end_i) of source key src_i for every entry i of a list
+// (same columns as src); key i of the slice is the list's entry i
 struct HostSlice {
   am_op_log log{};
   std::vector<uint64_t> key_off, commit_time, snap_vc, op_txid, p0, p1, var_off, var_data;
   std::vector<uint8_t> key_type, key_flags, op_meta;
   std::vector<uint32_t> snap_pres;
-  HostSlice(const am_op_log &s, const std::vector<uint64_t> &beg, const std::vector<uint64_t> &end) {
-    const uint64_t nk = s.n_keys, nd = s.n_dc, ss = s.snap_stride ? s.snap_stride : s.n_ops;
+  HostSlice(const am_op_log &s, const std::vector<uint64_t> &src, const std::vector<uint64_t> &beg,
+            const std::vector<uint64_t> &end) {
+    const uint64_t nk = src.size(), nd = s.n_dc, ss = s.snap_stride ? s.snap_stride : s.n_ops;
     key_off.assign(nk + 1, 0);
-    for (uint64_t k = 0; k < nk; ++k) key_off[k + 1] = key_off[k] + (end[k] - beg[k]);
+    for (uint64_t i = 0; i < nk; ++i) key_off[i + 1] = key_off[i] + (end[i] - beg[i]);
     const uint64_t n = key_off[nk];
-    key_type.assign(s.key_type, s.key_type + nk);
-    if (s.key_flags) key_flags.assign(s.key_flags, s.key_flags + nk);
+    key_type.resize(nk);
+    key_flags.resize(nk);
+    for (uint64_t i = 0; i < nk; ++i) {
+      key_type[i] = s.key_type[src[i]];
+      key_flags[i] = s.key_flags ? s.key_flags[src[i]] : 0;
+    }
     snap_vc.assign(nd * n, 0);
     if (s.var_off) var_off.assign(n + 1, 0);
     uint64_t q = 0;
-    for (uint64_t k = 0; k < nk; ++k)
-      for (uint64_t p = beg[k]; p < end[k]; ++p, ++q) {
+    for (uint64_t i = 0; i < nk; ++i)
+      for (uint64_t p = beg[i]; p < end[i]; ++p, ++q) {
         op_meta.push_back(s.op_meta[p]);
         commit_time.push_back(s.commit_time[p]);
         for (uint64_t d = 0; d < nd; ++d) snap_vc[d * n + q] = s.snap_vc[d * ss + p];
@@ -147,10 +261,11 @@ struct HostSlice {
         p0.push_back(s.p0[p]);
         p1.push_back(s.p1 ? s.p1[p] : 0);
         if (s.var_off) {
-          for (uint64_t i = s.var_off[p]; i < s.var_off[p + 1]; ++i) var_data.push_back(s.var_data[i]);
+          for (uint64_t w = s.var_off[p]; w < s.var_off[p + 1]; ++w) var_data.push_back(s.var_data[w]);
           var_off[q + 1] = var_data.size();
         }
       }
+    op_meta.push_back(0), commit_time.push_back(0), p0.push_back(0), p1.push_back(0);  // non-null when empty
     log.n_dc = s.n_dc;
     log.n_keys = nk;
     log.n_ops = n;
@@ -171,21 +286,55 @@ struct HostSlice {
   }
 };
 
-// appends src's ops [beg[k], end[k)) to every key (ids OpCounter + 1, ...)
-int append(am_vnode *v, const am_op_log &src, const std::vector<uint64_t> &beg, const std::vector<uint64_t> &end) {
-  HostSlice hs(src, beg, end);
-  if (hs.log.n_ops == 0) return AM_OK;
+// appends src's ops [beg_i, end_i) of source key src_i to vnode key keys_i (ids OpCounter +
+// 1, ...): in place, or a whole-store rebuild with the new ops when a key outgrows its room
+int append(am_vnode *v, const am_op_log &src, const std::vector<uint64_t> &keys, const std::vector<uint64_t> &srck,
+           const std::vector<uint64_t> &beg, const std::vector<uint64_t> &end) {
+  if (keys.empty()) return AM_OK;
+  HostSlice hs(src, srck, beg, end);
   am_store *tmp = nullptr;
   int rc = am_store_create(v->ctx, &hs.log, &tmp);
   if (rc) return rc;
-  am_store *ns = nullptr;
-  rc = am_store_update(v->ctx, v->st, &tmp->dev, nullptr, nullptr, nullptr, nullptr, &ns);
+  DevKeys dk(v->ctx);
+  int applied = 0;
+  rc = dk.upload(keys);
+  if (!rc) rc = am_store_apply_ex(v->ctx, v->st, keys.size(), dk.p, &tmp->dev, nullptr, nullptr, nullptr, nullptr, nullptr,
+                               &applied);
   am_store_destroy(tmp);
   if (rc) return rc;
-  swap_store(v, ns);
-  for (uint64_t k = 0; k < v->n_keys; ++k) {
-    v->len[k] += end[k] - beg[k];
-    v->counter[k] += end[k] - beg[k];
+  if (applied) ++v->applies;
+  if (!applied) {  // the new ops as CSR over every vnode key, one rebuild (every key's room regrown)
+    std::vector<uint64_t> all_src(v->n_keys), all_beg(v->n_keys, 0), all_end(v->n_keys, 0);
+    std::vector<uint8_t> tp(v->n_keys, AM_PN);
+    for (uint64_t k = 0; k < v->n_keys; ++k) all_src[k] = k;
+    am_op_log s2 = src;  // key types of untouched keys are never read (no ops)
+    for (uint64_t i = 0; i < keys.size(); ++i) all_beg[keys[i]] = beg[i], all_end[keys[i]] = end[i];
+    // HostSlice reads key_type / key_flags at the source key index: give it a vnode-indexed copy
+    std::vector<uint8_t> kf(v->n_keys, 0);
+    for (uint64_t i = 0; i < keys.size(); ++i) {
+      tp[keys[i]] = src.key_type[srck[i]];
+      kf[keys[i]] = src.key_flags ? src.key_flags[srck[i]] : 0;
+    }
+    s2.key_type = tp.data();
+    s2.key_flags = src.key_flags ? kf.data() : nullptr;
+    HostSlice all(s2, all_src, all_beg, all_end);
+    am_store *t2 = nullptr;
+    rc = am_store_create(v->ctx, &all.log, &t2);
+    if (rc) return rc;
+    am_store *ns = nullptr;
+    CapHint ch(v->ctx);
+    rc = ch.upload(v, v->n_keys);
+    if (!rc)
+      rc = am_store_update_ex(v->ctx, v->st->dev, v->st->counter, &t2->dev, nullptr, nullptr, nullptr, nullptr, true,
+                              ch.p, &ns);
+    am_store_destroy(t2);
+    if (rc) return rc;
+    swap_store(v, ns);
+    ++v->rebuilds;
+  }
+  for (uint64_t i = 0; i < keys.size(); ++i) {
+    v->len[keys[i]] += end[i] - beg[i];
+    v->counter[keys[i]] += end[i] - beg[i];
   }
   return AM_OK;
 }
@@ -214,11 +363,8 @@ struct HostResult {
 };
 
 // op_insert_gc's GC reads: internal_read(Key, Type, Op.snapshot_time, ignore, [], true) for
-// the trigger op trig[k] of every key with one (~0 = none)
-int gc_reads(am_vnode *v, const am_op_log &src, const std::vector<uint64_t> &trig) {
-  std::vector<uint64_t> keys;
-  for (uint64_t k = 0; k < v->n_keys; ++k)
-    if (trig[k] != ~0ull) keys.push_back(k);
+// vnode key keys_i at the trigger op trig_i of the source log
+int gc_reads(am_vnode *v, const am_op_log &src, std::vector<uint64_t> keys, std::vector<uint64_t> trig) {
   const uint64_t nd = v->n_dc, ss = src.snap_stride ? src.snap_stride : src.n_ops;
   const uint32_t all = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
   // the read's value is discarded; a read short of set capacity stored nothing and reruns
@@ -228,8 +374,8 @@ int gc_reads(am_vnode *v, const am_op_log &src, const std::vector<uint64_t> &tri
     std::vector<uint64_t> vc(nd * n);
     std::vector<uint32_t> rp(n);
     for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t k = keys[i], p = trig[k];
-      type[i] = src.key_type[k];
+      const uint64_t p = trig[i];
+      type[i] = v->type[keys[i]];
       rp[i] = src.snap_pres ? (src.snap_pres[p] & all) : all;
       for (uint64_t d = 0; d < nd; ++d) vc[d * n + i] = ((rp[i] >> d) & 1u) ? src.snap_vc[d * ss + p] : 0;
     }
@@ -243,10 +389,53 @@ int gc_reads(am_vnode *v, const am_op_log &src, const std::vector<uint64_t> &tri
     HostResult hr(n, v->n_dc, cap);
     int rc = read_round(v, &b, sg.data(), &hr.r);
     if (rc) return rc;
-    std::vector<uint64_t> again;
+    std::vector<uint64_t> again, again_t;
     for (uint64_t i = 0; i < n; ++i)
-      if (hr.status[i] == AM_ERR_CAPACITY) again.push_back(keys[i]);
+      if (hr.status[i] == AM_ERR_CAPACITY) again.push_back(keys[i]), again_t.push_back(trig[i]);
     keys.swap(again);
+    trig.swap(again_t);
+  }
+  return AM_OK;
+}
+
+// op_insert_gc/3 for the ops [beg_i, end_i) of source key src_i into vnode key keys_i (keys
+// distinct), each key oldest -> newest, in rounds: every key appends up to its next GC trigger
+// (one in-place apply for all of them), the triggered keys' GC reads run as one batch (and
+// prune in place), repeat.  Host work is O(touched keys) per round.
+int insert_keys(am_vnode *v, const am_op_log &h, const std::vector<uint64_t> &keys, const std::vector<uint64_t> &srck,
+                const std::vector<uint64_t> &beg, const std::vector<uint64_t> &end) {
+  const uint64_t m = keys.size();
+  std::vector<uint64_t> pos(beg);
+  std::vector<uint8_t> pending(m, 0);  // the op at pos already ran its GC read
+  std::vector<uint64_t> live;          // entries with ops left
+  for (uint64_t i = 0; i < m; ++i)
+    if (pos[i] < end[i]) live.push_back(i);
+  while (!live.empty()) {
+    // plan: each key appends up to (not including) its next trigger op
+    std::vector<uint64_t> ak, asrc, abeg, aend, tk, tp, next;
+    for (uint64_t i : live) {
+      const uint64_t k = keys[i];
+      if (!v->list_len[k]) v->list_len[k] = OPS_THRESHOLD, v->type[k] = h.key_type[srck[i]];  // ets:insert of a new tuple
+      uint64_t p = pos[i], l = ref_len(v, k), c = v->counter[k];
+      if (pending[i]) ++p, ++l, ++c;  // the trigger op goes in after its GC read
+      uint64_t trig = ~0ull;
+      for (; p < end[i]; ++p, ++l, ++c) {
+        const uint64_t new_id = c + 1;
+        if (l >= v->list_len[k] || new_id % OPS_THRESHOLD == 0) {
+          trig = p;
+          break;
+        }
+      }
+      if (p > pos[i]) ak.push_back(k), asrc.push_back(srck[i]), abeg.push_back(pos[i]), aend.push_back(p);
+      pos[i] = p;
+      pending[i] = 0;
+      if (trig != ~0ull) tk.push_back(k), tp.push_back(trig), pending[i] = 1;
+      if (pos[i] < end[i]) next.push_back(i);
+    }
+    int rc = append(v, h, ak, asrc, abeg, aend);
+    if (rc) return rc;
+    if (!tk.empty() && (rc = gc_reads(v, h, tk, tp))) return rc;
+    live.swap(next);
   }
   return AM_OK;
 }
@@ -285,6 +474,9 @@ int am_vnode_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_vnode **out)
 
 int am_vnode_destroy(am_vnode *v) {
   if (!v) return AM_OK;
+  am_ctx *c = v->ctx;
+  while (v->in_flight.load()) std::this_thread::yield();  // submitted reads finish first
+  std::lock_guard<std::recursive_mutex> lk(c->mu);       // and every call in progress
   if (v->st) am_store_destroy(v->st);
   if (v->sc) am_snapcache_destroy(v->sc);
   if (v->gc_mask) am_dev_free(v->ctx, v->gc_mask);
@@ -298,48 +490,18 @@ int am_vnode_destroy(am_vnode *v) {
 int am_vnode_insert_host(am_vnode *v, const am_op_log *h) {
   if (!v) return AM_ERR_INVALID;
   AM_LOCK(v->ctx);
-  if (!v || !h || h->n_keys != v->n_keys || h->n_dc != v->n_dc || !h->key_off || !h->key_type || !h->op_meta ||
+  if (!v || !h || h->n_keys < v->n_keys || h->n_dc != v->n_dc || !h->key_off || !h->key_type || !h->op_meta ||
       !h->commit_time || !h->p0 || (h->n_ops && !h->snap_vc)) {
-    am_set_error("am_vnode_insert_host: the new ops must be a host log over the vnode's keys");
+    am_set_error("am_vnode_insert_host: the new ops must be a host log over (at least) the vnode's keys");
     return AM_ERR_INVALID;
   }
   AM_HIP(hipSetDevice(v->ctx->device));
-  const uint64_t nk = v->n_keys;
-  std::vector<uint64_t> pos(nk), end(nk);
-  std::vector<uint8_t> pending(nk, 0);  // the op at pos already ran its GC read
-  for (uint64_t k = 0; k < nk; ++k) pos[k] = h->key_off[k], end[k] = h->key_off[k + 1];
-  for (;;) {
-    // plan: each key appends up to (not including) its next trigger op
-    std::vector<uint64_t> seg_end(nk), trig(nk, ~0ull);
-    bool any = false;
-    for (uint64_t k = 0; k < nk; ++k) {
-      if (pos[k] == end[k]) {
-        seg_end[k] = pos[k];
-        continue;
-      }
-      any = true;
-      if (!v->list_len[k]) v->list_len[k] = OPS_THRESHOLD, v->type[k] = h->key_type[k];  // ets:insert of a new tuple
-      uint64_t p = pos[k], l = ref_len(v, k), c = v->counter[k];
-      if (pending[k]) ++p, ++l, ++c;  // the trigger op goes in after its GC read
-      for (; p < end[k]; ++p, ++l, ++c) {
-        const uint64_t new_id = c + 1;
-        if (l >= v->list_len[k] || new_id % OPS_THRESHOLD == 0) {
-          trig[k] = p;
-          break;
-        }
-      }
-      seg_end[k] = p;
-    }
-    if (!any) break;
-    int rc = append(v, *h, pos, seg_end);
-    if (rc) return rc;
-    for (uint64_t k = 0; k < nk; ++k) pos[k] = seg_end[k], pending[k] = 0;
-    rc = gc_reads(v, *h, trig);
-    if (rc) return rc;
-    for (uint64_t k = 0; k < nk; ++k)
-      if (trig[k] != ~0ull) pending[k] = 1;
-  }
-  return AM_OK;
+  if (h->n_keys > v->n_keys)  // keys seen for the first time beyond the key space
+    if (int rc = grow_keys(v, h->n_keys)) return rc;
+  std::vector<uint64_t> keys, beg, end;
+  for (uint64_t k = 0; k < v->n_keys; ++k)
+    if (h->key_off[k + 1] > h->key_off[k]) keys.push_back(k), beg.push_back(h->key_off[k]), end.push_back(h->key_off[k + 1]);
+  return insert_keys(v, *h, keys, keys, beg, end);
 }
 
 int am_vnode_read_host(am_vnode *v, const am_read_batch *hb, const uint8_t *should_gc, am_read_result *hr) {
@@ -431,8 +593,17 @@ int am_vnode_relabel(am_vnode *v, const uint64_t *old_labels, const uint64_t *ne
 
 int am_vnode_parts(am_vnode *v, am_store **st, am_snapcache **sc) {
   if (!v) return AM_ERR_INVALID;
+  AM_LOCK(v->ctx);
   if (st) *st = v->st;
   if (sc) *sc = v->sc;
+  return AM_OK;
+}
+
+int am_vnode_stats(am_vnode *v, uint64_t *rebuilds, uint64_t *in_place) {
+  if (!v) return AM_ERR_INVALID;
+  AM_LOCK(v->ctx);
+  if (rebuilds) *rebuilds = v->rebuilds;
+  if (in_place) *in_place = v->applies;
   return AM_OK;
 }
 
@@ -499,7 +670,11 @@ int am_read_objects_submit(am_vnode *v, uint32_t n_parts, const uint64_t *part_k
   }
   t->b = *hb;
   t->b.key = t->key.data();
-  t->th = std::thread([t, v, hr]() { t->rc = am_vnode_read_host(v, &t->b, nullptr, hr); });
+  v->in_flight.fetch_add(1);
+  t->th = std::thread([t, v, hr]() {
+    t->rc = am_vnode_read_host(v, &t->b, nullptr, hr);
+    v->in_flight.fetch_sub(1);
+  });
   *out = t;
   return AM_OK;
 }

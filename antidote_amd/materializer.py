@@ -84,6 +84,53 @@ class Store:
             if tmp_store is not None:
                 tmp_store.close()
 
+    def reserve(self) -> "Store":
+        """A copy with room for appends per key (am_store_reserve), the layout am_store_apply
+        updates in place."""
+        h = ctypes.c_void_p()
+        abi.check(self.mat.L.am_store_reserve(self.mat.ctx, self.handle, ctypes.byref(h)), "am_store_reserve")
+        return Store(self.mat, h, self.n_dc)
+
+    def apply(self, keys: Sequence[int], new_log: Optional[HostLog] = None, prune: Any = None):
+        """In-place ingestion + GC of the touched keys only (am_store_apply).  new_log: CSR over
+        the touched keys (entry i appends to keys[i]); prune: (mask[n_keys], thr_vc[n_dc][n_keys],
+        thr_pres[n_keys]) host arrays or device buffers.  Returns (applied, gc_flags[len(keys)]);
+        applied False: some key outgrew its room and nothing was written."""
+        import numpy as np
+        L = self.mat.L
+        m = len(keys)
+        bufs: List[_DevBuf] = []
+        tmp_store = None
+        try:
+            kb = _DevBuf.of(self.mat, np.ascontiguousarray(keys, np.uint64))
+            flags = _DevBuf(self.mat, max(m, 1))
+            bufs += [kb, flags]
+            mask = thr = pres = None
+            if prune is not None and isinstance(prune[0], _DevBuf):
+                mask, thr, pres = prune
+            elif prune is not None:
+                mask, thr, pres = (_DevBuf.of(self.mat, np.ascontiguousarray(prune[0], np.uint8)),
+                                   _DevBuf.of(self.mat, np.ascontiguousarray(prune[1], np.uint64)),
+                                   _DevBuf.of(self.mat, np.ascontiguousarray(prune[2], np.uint32)))
+                bufs += [mask, thr, pres]
+            new_dev = None
+            if new_log is not None:
+                tmp_store = self.mat.store(new_log)
+                new_dev = tmp_store.device_log()
+            ap = ctypes.c_int(0)
+            abi.check(L.am_store_apply(self.mat.ctx, self.handle, m, kb.ptr,
+                                       ctypes.byref(new_dev) if new_dev is not None else None,
+                                       mask.ptr if mask else None, thr.ptr if thr else None, pres.ptr if pres else None,
+                                       flags.ptr, ctypes.byref(ap)), "am_store_apply")
+            out = np.zeros(max(m, 1), np.uint8)
+            flags.download(out)
+            return bool(ap.value), out[:m]
+        finally:
+            for b in bufs:
+                b.free()
+            if tmp_store is not None:
+                tmp_store.close()
+
     def relabel(self, old, new):
         """Apply a codec relabel map (Codec.take_relabel) to the store's label words in place."""
         import numpy as np
@@ -115,15 +162,32 @@ class Store:
                "var_off": get(s.var_off, n + 1, np.uint64) if s.var_off else None,
                "var_data": get(s.var_data, int(s.n_var), np.uint64) if s.var_off else None,
                "explicit_op_id": bool(s.op_id)}
+        key_end = get(s.key_end, nk, np.uint64) if s.key_end else key_off[1:]
         if s.op_id:
             out["op_id"] = get(s.op_id, n, np.uint64)
         else:
             idb = get(s.key_id_base, nk, np.uint64) if s.key_id_base else np.ones(nk, np.uint64)
             ids = np.zeros(n, np.uint64)
             for k in range(nk):
-                o0, o1 = int(key_off[k]), int(key_off[k + 1])
+                o0, o1 = int(key_off[k]), int(key_end[k])
                 ids[o0:o1] = np.arange(o1 - o0, dtype=np.uint64) + idb[k]
             out["op_id"] = ids
+        if s.key_end:  # a vnode store's room for appends: the used ops only, as a dense CSR
+            sel = np.concatenate([np.arange(int(key_off[k]), int(key_end[k]), dtype=np.int64) for k in range(nk)]
+                                 + [np.zeros(0, np.int64)])
+            dense_off = np.zeros(nk + 1, np.uint64)
+            dense_off[1:] = np.cumsum((key_end - key_off[:-1]).astype(np.uint64))
+            for c in ("op_meta", "commit_time", "snap_pres", "op_txid", "p0", "p1", "op_id"):
+                if out[c] is not None:
+                    out[c] = out[c][sel]
+            out["snap_vc"] = out["snap_vc"][:, sel]
+            if out["var_off"] is not None:
+                vo, vd = out["var_off"], out["var_data"]
+                words = [vd[int(vo[p]):int(vo[p + 1])] for p in sel]
+                lens = np.array([len(w) for w in words], np.uint64)
+                out["var_off"] = np.concatenate([np.zeros(1, np.uint64), np.cumsum(lens, dtype=np.uint64)])
+                out["var_data"] = np.concatenate(words + [np.zeros(0, np.uint64)]).astype(np.uint64)
+            out["key_off"] = dense_off
         return out
 
     def close(self):
@@ -286,6 +350,7 @@ class Vnode:
         log = HostLog(self.n_dc, ops_by_key, key_types=key_types)
         s = log.as_struct()
         abi.check(self.mat.L.am_vnode_insert_host(self.handle, ctypes.byref(s)), "am_vnode_insert_host")
+        self.n_keys = max(self.n_keys, len(ops_by_key))  # keys past the key space grow it
 
     def read(self, reads: Sequence[Read], should_gc: Optional[Sequence[bool]] = None, set_capacity=None) -> HostBatch:
         """internal_read/7 per read (read.base_* ignored); ('error', AM_ERR_COLD_PATH) for the log path."""
@@ -304,6 +369,12 @@ class Vnode:
                   "am_vnode_key_info")
         return int(a.value), int(b.value), int(c.value)
 
+    def stats(self):
+        """(whole-store rebuilds, in-place applies) of the ops cache's ingestion and GC."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        abi.check(self.mat.L.am_vnode_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "am_vnode_stats")
+        return int(a.value), int(b.value)
+
     def relabel(self, old, new):
         """Apply a codec relabel map (Codec.take_relabel) to the ops cache and snapshot cache."""
         import numpy as np
@@ -316,7 +387,8 @@ class Vnode:
         return st, sc
 
     def store(self) -> Store:
-        """The ops cache as a borrowed Store (valid until the next insert)."""
+        """The ops cache as a borrowed Store: valid until the next insert or read (a read's GC can
+        rebuild the store when a key outgrows its room for appends)."""
         st, _ = self._parts()
         return Store(self.mat, st, self.n_dc, owned=False)
 
@@ -329,6 +401,8 @@ class Vnode:
         L = self.mat.L
         ko = np.zeros(2, np.uint64)
         abi.check(L.am_memcpy_d2h(self.mat.ctx, ko.ctypes.data, d.key_off + key * 8, 16), "am_memcpy_d2h")
+        if d.key_end:
+            abi.check(L.am_memcpy_d2h(self.mat.ctx, ko[1:].ctypes.data, d.key_end + key * 8, 8), "am_memcpy_d2h")
         n = int(ko[1] - ko[0])
         if n == 0:
             return []

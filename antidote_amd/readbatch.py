@@ -16,6 +16,7 @@ keys (get_key_partition's integer branch, am_key_partition); every call runs the
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -26,17 +27,30 @@ from .oplog import HostBatch, Op, Read
 
 
 class PendingRead:
-    """A submitted read_objects call (am_ticket); result() waits for it."""
+    """A submitted read_objects call (am_ticket); result() waits for it.  The worker thread
+    writes into this object's host buffers until the ticket is waited on, so a PendingRead
+    that is dropped (or closed by its reader) waits first."""
 
-    def __init__(self, ticket, hb: HostBatch, keep):
-        self.ticket, self.hb, self.keep, self.rc = ticket, hb, keep, None
+    def __init__(self, ticket, hb: HostBatch, keep, owner=None):
+        self.ticket, self.hb, self.keep, self.rc, self.owner = ticket, hb, keep, None, owner
 
-    def result(self) -> list:
+    def wait(self) -> int:
         if self.rc is None:
             self.rc = abi.lib().am_ticket_wait(self.ticket)
             self.ticket = None
-        abi.check(self.rc, "am_read_objects")
+            if self.owner is not None:
+                self.owner._pending.discard(self)
+        return self.rc
+
+    def result(self) -> list:
+        abi.check(self.wait(), "am_read_objects")
         return [self.hb.result(i) for i in range(self.hb.n)]
+
+    def __del__(self):
+        try:
+            self.wait()
+        except Exception:
+            pass
 
 
 class PartitionedReader:
@@ -60,6 +74,8 @@ class PartitionedReader:
             order += keys
             base.append(base[-1] + len(keys))
         self.part_key_base = np.array(base, np.uint64)
+        # submitted reads not yet waited on: close() waits for them; a dropped one waits in __del__
+        self._pending = weakref.WeakSet()
         self.vnode: Vnode = mat.vnode(n_dc, max(len(order), 1))
         if order:
             self.vnode.insert([list(objects[k][1]) for k in order], [objects[k][0] for k in order])
@@ -84,7 +100,9 @@ class PartitionedReader:
         abi.check(self.mat.L.am_read_objects_submit(self.vnode.handle, self.n_partitions, self.part_key_base.ctypes.data,
                                                     parts.ctypes.data, ctypes.byref(b), ctypes.byref(r),
                                                     ctypes.byref(t)), "am_read_objects_submit")
-        return PendingRead(t, hb, (b, r, parts))
+        pr = PendingRead(t, hb, (b, r, parts), owner=self)
+        self._pending.add(pr)
+        return pr
 
     def read_objects(self, objects: Sequence[Tuple[int, int]], snapshot_time: Dict[int, int],
                      txid: Optional[int] = None) -> list:
@@ -93,6 +111,8 @@ class PartitionedReader:
         return self.submit(objects, snapshot_time, txid).result()
 
     def close(self):
+        for pr in list(self._pending):
+            pr.wait()
         if self.vnode is not None:
             self.vnode.close()
             self.vnode = None

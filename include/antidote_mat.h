@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 3
+#define AM_ABI_VERSION 4
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -191,6 +191,15 @@ typedef struct am_op_log {
   const uint32_t *rec_g;       /* [n_rec]                                            */
   const uint64_t *grp;         /* [n_rec][2], 16-byte aligned: one load per survivor */
   const uint32_t *key_ngrp;    /* [n_keys]                                           */
+  /* Room for appends (the ETS tuple's ListLen slack, src/materializer_vnode.erl:540-560; vnode
+   * stores only, NULL elsewhere).  With key_end set, key k's ops are [key_off[k], key_end[k])
+   * and [key_end[k], key_off[k+1]) is free room that am_store_apply fills in place (always at
+   * least one free slot: var_off[key_end[k]] ends the key's last op's words); with rec_key_end
+   * set, its records are [rec_key_off[k], rec_key_end[k]) with room up to rec_key_off[k+1]
+   * (group g still at grp[2 (rec_key_off[k] + g)]).  Every reader takes a key's end from
+   * key_end when present, else key_off[k+1]. */
+  const uint64_t *key_end;     /* [n_keys] or NULL                                   */
+  const uint64_t *rec_key_end; /* [n_keys] or NULL                                   */
 } am_op_log;
 #define AM_REC_KILL (1u << 16)
 #define AM_REC_OP(m) ((m) & 0xFFFFu)
@@ -360,14 +369,18 @@ int am_snapcache_gc_threshold(am_ctx *ctx, am_snapcache *cache, uint8_t *mask, u
 
 /* ---- one partition's materializer_vnode state: ops cache + snapshot cache ----
  * am_vnode_insert_host runs op_insert_gc/3 (src/materializer_vnode.erl:622-647) for every op
- * of host_ops (a host log over the vnode's n_keys keys, each key's ops oldest -> newest):
+ * of host_ops (a host log over the vnode's keys, each key's ops oldest -> newest; a log over
+ * more keys grows the vnode's key space first -- the new keys' tuples appear with their first
+ * op, :624-629 -- reads of keys past the key space are AM_ERR_INVALID):
  * NewId = OpCounter + 1, and when Length >= ListLen or NewId rem 50 == 0 the GC read
  * internal_read(Key, Type, Op.snapshot_time, ignore, [], true) runs first (store the
  * snapshot, snapshot_insert_gc/4: keep SNAPSHOT_MIN snapshots, prune_ops below their min,
  * resize ListLen); load_ops/2 (:312-319) replays the log through this call.
  * am_vnode_read_host runs internal_read/7 (:371-376) for a host batch (should_gc [n] or
  * NULL), repeated keys served in batch order.  Reads whose dict reaches SNAPSHOT_THRESHOLD
- * GC the same way.  Both block. */
+ * GC the same way.  Both block.  The ops cache keeps room for appends per key: a batch touching
+ * a few keys is applied in place at O(those keys' ops) (am_store_apply); a key that outgrows its
+ * room rebuilds the store once, regrowing every key's room (am_vnode_stats counts both). */
 typedef struct am_vnode am_vnode;
 int am_vnode_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_vnode **out);
 int am_vnode_destroy(am_vnode *v);
@@ -376,6 +389,9 @@ int am_vnode_read_host(am_vnode *v, const am_read_batch *host_batch, const uint8
                        am_read_result *host_res);
 /* the vnode's current store and snapshot cache (borrowed; the store changes on GC) */
 int am_vnode_parts(am_vnode *v, am_store **st, am_snapcache **sc);
+/* ingestion counters: whole-store rebuilds (a key outgrew its room for appends, or the first
+ * insert) and in-place applies of the touched keys (am_store_apply, the common case) */
+int am_vnode_stats(am_vnode *v, uint64_t *rebuilds, uint64_t *in_place);
 /* the ops-cache tuple header of a key: {Length, ListLen} and OpCounter (element 3) */
 int am_vnode_key_info(am_vnode *v, uint64_t key, uint64_t *length, uint64_t *list_len, uint64_t *op_counter);
 
@@ -416,6 +432,23 @@ int am_ticket_wait(am_ticket *t);
 #define AM_OPS_THRESHOLD 50    /* src/materializer_vnode.erl:41 */
 int am_store_update(am_ctx *ctx, const am_store *st, const am_op_log *dev_new, const uint8_t *prune_mask,
                     const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags, am_store **out);
+
+/* In-place ingestion + GC (the vnode's path; src/materializer_vnode.erl:515-647 per touched key).
+ * am_store_reserve: a copy of st whose keys have room for appends (key_end / rec_key_end set: a
+ * quarter of each key's ops and at least 4 free op slots, variable words and records in
+ * proportion), the ETS tuple's ListLen slack (:540-560).  Blocks.
+ * am_store_apply: on a store with room, the same prune + append as am_store_update, for the
+ * n_touched keys keys[] (device, distinct) only, written into their room in place: dev_new is
+ * CSR over the n_touched keys (entry i = keys[i]; or NULL), prune_mask / thr_vc / thr_pres are
+ * over the store's n_keys as in am_store_update (or NULL), gc_flags [n_touched] (device, or
+ * NULL) receives AM_GC_*.  Cost O(the touched keys' ops).  *applied = 0 when some touched key
+ * would outgrow its room (or the store has none): nothing is written, and the caller rebuilds
+ * with am_store_update (+ am_store_reserve).  Readers of the store must not run concurrently
+ * (the context lock serializes library calls).  Blocks. */
+int am_store_reserve(am_ctx *ctx, const am_store *st, am_store **out);
+int am_store_apply(am_ctx *ctx, am_store *st, uint64_t n_touched, const uint64_t *keys, const am_op_log *dev_new,
+                   const uint8_t *prune_mask, const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags,
+                   int *applied);
 
 /* ---- GST (global stable time) ---- */
 /* lanes[0..n_dc-1] = per-DC min over the partitions that have the DC (absent = UINT64_MAX);

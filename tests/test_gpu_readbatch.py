@@ -83,3 +83,36 @@ def test_gpu_read_objects_partitioned():
     finally:
         rd.close()
         mat.close()
+
+
+def test_gpu_read_objects_dropped_and_closed():
+    """A PendingRead dropped before result() waits for its worker (the worker writes into its
+    host buffers until am_ticket_wait), and closing the reader with reads in flight waits for
+    them before the vnode goes away."""
+    import gc
+
+    from antidote_amd.materializer import Materializer
+    from antidote_amd.readbatch import PartitionedReader
+    rng = random.Random(616)
+    n_dc, n_part = 2, 4
+    keys = list(range(40))
+    objects = {}
+    for key in keys:
+        g = KeyGen(rng, randlog.TYPES[key % 4], n_dc, 10)
+        objects[key] = (randlog.TYPES[key % 4], g.ops(rng.choice([1, 8, 60])))
+    mat = Materializer(0)
+    rd = PartitionedReader(mat, n_part, n_dc, objects)
+    try:
+        clock = {d: 10 ** 6 for d in range(n_dc)}
+        req = [(k, objects[k][0]) for k in keys]
+        ref = rd.read_objects(req, clock)
+        for _ in range(4):
+            p = rd.submit(req, clock)
+            del p
+            gc.collect()
+        assert not rd._pending
+        assert rd.read_objects(req, clock) == ref
+        rd.submit(req, clock), rd.submit(req, clock)  # left in flight
+    finally:
+        rd.close()
+        mat.close()
