@@ -65,8 +65,6 @@ class am_values(ctypes.Structure):
     _fields_ = [
         ("v0", c_void_p), ("v1", c_void_p), ("vflag", c_void_p),
         ("set_off", c_void_p), ("set_len", c_void_p), ("set_a", c_void_p), ("set_b", c_void_p),
-        ("bc_p", c_void_p), ("bc_p_pres", c_void_p), ("bc_d", c_void_p), ("bc_d_pres", c_void_p),
-        ("bc_off", c_void_p),
     ]
 
 
@@ -211,7 +209,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 4:
+        if L.am_abi_version() != 5:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

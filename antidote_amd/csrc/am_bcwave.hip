@@ -147,16 +147,14 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
       for (uint32_t k = lane; k < ns; k += WAVE) ovf |= s.hi[k] != ((int64_t)s.lo[k] < 0 ? -1 : 0);
       if (__ballot(ovf)) status = AM_ERR_OVERFLOW;
     }
-    if (status == AM_OK)
-      for (uint32_t k = lane; k < ns; k += WAVE) {
-        if (k < np) {
-          R.value.bc_p[r * np + k] = (int64_t)s.lo[k];
-          R.value.bc_p_pres[r * np + k] = s.pres[k] ? 1 : 0;
-        } else {
-          R.value.bc_d[r * nd + (k - np)] = (int64_t)s.lo[k];
-          R.value.bc_d_pres[r * nd + (k - np)] = s.pres[k] ? 1 : 0;
-        }
-      }
+    uint32_t nent = 0;
+    if (status == AM_OK) {
+      nent = bc_emit<WAVE>(R, r, ns, lane, 0, [&](uint32_t k, int64_t &v) {
+        v = (int64_t)s.lo[k];
+        return s.pres[k] != 0;
+      });
+      if (nent > R.value.set_off[r + 1] - R.value.set_off[r]) status = AM_ERR_CAPACITY;
+    }
     const bool ign = u.base_ignore && count == 0;
     const uint32_t opres = ign ? 0u : (pres | u.cpres);
     if (status == AM_OK && lane < nd) {
@@ -182,6 +180,7 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
         R.last_ct_pres[r] = opres;
         R.is_new_ss[r] = count > 0;
         R.count[r] = count;
+        R.value.set_len[r] = nent;
       }
     }
     wave_sync();  // the slots are rewritten by the wave's next read
@@ -207,8 +206,8 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
 }  // namespace
 
 bool am_bcwave_applies(const am_op_log *L, const am_read_result *R) {
-  return am_log_packed(L) && L->n_dc <= 16 && L->op_meta && R->value.bc_p && R->value.bc_p_pres && R->value.bc_d &&
-         R->value.bc_d_pres;
+  return am_log_packed(L) && L->n_dc <= 16 && L->op_meta && R->value.set_off && R->value.set_len && R->value.set_a &&
+         R->value.set_b;
 }
 
 int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,

@@ -497,18 +497,24 @@ __global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch
         if (SL.hi[q] != ((int64_t)SL.lo[q] < 0 ? -1 : 0)) ovf = 1;
       }
       ovf = (uint32_t)block_red_u64(s.red, wave_or_u32(ovf), 1);
-      if (ovf) status = AM_ERR_OVERFLOW;  // Erlang: a bignum
-      else
-        for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
-          const uint64_t q = (uint64_t)b * SL.ns + i;
-          if (i < np) {
-            R.value.bc_p[r * np + i] = (int64_t)SL.lo[q];
-            R.value.bc_p_pres[r * np + i] = SL.pres[q] ? 1 : 0;
-          } else {
-            R.value.bc_d[r * nd + (i - np)] = (int64_t)SL.lo[q];
-            R.value.bc_d_pres[r * nd + (i - np)] = SL.pres[q] ? 1 : 0;
-          }
+      (void)np;
+      if (ovf) {
+        status = AM_ERR_OVERFLOW;  // Erlang: a bignum
+      } else {
+        if (tid < WAVE) {  // one wave compacts the present slots into the read's CSR range
+          const uint64_t q0 = (uint64_t)b * SL.ns;
+          const uint32_t ne = bc_emit<WAVE>(R, r, SL.ns, tid, 0, [&](uint32_t k, int64_t &v) {
+            v = (int64_t)SL.lo[q0 + k];
+            return SL.pres[q0 + k] != 0;
+          });
+          if (tid == 0) s.ctr[7] = ne;
         }
+        __syncthreads();
+        const uint32_t ne = s.ctr[7];
+        if (ne > R.value.set_off[r + 1] - R.value.set_off[r]) status = AM_ERR_CAPACITY;
+        else if (tid == 0) R.value.set_len[r] = ne;
+        __syncthreads();
+      }
     } else if (status == AM_OK) {
       // count survivors, then gather them (LDS, or the read's kill records as scratch)
       uint32_t alive = 0;

@@ -32,7 +32,6 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
   if (n == 0) return AM_OK;
   const uint32_t nd = st->dev.n_dc;
   const uint64_t nclk = hb->per_read_clock ? n : 1;
-  const uint64_t np = (uint64_t)nd * nd;
   const uint64_t nset_in = hb->base.set_off ? hb->base.set_off[n] : 0;
   const uint64_t nset_out = hr->value.set_off ? hr->value.set_off[n] : 0;
 
@@ -48,7 +47,6 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
   };
   am_read_batch db = *hb;
   am_read_result dr = *hr;
-  db.base.bc_off = nullptr;  // a device-side layout (snapshot-cache bases); host bases use rows
   std::vector<In> ins;
   std::vector<Out> outs;
   auto in = [&](const void *h, size_t bytes, const void **slot) {
@@ -74,10 +72,6 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
   in(hb->base.set_len, n * 4, (const void **)&db.base.set_len);
   in(hb->base.set_a, nset_in * 8, (const void **)&db.base.set_a);
   in(hb->base.set_b, nset_in * 8, (const void **)&db.base.set_b);
-  in(hb->base.bc_p, n * np * 8, (const void **)&db.base.bc_p);
-  in(hb->base.bc_p_pres, n * np, (const void **)&db.base.bc_p_pres);
-  in(hb->base.bc_d, n * nd * 8, (const void **)&db.base.bc_d);
-  in(hb->base.bc_d_pres, n * nd, (const void **)&db.base.bc_d_pres);
   in(hr->value.set_off, (n + 1) * 8, (const void **)&dr.value.set_off);
   const void *extra_dev = nullptr;
   in(extra_host, extra_bytes, &extra_dev);
@@ -96,10 +90,6 @@ static int run_host(am_ctx *c, const am_store *st, const am_read_batch *hb, am_r
   out(hr->value.set_len, n * 4, (void **)&dr.value.set_len);
   out(hr->value.set_a, nset_out * 8, (void **)&dr.value.set_a);
   out(hr->value.set_b, nset_out * 8, (void **)&dr.value.set_b);
-  out(hr->value.bc_p, n * np * 8, (void **)&dr.value.bc_p);
-  out(hr->value.bc_p_pres, n * np, (void **)&dr.value.bc_p_pres);
-  out(hr->value.bc_d, n * nd * 8, (void **)&dr.value.bc_d);
-  out(hr->value.bc_d_pres, n * nd, (void **)&dr.value.bc_d_pres);
   if (!hr->status || !hr->new_last_op || !hr->last_ct || !hr->last_ct_pres || !hr->last_ct_ignore || !hr->is_new_ss ||
       !hr->count || !hr->flags) {
     am_set_error("host batch: every result column is required");

@@ -176,7 +176,7 @@ int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *
 // the batch uses partial clocks, op ids, TxIds, cached bases or per-read clocks
 inline bool am_batch_general(const am_op_log *L, const am_read_batch *B) {
   return L->snap_pres || L->op_id || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock || B->base.v0 ||
-         B->base.set_off || B->base.bc_p || B->base.bc_d || B->base.bc_p_pres || B->base.bc_d_pres;
+         B->base.set_off;
 }
 // the packed streaming view applies (u32 entries relative to the key time base, full clocks)
 inline bool am_log_packed(const am_op_log *L) { return L->key_tbase && L->pk_vc && !L->snap_pres; }

@@ -65,8 +65,15 @@ struct ROut {  // per-lane buffered outputs of read (batch base + lane)
   uint64_t v0, v1;
 };
 
+// waves per SIMD the register allocation must allow (experiment switch; 1 = the compiler's
+// choice).  At D = 16 the compiler takes ~350 VGPRs (one wave per SIMD); asked for two it fits
+// 224 without spilling, but C5's bounded-counter rows then ran 2.1x slower (3.3 -> 7.1 ms)
+#ifndef AMK_ROWS_MINW
+#define AMK_ROWS_MINW 1
+#endif
+
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
-__global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+__global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                 am_rows_cfg C) {
   constexpr bool BC = TYPE == AM_BCOUNTER;
   constexpr bool LDS = BC;
@@ -363,7 +370,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                   pr = bp | ((rs->pres[i >> 5] >> (i & 31)) & 1u);
                 };
                 uint32_t ovf = 0;
-                if (GENERAL && (B.base.bc_p || B.base.bc_d))
+                if (GENERAL && B.base.set_off)
                   for (uint32_t i = sl; i < nslot; i += G) {
                     int64_t hi;
                     uint64_t lo;
@@ -373,20 +380,36 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                   }
                 if (row_or_u32(ovf)) {
                   status = AM_ERR_OVERFLOW;
-                } else {
-                  for (uint32_t i = sl; i < nslot; i += G) {
-                    int64_t hi;
-                    uint64_t lo;
-                    uint32_t pr;
-                    total(i, hi, lo, pr);
-                    if (i < np) {
-                      R.value.bc_p[rj * np + i] = (int64_t)lo;
-                      R.value.bc_p_pres[rj * np + i] = pr ? 1 : 0;
-                    } else {
-                      R.value.bc_d[rj * nd + (i - np)] = (int64_t)lo;
-                      R.value.bc_d_pres[rj * nd + (i - np)] = pr ? 1 : 0;
+                } else {  // the present slots as (slot, value) pairs: the P / D orddicts' entries
+                  // (a slot's place = the present slots below it, popcounts of the row's bitmap)
+                  if (GENERAL && B.base.set_off) {
+                    for (uint32_t i = sl; i < nslot; i += G) {
+                      uint32_t bp = 0;
+                      (void)bc_base(B, rj, np, nd, i, bp);
+                      if (bp) atomicOr(&rs->pres[i >> 5], 1u << (i & 31));
                     }
+                    wave_sync();
                   }
+                  // chunk c = slots [16c, 16c + 16), lane sl slot 16c + sl: the chunk's 16 bits
+                  // are one half of a bitmap word (the same word for the whole row)
+                  const uint64_t so = R.value.set_off[rj], cap = R.value.set_off[rj + 1] - so;
+                  uint32_t ne = 0;
+                  for (uint32_t c = 0; c * G < nslot; ++c) {
+                    const uint32_t bits = (rs->pres[c >> 1] >> ((c & 1u) * 16u)) & 0xFFFFu;
+                    const uint32_t i = c * G + sl;
+                    const uint32_t rank = ne + (uint32_t)__popc(bits & ((1u << sl) - 1u));
+                    if (i < nslot && ((bits >> sl) & 1u) && rank < cap) {
+                      int64_t hi;
+                      uint64_t lo;
+                      uint32_t pr;
+                      total(i, hi, lo, pr);
+                      R.value.set_a[so + rank] = i;
+                      R.value.set_b[so + rank] = lo;
+                    }
+                    ne += (uint32_t)__popc(bits);
+                  }
+                  if (ne > cap) status = AM_ERR_CAPACITY;
+                  v0 = ne;
                 }
               } else if (status == AM_OK && !defer) {
                 const uint32_t ne = rs->ctr[0];
@@ -394,7 +417,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                 if (sl < ne4 - ne) rs->kp[ne + sl] = -1;  // pad the slot list to whole int4 loads
                 // With every |amount| < 2^56 (and no base values) the <= 64 entries of a
                 // slot cannot leave int64: the exact overflow pass is skipped.
-                uint32_t big = (GENERAL && (B.base.bc_p || B.base.bc_d)) ? 1u : 0u;
+                uint32_t big = (GENERAL && B.base.set_off) ? 1u : 0u;
                 for (uint32_t e = sl; e < ne; e += G) {
                   const int64_t x = (int64_t)rs->ka[e];
                   big |= (x >= (1ll << 56) || x < -(1ll << 56)) ? 1u : 0u;
@@ -439,21 +462,18 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
                 }
                 if (big && rs->ctr[2]) {
                   status = AM_ERR_OVERFLOW;
-                } else {  // write the slots
-                  for (uint32_t i = sl; i < nslot; i += G) {
+                } else {  // the present slots as (slot, value) pairs
+                  const uint32_t ne = bc_emit<G>(R, rj, nslot, sl, row * G, [&](uint32_t i, int64_t &x) {
                     uint32_t bpres;
                     const int64_t bv = base_of(i, bpres);
                     int64_t hi = bv < 0 ? -1 : 0;
                     uint64_t lo = (uint64_t)bv;
                     bpres |= slot_sum(i, hi, lo);
-                    if (i < np) {
-                      R.value.bc_p[rj * np + i] = (int64_t)lo;
-                      R.value.bc_p_pres[rj * np + i] = bpres ? 1 : 0;
-                    } else {
-                      R.value.bc_d[rj * nd + (i - np)] = (int64_t)lo;
-                      R.value.bc_d_pres[rj * nd + (i - np)] = bpres ? 1 : 0;
-                    }
-                  }
+                    x = (int64_t)lo;
+                    return bpres != 0;
+                  });
+                  if (ne > R.value.set_off[rj + 1] - R.value.set_off[rj]) status = AM_ERR_CAPACITY;
+                  v0 = ne;
                 }
               }
             }
@@ -511,6 +531,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
         R.is_new_ss[r] = (uint8_t)o.newss;
         R.count[r] = o.count;
         if (TYPE == AM_PN || TYPE == AM_LWW) R.value.v0[r] = (int64_t)o.v0;
+        if (TYPE == AM_BCOUNTER) R.value.set_len[r] = (uint32_t)o.v0;  // the entry count
         if (TYPE == AM_LWW) {
           R.value.v1[r] = o.v1;
           R.value.vflag[r] = (uint8_t)o.vflag;

@@ -291,17 +291,22 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
         if (hi != ((int64_t)lo < 0 ? -1 : 0)) atomicOr(ovf, 1u);
       }
       __syncthreads();
-      if (*ovf) status = AM_ERR_OVERFLOW;
-      else
-        for (uint32_t i = tid; i < np + nd; i += BLOCK) {
-          if (i < np) {
-            R.value.bc_p[r * np + i] = (int64_t)s.slo[i];
-            R.value.bc_p_pres[r * np + i] = s.spres[i] ? 1 : 0;
-          } else {
-            R.value.bc_d[r * nd + (i - np)] = (int64_t)s.slo[i];
-            R.value.bc_d_pres[r * nd + (i - np)] = s.spres[i] ? 1 : 0;
-          }
+      if (*ovf) {
+        status = AM_ERR_OVERFLOW;
+      } else {
+        if (tid < WAVE) {  // one wave compacts the present slots into the read's CSR range
+          const uint32_t ne = bc_emit<WAVE>(R, r, np + nd, tid, 0, [&](uint32_t k, int64_t &v) {
+            v = (int64_t)s.slo[k];
+            return s.spres[k] != 0;
+          });
+          if (tid == 0) *ovf = ne;
         }
+        __syncthreads();
+        const uint32_t ne = *ovf;
+        if (ne > R.value.set_off[r + 1] - R.value.set_off[r]) status = AM_ERR_CAPACITY;
+        else if (tid == 0) R.value.set_len[r] = ne;
+        __syncthreads();
+      }
     }
     if (status == AM_OK && TYPE != AM_BCOUNTER) {
       const uint32_t nk = s.ctr[0], nb = s.ctr[1];
@@ -399,7 +404,7 @@ template <int TYPE>
 int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                 am_retry retry) {
   const bool cols = TYPE == AM_BCOUNTER
-                        ? (R->value.bc_p && R->value.bc_p_pres && R->value.bc_d && R->value.bc_d_pres)
+                        ? (R->value.set_off && R->value.set_len && R->value.set_a && R->value.set_b)
                         : (R->value.set_off && R->value.set_len && R->value.set_a && R->value.set_b);
   if (!cols && S.idx) {
     hipLaunchKernelGGL(k_sets_nocols, dim3(64), dim3(256), 0, ctx->stream, *R, S);
@@ -407,7 +412,7 @@ int launch_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read
     return AM_OK;
   }
   if (!cols) {
-    am_set_error(TYPE == AM_BCOUNTER ? "bcounter results need value.bc_p/bc_p_pres/bc_d/bc_d_pres"
+    am_set_error(TYPE == AM_BCOUNTER ? "bcounter results need value.set_off/set_len/set_a/set_b"
                                      : "set results need value.set_off/set_len/set_a/set_b");
     return AM_ERR_INVALID;
   }

@@ -19,10 +19,10 @@
 //   k_sc_release   frees the key claims
 // Layout: per key a fixed array of CAP entries, newest first (clock [n_dc] + presence,
 // last_op_id, value).  Scalar values (PN counter, LWW register) live in the entry; set
-// values (add-wins set / MV register pairs) and bounded-counter slots live in a value pool
-// (pool_a / pool_b / pool_p words, bump-allocated, compacted on the host side when a batch
-// could overflow it) that the next read's base points into (base.set_off/set_len,
-// base.bc_off), so a cached base is never copied.
+// values (add-wins set / MV register pairs) and bounded-counter (slot, value) entries live in
+// a value pool (pool_a / pool_b words, bump-allocated, compacted on the host side when a batch
+// could overflow it) that the next read's base points into (base.set_off/set_len), so a
+// cached base is never copied.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -81,7 +81,7 @@ struct ScView {  // kernel-side copy of the cache pointers
 // selected bases (scratch, columns of the batch handed to am_materialize)
 struct ScSel {
   uint8_t *code, *newest, *base_ignore, *vflag;
-  uint64_t *base_vc, *v1, *set_off, *bc_off;
+  uint64_t *base_vc, *v1, *set_off;
   uint32_t *base_pres, *set_len;
   int64_t *base_last_op, *v0;
 };
@@ -95,7 +95,6 @@ struct ScGc {
 __device__ __forceinline__ uint64_t clk(const uint64_t *vc, uint32_t pres, uint32_t d) {
   return ((pres >> d) & 1u) ? vc[d] : 0;
 }
-__device__ __forceinline__ uint32_t n_slots(uint32_t nd) { return nd * nd + nd; }
 
 // snapshot_insert_gc/4's prune threshold (src/materializer_vnode.erl:523-527) over the kept
 // entries [s0, s0 + keep) (newest first): Acc = the oldest kept clock, then for every entry
@@ -192,16 +191,16 @@ __global__ void k_sc_select(ScView C, am_read_batch B, ScSel S) {
     S.v1[r] = bv1;
     S.vflag[r] = bvf;
     S.set_off[r] = boff;
-    S.set_len[r] = t == AM_BCOUNTER ? 0u : blen;
-    S.bc_off[r] = t == AM_BCOUNTER && blen ? boff : 0;
+    S.set_len[r] = blen;  // set pairs; bounded counter (slot, value) entries
   }
 }
 
-// value words of read r's result (sets: pairs; bounded counter: every slot), or 0 when the
-// result columns for its type are absent (not cached then)
+// value words of read r's result (set pairs; bounded counter (slot, value) entries), or 0
+// when the result columns are absent (not cached then)
 __device__ __forceinline__ uint32_t value_words(const am_read_result &R, uint64_t r, uint32_t t, uint32_t nd) {
-  if (t == AM_AWSET || t == AM_MVREG) return (R.value.set_len && R.value.set_a && R.value.set_b) ? R.value.set_len[r] : 0u;
-  if (t == AM_BCOUNTER) return (R.value.bc_p && R.value.bc_p_pres && R.value.bc_d && R.value.bc_d_pres) ? n_slots(nd) : 0u;
+  (void)nd;
+  if (t == AM_AWSET || t == AM_MVREG || t == AM_BCOUNTER)
+    return (R.value.set_len && R.value.set_a && R.value.set_b) ? R.value.set_len[r] : 0u;
   return 0;
 }
 
@@ -294,17 +293,8 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
       // the value words into the pool
       if (w) {
-        if (t == AM_BCOUNTER) {
-          const uint32_t q = nd * nd;
-          for (uint32_t i = 0; i < w; ++i) {
-            const bool p = i < q;
-            C.pool_a[off + i] = (uint64_t)(p ? R.value.bc_p[r * q + i] : R.value.bc_d[r * nd + (i - q)]);
-            C.pool_p[off + i] = p ? R.value.bc_p_pres[r * q + i] : R.value.bc_d_pres[r * nd + (i - q)];
-          }
-        } else {
-          const uint64_t so = R.value.set_off[r];
-          for (uint32_t i = 0; i < w; ++i) C.pool_a[off + i] = R.value.set_a[so + i], C.pool_b[off + i] = R.value.set_b[so + i];
-        }
+        const uint64_t so = R.value.set_off[r];
+        for (uint32_t i = 0; i < w; ++i) C.pool_a[off + i] = R.value.set_a[so + i], C.pool_b[off + i] = R.value.set_b[so + i];
       }
       C.poff[s0] = off;
       C.plen[s0] = off ? w : 0;
@@ -633,7 +623,7 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   const uint32_t nd = c->n_dc;
   // value pool room for every value this batch could store
   uint64_t need = 0;
-  if (th == 0 || th == AM_AWSET || th == AM_MVREG) {
+  if (th == 0 || th == AM_AWSET || th == AM_MVREG || th == AM_BCOUNTER) {
     if (R->value.set_off) {
       uint64_t so[2] = {0, 0};
       int rc = am_ctx_fetch(ctx, R->value.set_off, 1, &so[0]);
@@ -642,14 +632,13 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
       need += so[1] - so[0];
     }
   }
-  if ((th == 0 || th == AM_BCOUNTER) && R->value.bc_p) need += n * ((uint64_t)nd * nd + nd);
   if (need) {
     int rc = pool_reserve(c, need);
     if (rc) return rc;
   }
   // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres, set_len [n] u32 |
-  // base_last_op, v0, v1, set_off, bc_off [n] u64 | base_vc [nd][n]
-  const size_t bytes = n * (4 + 8 + 5 * 8 + (size_t)nd * 8) + 4096;
+  // base_last_op, v0, v1, set_off [n] u64 | base_vc [nd][n]
+  const size_t bytes = n * (4 + 8 + 4 * 8 + (size_t)nd * 8) + 4096;
   void *scr = nullptr;
   int rc = am_ctx_scratch(ctx, AM_SCR_SNAP, bytes, &scr);
   if (rc) return rc;
@@ -664,7 +653,6 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   S.v0 = (int64_t *)take(n * 8);
   S.v1 = (uint64_t *)take(n * 8);
   S.set_off = (uint64_t *)take(n * 8);
-  S.bc_off = (uint64_t *)take(n * 8);
   S.base_vc = (uint64_t *)take(n * nd * 8);
   S.base_pres = (uint32_t *)take(n * 4);
   S.set_len = (uint32_t *)take(n * 4);
@@ -690,11 +678,6 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
     db.base.set_len = S.set_len;
     db.base.set_a = c->pool_a;
     db.base.set_b = c->pool_b;
-    db.base.bc_off = S.bc_off;    // cached bounded counters: slots in the pool
-    db.base.bc_p = (int64_t *)c->pool_a;
-    db.base.bc_p_pres = c->pool_p;
-    db.base.bc_d = (int64_t *)c->pool_a + (uint64_t)nd * nd;
-    db.base.bc_d_pres = c->pool_p + (uint64_t)nd * nd;
     rc = am_launch_materialize(ctx, L, &db, R);
     if (rc == AM_OK) {
       const ScGc G{gc_mask, thr_vc, thr_pres};

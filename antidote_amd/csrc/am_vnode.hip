@@ -343,22 +343,19 @@ int append(am_vnode *v, const am_op_log &src, const std::vector<uint64_t> &keys,
 struct HostResult {
   am_read_result r{};
   std::vector<int32_t> status;
-  std::vector<int64_t> nlo, v0, bc_p, bc_d;
+  std::vector<int64_t> nlo, v0;
   std::vector<uint64_t> last_ct, v1, set_off, set_a, set_b;
   std::vector<uint32_t> pres, count, set_len;
-  std::vector<uint8_t> ign, newss, flags, vflag, bc_pp, bc_dp;
+  std::vector<uint8_t> ign, newss, flags, vflag;
   HostResult(uint64_t n, uint32_t nd, uint64_t cap)
-      : status(n), nlo(n), v0(n), bc_p(n * nd * nd), bc_d(n * nd), last_ct(n * nd), v1(n), set_off(n + 1),
-        set_a(n * cap + 1), set_b(n * cap + 1), pres(n), count(n), set_len(n), ign(n), newss(n), flags(n), vflag(n),
-        bc_pp(n * nd * nd), bc_dp(n * nd) {
+      : status(n), nlo(n), v0(n), last_ct(n * nd), v1(n), set_off(n + 1),
+        set_a(n * cap + 1), set_b(n * cap + 1), pres(n), count(n), set_len(n), ign(n), newss(n), flags(n), vflag(n) {
     for (uint64_t i = 0; i <= n; ++i) set_off[i] = i * cap;
     r.status = status.data(), r.new_last_op = nlo.data(), r.last_ct = last_ct.data(), r.last_ct_pres = pres.data();
     r.last_ct_ignore = ign.data(), r.is_new_ss = newss.data(), r.count = count.data(), r.flags = flags.data();
     r.value.v0 = v0.data(), r.value.v1 = v1.data(), r.value.vflag = vflag.data();
     r.value.set_off = set_off.data(), r.value.set_len = set_len.data();
     r.value.set_a = set_a.data(), r.value.set_b = set_b.data();
-    r.value.bc_p = bc_p.data(), r.value.bc_p_pres = bc_pp.data(), r.value.bc_d = bc_d.data(),
-    r.value.bc_d_pres = bc_dp.data();
   }
 };
 
@@ -521,7 +518,6 @@ int am_vnode_read_host(am_vnode *v, const am_read_batch *hb, const uint8_t *shou
   }
   const uint32_t rounds = 1 + *std::max_element(occ.begin(), occ.end());
   if (rounds == 1) return read_round(v, hb, should_gc, hr);
-  const uint64_t np = nd * nd;
   for (uint32_t j = 0; j < rounds; ++j) {
     std::vector<uint64_t> sel;
     for (uint64_t i = 0; i < n; ++i)
@@ -572,12 +568,6 @@ int am_vnode_read_host(am_vnode *v, const am_read_batch *hb, const uint8_t *shou
           hr->value.set_b[hr->value.set_off[i] + x] = res.set_b[so[q] + x];
         }
       }
-      if (hr->value.bc_p)
-        for (uint64_t s = 0; s < np; ++s)
-          hr->value.bc_p[i * np + s] = res.bc_p[q * np + s], hr->value.bc_p_pres[i * np + s] = res.bc_pp[q * np + s];
-      if (hr->value.bc_d)
-        for (uint64_t s = 0; s < nd; ++s)
-          hr->value.bc_d[i * nd + s] = res.bc_d[q * nd + s], hr->value.bc_d_pres[i * nd + s] = res.bc_dp[q * nd + s];
     }
   }
   return AM_OK;

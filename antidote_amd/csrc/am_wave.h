@@ -432,16 +432,51 @@ __device__ __forceinline__ uint32_t incl4(const am_op_log &L, uint32_t nd, uint6
 
 // base bounded-counter slot i of read r (P slots i < np, then the nd D slots): row r of the
 // [n][np] / [n][nd] arrays, or at base.bc_off[r] (snapshot-cache bases in the value pool)
+// the base snapshot's bounded-counter entry at slot i (P {From,To} at From*nd+To, D Id at
+// np+Id): its (slot, value) pairs sit in the base CSR sorted by slot -- binary search
 __device__ __forceinline__ int64_t bc_base(const am_read_batch &B, uint64_t r, uint32_t np, uint32_t nd, uint32_t i,
                                            uint32_t &pres) {
-  const bool p = i < np;
-  const uint64_t idx = B.base.bc_off ? B.base.bc_off[r] + (p ? i : i - np) : (p ? r * np + i : r * nd + (i - np));
-  if (p) {
-    pres = B.base.bc_p_pres ? B.base.bc_p_pres[idx] : 0u;
-    return B.base.bc_p ? B.base.bc_p[idx] : 0;
+  (void)np, (void)nd;
+  pres = 0;
+  if (!B.base.set_off || !B.base.set_len) return 0;
+  const uint64_t o = B.base.set_off[r];
+  uint32_t lo = 0, hi = B.base.set_len[r];
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (B.base.set_a[o + mid] < (uint64_t)i) lo = mid + 1;
+    else hi = mid;
   }
-  pres = B.base.bc_d_pres ? B.base.bc_d_pres[idx] : 0u;
-  return B.base.bc_d ? B.base.bc_d[idx] : 0;
+  if (lo < B.base.set_len[r] && B.base.set_a[o + lo] == (uint64_t)i) {
+    pres = 1;
+    return (int64_t)B.base.set_b[o + lo];
+  }
+  return 0;
+}
+
+// A bounded-counter result: the read's present slots as (slot, value) pairs, slot order (the P
+// orddict, then D, each in key order), into its CSR range of the result -- GL lanes of a wave
+// (lane gl of the group, the group's lanes at wave bits [gbit, gbit + GL)), every lane of the
+// group in the call.  get(k, v) -> slot k's presence and value.  Returns the number of present
+// slots; more than the read's capacity: nothing past it is written (AM_ERR_CAPACITY).
+template <int GL, class Get>
+__device__ __forceinline__ uint32_t bc_emit(const am_read_result &R, uint64_t r, uint32_t ns, uint32_t gl,
+                                            uint32_t gbit, Get get) {
+  const uint64_t o = R.value.set_off[r], cap = R.value.set_off[r + 1] - o;
+  const uint64_t gm = GL >= 64 ? ~0ull : ((1ull << GL) - 1ull), lt = (1ull << gl) - 1ull;
+  uint32_t cnt = 0;
+  for (uint32_t k0 = 0; k0 < ns; k0 += GL) {
+    const uint32_t k = k0 + gl;
+    int64_t v = 0;
+    const bool p = k < ns && get(k, v);
+    const uint64_t m = (__ballot(p) >> gbit) & gm;
+    const uint64_t pos = cnt + (uint32_t)__popcll(m & lt);
+    if (p && pos < cap) {
+      R.value.set_a[o + pos] = k;
+      R.value.set_b[o + pos] = (uint64_t)v;
+    }
+    cnt += (uint32_t)__popcll(m);
+  }
+  return cnt;
 }
 
 // ---- per-type value reductions (apply_operations folds of commutative updates) ----

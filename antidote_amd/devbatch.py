@@ -51,18 +51,22 @@ class DeviceReads:
         self.v1 = z(torch.int64, n_reads)
         self.vflag = z(torch.uint8, n_reads)
         self.set_off = self.set_len = self.set_a = self.set_b = None
-        self.bc_p = self.bc_pp = self.bc_d = self.bc_dp = None
         self.set_cap = set_cap
-        if present & {abi.AM_AWSET, abi.AM_MVREG}:
-            self.set_off = torch.arange(0, (n_reads + 1) * set_cap, set_cap, dtype=torch.int64, device=dev)
+        # value CSR: set pairs (set_cap per read) and bounded-counter (slot, value) entries (at
+        # most n_dc^2 + n_dc per read: every P and D orddict entry)
+        if present & {abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER}:
+            bc_cap = n_dc * n_dc + n_dc
+            if abi.AM_BCOUNTER not in present:
+                caps = None
+                self.set_off = torch.arange(0, (n_reads + 1) * set_cap, set_cap, dtype=torch.int64, device=dev)
+            else:
+                caps = torch.where(self.types == abi.AM_BCOUNTER, bc_cap, set_cap).to(torch.int64)
+                self.set_off = torch.zeros(n_reads + 1, dtype=torch.int64, device=dev)
+                self.set_off[1:] = torch.cumsum(caps, 0)
+            tot = int(self.set_off[-1].item())
             self.set_len = z(torch.int32, n_reads)
-            self.set_a = z(torch.int64, n_reads * set_cap)
-            self.set_b = z(torch.int64, n_reads * set_cap)
-        if abi.AM_BCOUNTER in present:
-            self.bc_p = z(torch.int64, n_reads, n_dc * n_dc)
-            self.bc_pp = z(torch.uint8, n_reads, n_dc * n_dc)
-            self.bc_d = z(torch.int64, n_reads, n_dc)
-            self.bc_dp = z(torch.uint8, n_reads, n_dc)
+            self.set_a = z(torch.int64, max(tot, 1))
+            self.set_b = z(torch.int64, max(tot, 1))
 
     def set_base_from(self, other: "DeviceReads"):
         """Use another batch's results as the cached base snapshots (incremental reads)."""
@@ -90,8 +94,6 @@ class DeviceReads:
         r.value.v0, r.value.v1, r.value.vflag = p(self.v0), p(self.v1), p(self.vflag)
         r.value.set_off, r.value.set_len, r.value.set_a, r.value.set_b = (p(self.set_off), p(self.set_len),
                                                                           p(self.set_a), p(self.set_b))
-        r.value.bc_p, r.value.bc_p_pres, r.value.bc_d, r.value.bc_d_pres = (p(self.bc_p), p(self.bc_pp),
-                                                                            p(self.bc_d), p(self.bc_dp))
         self._keep = (b, r)
         return b, r
 
@@ -100,26 +102,24 @@ class DeviceReads:
         out = []
         nd = self.n_dc
         types = self.types.cpu().numpy()
-        sl = sa = sb = bp = bpp = bd = bdp = None
+        sl = sa = sb = so = None
         if self.set_len is not None:
             sl = self.set_len.cpu().numpy()
             sa = self.set_a.cpu().numpy().view(np.uint64)
             sb = self.set_b.cpu().numpy().view(np.uint64)
-        if self.bc_p is not None:
-            bp, bpp = self.bc_p.cpu().numpy(), self.bc_pp.cpu().numpy()
-            bd, bdp = self.bc_d.cpu().numpy(), self.bc_dp.cpu().numpy()
+            so = self.set_off.cpu().numpy()
         v0 = self.v0.cpu().numpy()
         v1 = self.v1.cpu().numpy().view(np.uint64)
         vf = self.vflag.cpu().numpy()
         for i in idx:
             t = int(types[i])
             if t in (abi.AM_AWSET, abi.AM_MVREG):
-                o = int(i) * self.set_cap
+                o = int(so[i])
                 out.append([(int(sa[o + j]), int(sb[o + j])) for j in range(int(sl[i]))])
             elif t == abi.AM_BCOUNTER:
-                pd = {(j // nd, j % nd): int(bp[i, j]) for j in range(nd * nd) if bpp[i, j]}
-                dd = {j: int(bd[i, j]) for j in range(nd) if bdp[i, j]}
-                out.append((pd, dd))
+                from .oplog import bc_dicts
+                o = int(so[i])
+                out.append(bc_dicts([(int(sa[o + j]), int(sb[o + j])) for j in range(int(sl[i]))], nd))
             elif t == abi.AM_PN:
                 out.append(int(v0[i]))
             else:

@@ -192,7 +192,7 @@ class Store:
 
     def close(self):
         if self.handle:
-            if self.owned:
+            if self.owned and self.mat.ctx:  # a closed context already released its memory
                 abi.lib().am_store_destroy(self.handle)
             self.handle = None
 
@@ -265,12 +265,8 @@ def _cache_snapshots(mat, sc, n_dc: int, key: int, type_: int):
                                                b.ctypes.data, p.ctypes.data), "am_snapcache_get_value")
             w = int(nw.value)
             if type_ == abi.AM_BCOUNTER:
-                if w == 0:
-                    val = ({}, {})
-                else:
-                    val = ({(j // nd, j % nd): int(a[j:j + 1].view(np.int64)[0]) for j in range(nd * nd) if p[j]},
-                           {j: int(a[nd * nd + j:nd * nd + j + 1].view(np.int64)[0]) for j in range(nd)
-                            if p[nd * nd + j]})
+                from .oplog import bc_dicts
+                val = bc_dicts([(int(a[j]), int(b[j])) for j in range(w)], nd)
             else:
                 val = [(int(a[j]), int(b[j])) for j in range(w)]
         out.append((clock, int(lo[e]), val))
@@ -331,7 +327,8 @@ class SnapshotCache:
 
     def close(self):
         if self.handle:
-            self.mat.L.am_snapcache_destroy(self.handle)
+            if self.mat.ctx:
+                self.mat.L.am_snapcache_destroy(self.handle)
             self.handle = ctypes.c_void_p()
 
 
@@ -422,7 +419,8 @@ class Vnode:
 
     def close(self):
         if self.handle:
-            self.mat.L.am_vnode_destroy(self.handle)
+            if self.mat.ctx:
+                self.mat.L.am_vnode_destroy(self.handle)
             self.handle = ctypes.c_void_p()
 
 

@@ -169,6 +169,26 @@ def _pres(clock: Dict[int, int]) -> int:
     return m
 
 
+def bc_pairs(value, n_dc: int) -> List[Tuple[int, int]]:
+    """A bounded counter's ({(From, To): N}, {Id: N}) as the ABI's (slot, value) entries: P at
+    From*n_dc+To, then D at n_dc*n_dc+Id, slot order (include/antidote_mat.h am_values)."""
+    pdict, ddict = value
+    out = [(f * n_dc + t, int(v)) for (f, t), v in pdict.items()] + [(n_dc * n_dc + d, int(v)) for d, v in ddict.items()]
+    return [(s, int(np.array([v], np.int64).view(np.uint64)[0])) for s, v in sorted(out)]
+
+
+def bc_dicts(pairs, n_dc: int):
+    """The inverse of bc_pairs: (slot, value-bits) entries -> ({(From, To): N}, {Id: N})."""
+    pd, dd = {}, {}
+    for s, v in pairs:
+        x = int(np.array([v], np.uint64).view(np.int64)[0])
+        if s < n_dc * n_dc:
+            pd[(s // n_dc, s % n_dc)] = x
+        else:
+            dd[s - n_dc * n_dc] = x
+    return pd, dd
+
+
 class HostBatch:
     """am_read_batch + am_read_result in host memory."""
 
@@ -190,11 +210,6 @@ class HostBatch:
         self.b_v0 = np.zeros(max(n, 1), np.int64)
         self.b_v1 = np.zeros(max(n, 1), U64)
         self.b_vflag = np.ones(max(n, 1), np.uint8)
-        np_ = n_dc * n_dc
-        self.b_bc_p = np.zeros((max(n, 1), np_), np.int64)
-        self.b_bc_pp = np.zeros((max(n, 1), np_), np.uint8)
-        self.b_bc_d = np.zeros((max(n, 1), n_dc), np.int64)
-        self.b_bc_dp = np.zeros((max(n, 1), n_dc), np.uint8)
         base_pairs: List[List[Tuple[int, int]]] = []
         for i, r in enumerate(reads):
             for d, t in r.clock.items():
@@ -223,14 +238,8 @@ class HostBatch:
                     pairs = [(int(a), int(b)) for a, b in bv]
                 elif r.type == abi.AM_MVREG:  # a sorted list of {Value, Token}
                     pairs = sorted((int(a), int(b)) for a, b in bv)
-                elif r.type == abi.AM_BCOUNTER:
-                    pdict, ddict = bv
-                    for (f, t), v in pdict.items():
-                        self.b_bc_p[i, f * n_dc + t] = v
-                        self.b_bc_pp[i, f * n_dc + t] = 1
-                    for d, v in ddict.items():
-                        self.b_bc_d[i, d] = v
-                        self.b_bc_dp[i, d] = 1
+                elif r.type == abi.AM_BCOUNTER:  # the P / D orddicts as (slot, value) entries
+                    pairs = bc_pairs(bv, n_dc)
             base_pairs.append(pairs)
         self.has_txid = any(r.txid is not None for r in reads)
         self.has_base = any(r.base_clock is not None for r in reads)
@@ -254,17 +263,15 @@ class HostBatch:
         self.v0 = np.zeros(max(n, 1), np.int64)
         self.v1 = np.zeros(max(n, 1), U64)
         self.vflag = np.zeros(max(n, 1), np.uint8)
-        caps = list(set_capacity) if set_capacity is not None else [64] * n
+        # default room per read: 64 set pairs; every orddict entry of a bounded counter
+        caps = (list(set_capacity) if set_capacity is not None else
+                [max(64, n_dc * n_dc + n_dc) if r.type == abi.AM_BCOUNTER else 64 for r in reads])
         self.o_set_off = np.zeros(n + 1, U64)
         self.o_set_off[1:] = np.cumsum(caps, dtype=U64) if n else []
         tot = int(self.o_set_off[-1]) if n else 0
         self.o_set_len = np.zeros(max(n, 1), np.uint32)
         self.o_set_a = np.zeros(max(tot, 1), U64)
         self.o_set_b = np.zeros(max(tot, 1), U64)
-        self.o_bc_p = np.zeros((max(n, 1), np_), np.int64)
-        self.o_bc_pp = np.zeros((max(n, 1), np_), np.uint8)
-        self.o_bc_d = np.zeros((max(n, 1), n_dc), np.int64)
-        self.o_bc_dp = np.zeros((max(n, 1), n_dc), np.uint8)
 
     def structs(self):
         p = lambda a: a.ctypes.data  # noqa: E731
@@ -279,7 +286,6 @@ class HostBatch:
         bv.v0, bv.v1, bv.vflag = p(self.b_v0), p(self.b_v1), p(self.b_vflag)
         bv.set_off, bv.set_len, bv.set_a, bv.set_b = (p(self.b_set_off), p(self.b_set_len), p(self.b_set_a),
                                                       p(self.b_set_b))
-        bv.bc_p, bv.bc_p_pres, bv.bc_d, bv.bc_d_pres = p(self.b_bc_p), p(self.b_bc_pp), p(self.b_bc_d), p(self.b_bc_dp)
         r = abi.am_read_result()
         r.status, r.new_last_op, r.last_ct, r.last_ct_pres = (p(self.status), p(self.new_last_op), p(self.last_ct),
                                                               p(self.last_ct_pres))
@@ -289,7 +295,6 @@ class HostBatch:
         rv.v0, rv.v1, rv.vflag = p(self.v0), p(self.v1), p(self.vflag)
         rv.set_off, rv.set_len, rv.set_a, rv.set_b = (p(self.o_set_off), p(self.o_set_len), p(self.o_set_a),
                                                       p(self.o_set_b))
-        rv.bc_p, rv.bc_p_pres, rv.bc_d, rv.bc_d_pres = p(self.o_bc_p), p(self.o_bc_pp), p(self.o_bc_d), p(self.o_bc_dp)
         self._keep = (b, r)
         return b, r
 
@@ -304,10 +309,8 @@ class HostBatch:
             o, n = int(self.o_set_off[i]), int(self.o_set_len[i])
             return [(int(self.o_set_a[o + j]), int(self.o_set_b[o + j])) for j in range(n)]
         if t == abi.AM_BCOUNTER:
-            nd = self.n_dc
-            pd = {(j // nd, j % nd): int(self.o_bc_p[i, j]) for j in range(nd * nd) if self.o_bc_pp[i, j]}
-            dd = {j: int(self.o_bc_d[i, j]) for j in range(nd) if self.o_bc_dp[i, j]}
-            return (pd, dd)
+            o, n = int(self.o_set_off[i]), int(self.o_set_len[i])
+            return bc_dicts([(int(self.o_set_a[o + j]), int(self.o_set_b[o + j])) for j in range(n)], self.n_dc)
         raise ValueError(t)
 
     def result(self, i: int):

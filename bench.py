@@ -88,13 +88,13 @@ def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
     new_last_op 8, last_ct 8*D, last_ct_pres 4, last_ct_ignore 1, is_new_ss 1, count 4,
     flags 1, value (PN 8; LWW 8+8+1; sets: rec_key_off 8 + key_ngrp 4 + set_off 8 +
     set_len 4 + per surviving pair 16 gathered from the group table and 16 written;
-    bcounter (D*D + D) slots x 9)."""
+    bcounter: set_off 8 + set_len 4 + 16 per orddict entry written, (slot, value))."""
     if type_ == abi.AM_PN:
         val = 8
     elif type_ == abi.AM_LWW:
         val = 17
     elif type_ == abi.AM_BCOUNTER:
-        val = 9 * (n_dc * n_dc + n_dc)
+        val = 12 + 16 * set_len
     else:
         val = 24 + 32 * set_len
     return 8 + 1 + 8 + 1 + 4 + 8 + 8 * n_dc + 4 + 1 + 1 + 4 + 1 + val
@@ -133,7 +133,8 @@ def workload_bytes(cfg, dlog, ko, kt, reads, packed):
     for t in sorted(set(int(x) for x in np.unique(kt))):
         m = kt == t
         total += float(lens[m].sum()) * bytes_per_op(t, cfg["n_dc"], packed)
-        sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG)) else 0.0
+        sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER)) \
+            else 0.0
         total += float(m.sum()) * (bytes_per_key(t, cfg["n_dc"], sl) + (8 if packed else 0))
     return total
 
@@ -181,12 +182,12 @@ def cpu_baseline(cfg, p, budget_s=10.0, cached=False):
         log = synth.host_log(p, k0, per)
         kt = log.key_type[:per]
         reads = [Read(k, int(kt[k]), {d: clock[d] for d in range(p.n_dc)}) for k in range(per)]
-        hb = HostBatch(p.n_dc, reads, [max(cfg["set_cap"], 1)] * per)
+        caps = [p.n_dc * p.n_dc + p.n_dc if int(kt[k]) == abi.AM_BCOUNTER else max(cfg["set_cap"], 1) for k in range(per)]
+        hb = HostBatch(p.n_dc, reads, caps)
         s = log.as_struct()
         if cached:
             half = synth.read_clock(p, 0.5)
-            h0 = HostBatch(p.n_dc, [Read(k, int(kt[k]), {d: half[d] for d in range(p.n_dc)}) for k in range(per)],
-                           [max(cfg["set_cap"], 1)] * per)
+            h0 = HostBatch(p.n_dc, [Read(k, int(kt[k]), {d: half[d] for d in range(p.n_dc)}) for k in range(per)], caps)
             b0, r0 = h0.structs()
             amo.lib().amo_materialize_range(ctypes.byref(s), ctypes.byref(b0), 0, per, ctypes.byref(r0))
             assert (h0.status[:per] == 0).all(), "cpu baseline: q=0.5 reads failed"
@@ -196,7 +197,6 @@ def cpu_baseline(cfg, p, budget_s=10.0, cached=False):
             hb.base_last_op[:] = h0.new_last_op
             hb.b_v0[:], hb.b_v1[:], hb.b_vflag[:] = h0.v0, h0.v1, h0.vflag
             hb.b_set_off, hb.b_set_len, hb.b_set_a, hb.b_set_b = h0.o_set_off, h0.o_set_len, h0.o_set_a, h0.o_set_b
-            hb.b_bc_p, hb.b_bc_pp, hb.b_bc_d, hb.b_bc_dp = h0.o_bc_p, h0.o_bc_pp, h0.o_bc_d, h0.o_bc_dp
             hb._h0 = h0
         b, r = hb.structs()
         parts.append((s, b, r, per, int(log.n_ops), log, hb))

@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 4
+#define AM_ABI_VERSION 5
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -218,9 +218,12 @@ typedef struct am_op_log {
  *             the newest add first)
  *   MVREG     CSR of (value, token) pairs sorted (insert_sorted).  set_off[n+1] gives
  *             each read's capacity, set_len[n] the used length.
- *   BCOUNTER  bc_p[n][n_dc*n_dc] + bc_p_pres, bc_d[n][n_dc] + bc_d_pres
- *             (P key {From,To} at From*n_dc+To; an orddict entry is present iff
- *             it was ever updated)
+ *   BCOUNTER  the same CSR, one (slot, value) pair per orddict entry (present iff it was
+ *             ever updated): the P orddict {From,To} -> N at slot From*n_dc+To, then the D
+ *             orddict Id -> N at slot n_dc*n_dc+Id, each in key order (set_a = slot,
+ *             set_b = the int64 value) -- only the touched entries, as the reference's
+ *             orddicts hold them (src/bcounter_mgr.erl:80-97 effects), at most
+ *             n_dc*n_dc + n_dc per read
  */
 typedef struct am_values {
   int64_t *v0;
@@ -230,13 +233,6 @@ typedef struct am_values {
   uint32_t *set_len;
   uint64_t *set_a;
   uint64_t *set_b;
-  int64_t *bc_p;
-  uint8_t *bc_p_pres;
-  int64_t *bc_d;
-  uint8_t *bc_d_pres;
-  /* bases only: read r's bcounter slots at bc_p / bc_p_pres + bc_off[r] (P, i < n_dc^2) and
-   * bc_d / bc_d_pres + bc_off[r] (D) instead of rows r * n_dc^2 / r * n_dc; NULL => rows */
-  const uint64_t *bc_off;
 } am_values;
 
 /* One batch of snapshot reads: the materialize/4 inputs per key. */

@@ -433,14 +433,14 @@ int amo_materialize_one(const am_op_log *L, const am_read_batch *B, uint64_t r, 
       uint8_t pp[AM_MAX_DC * AM_MAX_DC];
       __int128 dv[AM_MAX_DC];
       uint8_t dp[AM_MAX_DC];
-      for (uint32_t i = 0; i < np; ++i) {
-        pv[i] = bv->bc_p ? bv->bc_p[r * np + i] : 0;
-        pp[i] = bv->bc_p_pres ? bv->bc_p_pres[r * np + i] : 0;
-      }
-      for (uint32_t i = 0; i < nd; ++i) {
-        dv[i] = bv->bc_d ? bv->bc_d[r * nd + i] : 0;
-        dp[i] = bv->bc_d_pres ? bv->bc_d_pres[r * nd + i] : 0;
-      }
+      memset(pv, 0, sizeof(pv)), memset(pp, 0, sizeof(pp)), memset(dv, 0, sizeof(dv)), memset(dp, 0, sizeof(dp));
+      if (bv->set_off && bv->set_len)  /* the base orddicts: (slot, value) entries */
+        for (uint32_t i = 0; i < bv->set_len[r]; ++i) {
+          const uint64_t slot = bv->set_a[bv->set_off[r] + i];
+          const int64_t v = (int64_t)bv->set_b[bv->set_off[r] + i];
+          if (slot < np) pv[slot] = v, pp[slot] = 1;
+          else if (slot < np + nd) dv[slot - np] = v, dp[slot - np] = 1;
+        }
       for (uint64_t j = n_incl; j-- > 0;) {
         const uint64_t p = incl[j];
         const unsigned kind = AM_META_KIND(L->op_meta[p]);
@@ -468,15 +468,20 @@ int amo_materialize_one(const am_op_log *L, const am_read_batch *B, uint64_t r, 
         for (uint32_t i = 0; i < nd; ++i)
           if (dv[i] > (__int128)INT64_MAX || dv[i] < (__int128)INT64_MIN) status = AM_ERR_OVERFLOW;
       }
-      if (status == AM_OK) {
-        for (uint32_t i = 0; i < np; ++i) {
-          ov->bc_p[r * np + i] = (int64_t)pv[i];
-          ov->bc_p_pres[r * np + i] = pp[i];
+      if (status == AM_OK) {  /* the touched entries, P then D, each in key order */
+        const uint64_t o = ov->set_off[r], cap = ov->set_off[r + 1] - o;
+        uint32_t ne = 0;
+        for (uint32_t i = 0; i < np + nd; ++i) {
+          const int present = i < np ? pp[i] : dp[i - np];
+          if (!present) continue;
+          if (ne < cap) {
+            ov->set_a[o + ne] = i;
+            ov->set_b[o + ne] = (uint64_t)(int64_t)(i < np ? pv[i] : dv[i - np]);
+          }
+          ++ne;
         }
-        for (uint32_t i = 0; i < nd; ++i) {
-          ov->bc_d[r * nd + i] = (int64_t)dv[i];
-          ov->bc_d_pres[r * nd + i] = dp[i];
-        }
+        if (ne > cap) status = AM_ERR_CAPACITY;
+        else ov->set_len[r] = ne;
       }
     } else {
       status = AM_ERR_UNEXPECTED_OPERATION;

@@ -167,3 +167,9 @@ def ref_materialize(t, ops: List[Op], read: Read):
     _, val, nlo, ct, newss, count = r
     flags = abi.AM_FLAG_MISSING_DC_LOGGED if R.MissingDcLog.count else 0
     return ("ok", canon_state(read.type, val), nlo, None if ct == R.IGNORE else dict(ct), newss, count, flags)
+
+
+def caps_for(reads, n_dc, cap):
+    """Result room per read: `cap` set pairs, and every orddict entry of a bounded counter
+    (n_dc^2 + n_dc (slot, value) entries; include/antidote_mat.h am_values)."""
+    return [max(cap, n_dc * n_dc + n_dc) if r.type == abi.AM_BCOUNTER else cap for r in reads]

@@ -9,6 +9,7 @@ from antidote_amd import abi, synth
 from antidote_amd.devbatch import DeviceReads, materialize
 from antidote_amd.oplog import HostBatch, Read
 from oracle import amo
+from tests import randlog
 
 pytestmark = pytest.mark.gpu
 
@@ -58,7 +59,7 @@ def test_config_shape_parity(mat, name):
             h = dr.host()
             sample = np.sort(rng.choice(len(keys), min(200, len(keys)), replace=False))
             reads = [Read(int(keys[i]), t, {d: clock[d] for d in range(p.n_dc)}) for i in sample]
-            ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, [128] * len(reads)))
+            ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, randlog.caps_for(reads, p.n_dc, 128)))
             vals = dr.values(sample)
             for j, i in enumerate(sample):
                 r = ref.result(j)
@@ -94,7 +95,7 @@ def test_config_mixed_batch_parity(mat, name):
     hot = np.argsort(-lens)[:8]  # always include the longest logs
     sample = np.unique(np.concatenate([hot, rng.choice(p.n_keys, min(300, p.n_keys), replace=False)]))
     reads = [Read(int(k), int(ktypes[k]), {d: clock[d] for d in range(p.n_dc)}) for k in sample]
-    ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, [128] * len(reads)))
+    ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, randlog.caps_for(reads, p.n_dc, 128)))
     vals = dr.values(sample)
     for j, i in enumerate(sample):
         ct = None if h["last_ct_ignore"][i] else {d: int(h["last_ct"][d, i]) for d in range(p.n_dc)

@@ -14,6 +14,7 @@ from antidote_amd import abi, synth
 from antidote_amd.devbatch import DeviceReads, materialize
 from antidote_amd.oplog import HostBatch, Read
 from oracle import amo
+from tests import randlog
 
 pytestmark = pytest.mark.gpu
 
@@ -67,7 +68,7 @@ def test_fullsize_config(mat, cfg_name):
                 nk -= 1
             hlog = synth.host_log(p, k0, nk)
             reads = [Read(k, int(hlog.key_type[k]), {d: clock[d] for d in range(p.n_dc)}) for k in range(nk)]
-            ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, [cap] * nk))
+            ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, randlog.caps_for(reads, p.n_dc, cap)))
             idx = np.arange(k0, k0 + nk)
             vals = dr.values(idx)
             for j, i in enumerate(idx):
