@@ -66,6 +66,9 @@ __device__ unsigned long long amk_phase_cycles[8];
 #define PH_END()
 #define PH_DECL()
 #endif
+#ifndef AMK_TILE_UNROLL
+#define AMK_TILE_UNROLL 1  // op tiles of the wave kernel unrolled (experiment switch)
+#endif
 #ifndef AMK_WAVE_OCC
 #define AMK_WAVE_OCC 4  // waves per SIMD the wave kernel is compiled for
 #endif
@@ -765,6 +768,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       ap.reset();
       a.reset();
       bool esc = false;  // some op of this lane did not fit the packed view
+#pragma unroll AMK_TILE_UNROLL
       for (uint64_t t = t0; !(AMK_SKIP & 4) && t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
         const uint32_t ib =
@@ -1111,8 +1115,10 @@ int launch_v(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   if (!general && packed)
     return L->n_dc == (uint32_t)D ? launch_d<D, TYPE, false, true, true>(ctx, L, B, R, S, next, tier)
                                   : launch_d<D, TYPE, false, true, false>(ctx, L, B, R, S, next, tier);
-  return packed ? launch_d<D, TYPE, true, true, false>(ctx, L, B, R, S, next, tier)
-                : launch_d<D, TYPE, true, false, false>(ctx, L, B, R, S, next, tier);
+  if (packed)  // cached bases, TxIds, per-read clocks (the vnode's read/6 path)
+    return L->n_dc == (uint32_t)D ? launch_d<D, TYPE, true, true, true>(ctx, L, B, R, S, next, tier)
+                                  : launch_d<D, TYPE, true, true, false>(ctx, L, B, R, S, next, tier);
+  return launch_d<D, TYPE, true, false, false>(ctx, L, B, R, S, next, tier);
 }
 
 }  // namespace amk_grp

@@ -135,6 +135,9 @@ struct LTile {
   uint64_t v0[OPL], v1[OPL];
 };
 
+#ifndef AMK_LANE_PH_UNROLL
+#define AMK_LANE_PH_UNROLL 1  // quad-scan phases unrolled (experiment switch)
+#endif
 // waves per SIMD the register allocation must allow (experiment switch; 1 = the compiler's choice)
 #ifndef AMK_LANE_MINW
 #define AMK_LANE_MINW 1
@@ -243,7 +246,7 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
       // to the read's own lane (ds_bpermute), which carries on as before.
       const uint32_t qj = lane & 3u;
       const uint32_t tk = take ? (t | 0x100u) : 0u;
-#pragma unroll 1
+#pragma unroll AMK_LANE_PH_UNROLL
       for (uint32_t ph = 0; ph < 4; ++ph) {
         const uint32_t src = 16u * ph + (lane >> 2);
         const uint32_t qt = shfl_u32(tk, src);

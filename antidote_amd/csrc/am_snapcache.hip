@@ -84,6 +84,8 @@ struct ScSel {
   uint64_t *base_vc, *v1, *set_off;
   uint32_t *base_pres, *set_len;
   int64_t *base_last_op, *v0;
+  uint64_t *cp_dst;  // k_sc_store -> k_sc_copy: the stored snapshot's value words go to pool
+  uint32_t *cp_len;  //   words [cp_dst, cp_dst + cp_len) from the read's result CSR (0: none)
 };
 // prune thresholds emitted by snapshot_insert_gc (optional)
 struct ScGc {
@@ -291,11 +293,9 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       C.v0[s0] = (t == AM_PN || t == AM_LWW) ? R.value.v0[r] : 0;
       C.v1[s0] = t == AM_LWW ? R.value.v1[r] : 0;
       C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
-      // the value words into the pool
-      if (w) {
-        const uint64_t so = R.value.set_off[r];
-        for (uint32_t i = 0; i < w; ++i) C.pool_a[off + i] = R.value.set_a[so + i], C.pool_b[off + i] = R.value.set_b[so + i];
-      }
+      // the value words into the pool: copied by k_sc_copy, a wave per read (one thread
+      // copying a read's pairs serially cost C3's read/6 3.4 ms of 16)
+      if (w && off) S.cp_dst[r] = off, S.cp_len[r] = w;
       C.poff[s0] = off;
       C.plen[s0] = off ? w : 0;
     }
@@ -304,6 +304,19 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
       G.thr_pres[key] = gc_threshold(C, s0, keep, G.thr_vc + key, C.n_keys);
       G.mask[key] = 1;
     }
+  }
+}
+
+// one wave per read: a stored snapshot's value words (set pairs, bounded-counter entries)
+// from the read's result CSR into the pool, coalesced
+__global__ void k_sc_copy(ScView C, am_read_result R, ScSel S, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < n; r += waves) {
+    const uint32_t w = S.cp_len[r];
+    if (!w) continue;
+    const uint64_t src = R.value.set_off[r], dst = S.cp_dst[r];
+    for (uint32_t i = lane; i < w; i += 64) C.pool_a[dst + i] = R.value.set_a[src + i], C.pool_b[dst + i] = R.value.set_b[src + i];
   }
 }
 
@@ -638,7 +651,7 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   }
   // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres, set_len [n] u32 |
   // base_last_op, v0, v1, set_off [n] u64 | base_vc [nd][n]
-  const size_t bytes = n * (4 + 8 + 4 * 8 + (size_t)nd * 8) + 4096;
+  const size_t bytes = n * (4 + 8 + 4 * 8 + (size_t)nd * 8 + 12) + 4096;
   void *scr = nullptr;
   int rc = am_ctx_scratch(ctx, AM_SCR_SNAP, bytes, &scr);
   if (rc) return rc;
@@ -653,6 +666,8 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   S.v0 = (int64_t *)take(n * 8);
   S.v1 = (uint64_t *)take(n * 8);
   S.set_off = (uint64_t *)take(n * 8);
+  S.cp_dst = (uint64_t *)take(n * 8);
+  S.cp_len = (uint32_t *)take(n * 4);
   S.base_vc = (uint64_t *)take(n * nd * 8);
   S.base_pres = (uint32_t *)take(n * 4);
   S.set_len = (uint32_t *)take(n * 4);
@@ -681,7 +696,13 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
     rc = am_launch_materialize(ctx, L, &db, R);
     if (rc == AM_OK) {
       const ScGc G{gc_mask, thr_vc, thr_pres};
-      hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G);
+      if (hipMemsetAsync(S.cp_len, 0, n * 4, ctx->stream) != hipSuccess) {
+        rc = AM_ERR_HIP;
+      } else {
+        hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G);
+        const uint64_t wg = (n + 3) / 4 < 65536 ? (n + 3) / 4 : 65536;
+        hipLaunchKernelGGL(k_sc_copy, dim3((unsigned)wg), dim3(256), 0, ctx->stream, V, *R, S, n);
+      }
       if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
     }
   }

@@ -17,6 +17,11 @@ for s in $STEPS; do
     bench) timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err; ok $? bench ;;
     benches) for c in ${BENCH_CFGS:-c2 c4 c5}; do timeout -k 10 400 python bench.py --config $c ${BENCH_ARGS:-} > $OUT/bench_$c.json 2> $OUT/bench_$c.err; ok $? bench_$c; done ;;
     gc) timeout -k 10 300 python scripts/bench_gc.py > $OUT/gc_bench.json 2> $OUT/gc_bench.err; ok $? gc ;;
+    cached) timeout -k 10 600 python bench.py --base cached > $OUT/bench_c3_cached.json 2> $OUT/bench_c3_cached.err; ok $? cached ;;
+    profcached) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3_cached -o run --output-format csv -- python bench.py --base cached --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_c3_cached.json 2> $OUT/prof_c3_cached.log; ok $? profcached ;;
+    pmccached)
+           timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_c3_cached -o pmc --output-format csv -- python bench.py --base cached --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmcf_c3_cached.log 2>&1; ok $? pmcf_c3_cached
+           timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_c3_cached -o pmc --output-format csv -- python bench.py --base cached --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmcw_c3_cached.log 2>&1; ok $? pmcw_c3_cached ;;
     ingest) timeout -k 10 400 python scripts/bench_ingest.py ${INGEST_ARGS:-} > $OUT/ingest.json 2> $OUT/ingest.err; ok $? ingest ;;
     prof) for c in ${PROF_CFGS:-c2 c3 c4 c5}; do timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline ${PROF_ARGS:-} > $OUT/prof_$c.json 2> $OUT/prof_$c.log; ok $? prof_$c; done ;;
     pmc) for c in ${PMC_CFGS:-c4 c5}; do
