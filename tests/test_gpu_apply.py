@@ -190,3 +190,33 @@ def test_gpu_vnode_grows_key_space(mat):
             compare_state(vn, st, {k: k for k in range(n)}, types, {d: d for d in range(n_dc)})
     finally:
         vn.close()
+
+
+def test_gpu_vnode_load_hot_key_beside_short_keys(mat):
+    """load_ops/2-style replay of one long log (3,000 ops: a GC read every 50 ids) beside 2,000
+    short ones: every GC round after the first is an in-place apply of the keys it touches (the
+    hot key), not a whole-store rebuild, and the hot key's tuple matches the oracle's."""
+    import time
+
+    from oracle import ref_materializer as R
+    from tests.test_gpu_vnode import KeyGen, compare_state
+    rng = random.Random(9700)
+    n_dc, n_keys = 2, 2001
+    types = [abi.AM_PN] * n_keys
+    gens = [KeyGen(rng, abi.AM_PN, n_dc, 10) for _ in range(n_keys)]
+    batch = [gens[k].ops(3000 if k == 0 else 3) for k in range(n_keys)]
+    st = R.VnodeState()
+    for k in (0, 1, 2):
+        for op in batch[k]:
+            R.op_insert_gc(k, randlog.payload_term(op, key=k), st)
+    vn = mat.vnode(n_dc, n_keys)
+    try:
+        t0 = time.perf_counter()
+        vn.insert(batch, types)
+        dt = time.perf_counter() - t0
+        rebuilds, in_place = vn.stats()
+        print(f"load: {sum(len(b) for b in batch)} ops, {dt * 1e3:.0f} ms, {rebuilds} rebuilds, {in_place} in place")
+        assert in_place >= 100 and rebuilds <= 8, (rebuilds, in_place)
+        compare_state(vn, st, {0: 0, 1: 1, 2: 2}, types, {d: d for d in range(n_dc)})
+    finally:
+        vn.close()
