@@ -394,7 +394,29 @@ __global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_r
                   // are one half of a bitmap word (the same word for the whole row)
                   const uint64_t so = R.value.set_off[rj], cap = R.value.set_off[rj + 1] - so;
                   uint32_t ne = 0;
-                  for (uint32_t c = 0; c * G < nslot; ++c) {
+                  if constexpr (!GENERAL) {
+                    // every LDS read of the emit issued up front (one exposed latency at one
+                    // wave per SIMD, not one per chunk); no base: a slot's value is its sum
+                    constexpr uint32_t NC = (RS::NS + G - 1) / G, NWD = (RS::NS + 31) / 32;
+                    uint32_t pw[NWD];
+                    uint64_t av[NC];
+#pragma unroll
+                    for (uint32_t w = 0; w < NWD; ++w) pw[w] = w < (nslot + 31) / 32 ? rs->pres[w] : 0u;
+#pragma unroll
+                    for (uint32_t c = 0; c < NC; ++c) av[c] = c * G + sl < nslot ? rs->acc[c * G + sl] : 0ull;
+#pragma unroll
+                    for (uint32_t c = 0; c < NC; ++c) {
+                      const uint32_t bits = (pw[c >> 1] >> ((c & 1u) * 16u)) & 0xFFFFu;
+                      const uint32_t i = c * G + sl;
+                      const uint32_t rank = ne + (uint32_t)__popc(bits & ((1u << sl) - 1u));
+                      if (i < nslot && ((bits >> sl) & 1u) && rank < cap) {
+                        R.value.set_a[so + rank] = i;
+                        R.value.set_b[so + rank] = av[c];
+                      }
+                      ne += (uint32_t)__popc(bits);
+                    }
+                  }
+                  for (uint32_t c = 0; GENERAL && c * G < nslot; ++c) {
                     const uint32_t bits = (rs->pres[c >> 1] >> ((c & 1u) * 16u)) & 0xFFFFu;
                     const uint32_t i = c * G + sl;
                     const uint32_t rank = ne + (uint32_t)__popc(bits & ((1u << sl) - 1u));
