@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_r
     const uint32_t nb = (uint32_t)(nsel - rb < (uint64_t)WAVE ? nsel - rb : (uint64_t)WAVE);
     const uint64_t bmask = C.mask ? uniform_u64(C.mask[bid]) : ~0ull;  // k_stream's hand-off
     if (!bmask) continue;
-    uint64_t key = 0, off0 = 0, off1 = 0, r = 0;
+    uint64_t key = 0, off0 = 0, off1 = 0, r = 0, tb = 0;  // tb: the key's packed time base
     int32_t st = AM_OK;
     if (lane < nb && ((bmask >> lane) & 1u)) {
       r = sbase ? (uint64_t)sbase[rb + lane] : rb + lane;
@@ -126,6 +126,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_r
       } else {
         off0 = L.key_off[key];
         off1 = am_kend(L, key);
+        if (PACKED) tb = L.key_tbase[key];  // with the batch's metadata, not per read start
         const uint32_t ktype = L.key_type[key];
         const uint32_t kfl = L.key_flags ? (uint32_t)L.key_flags[key] : 0u;
         if (off1 > off0 && (ktype != rtype || (kfl & AM_KEY_MIXED_TYPES)))
@@ -194,6 +195,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_r
       auto begin = [&](bool upd) {
         const uint32_t j = row * G + (s < 16 ? s : 0);
         const uint64_t n0 = shfl_u64(off0, j), n1 = shfl_u64(off1, j), nr = shfl_u64(r, j), nk = shfl_u64(key, j);
+        const uint64_t ntb = PACKED ? shfl_u64(tb, j) : 0;
         if (!upd) return;
         o0 = n0, o1 = n1, rj = nr, keyj = nk;
         t = 0;
@@ -213,7 +215,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_r
           u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[rj]) && L.op_txid;
           u.txid = u.has_txid ? B.txid[rj] : 0;
         }
-        if (PACKED) pk_setup(u, nd, L.key_tbase[keyj], pk);
+        if (PACKED) pk_setup(u, nd, ntb, pk);
         if (LDS) {
           if (sl == 0) rs->ctr[0] = 0, rs->ctr[1] = 0, rs->ctr[2] = 0, rs->ctr[3] = 0;
           if (RS::SLOTS) {
