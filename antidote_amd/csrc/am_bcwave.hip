@@ -142,18 +142,32 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
       if ((uint32_t)d == lane) myct = m;
     }
     status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
-    if (status == AM_OK) {
-      bool ovf = false;
-      for (uint32_t k = lane; k < ns; k += WAVE) ovf |= s.hi[k] != ((int64_t)s.lo[k] < 0 ? -1 : 0);
-      if (__ballot(ovf)) status = AM_ERR_OVERFLOW;
+    // the slots' LDS words read once, all up front (lane l: slots l, l + 64, ...)
+    constexpr uint32_t NC = (BcSmem<DMAX>::NS + WAVE - 1) / WAVE;
+    uint64_t slo[NC];
+    uint32_t spr[NC];
+    bool ovf = false;
+#pragma unroll
+    for (uint32_t c = 0; c < NC; ++c) {
+      const uint32_t k = c * WAVE + lane;
+      slo[c] = k < ns ? s.lo[k] : 0ull;
+      spr[c] = k < ns ? s.pres[k] : 0u;
+      ovf |= k < ns && s.hi[k] != ((int64_t)slo[c] < 0 ? -1 : 0);
     }
+    if (status == AM_OK && __ballot(ovf)) status = AM_ERR_OVERFLOW;
     uint32_t nent = 0;
-    if (status == AM_OK) {
-      nent = bc_emit<WAVE>(R, r, ns, lane, 0, [&](uint32_t k, int64_t &v) {
-        v = (int64_t)s.lo[k];
-        return s.pres[k] != 0;
-      });
-      if (nent > R.value.set_off[r + 1] - R.value.set_off[r]) status = AM_ERR_CAPACITY;
+    if (status == AM_OK) {  // the present slots as (slot, value) pairs, slot order
+      const uint64_t so = R.value.set_off[r], cap = R.value.set_off[r + 1] - so;
+#pragma unroll
+      for (uint32_t c = 0; c < NC; ++c) {
+        const uint32_t k = c * WAVE + lane;
+        const bool p = k < ns && spr[c] != 0;
+        const uint64_t m = __ballot(p);
+        const uint64_t pos = nent + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (p && pos < cap) R.value.set_a[so + pos] = k, R.value.set_b[so + pos] = slo[c];
+        nent += (uint32_t)__popcll(m);
+      }
+      if (nent > cap) status = AM_ERR_CAPACITY;
     }
     const bool ign = u.base_ignore && count == 0;
     const uint32_t opres = ign ? 0u : (pres | u.cpres);
