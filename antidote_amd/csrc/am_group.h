@@ -66,6 +66,9 @@ __device__ unsigned long long amk_phase_cycles[8];
 #define PH_END()
 #define PH_DECL()
 #endif
+#ifndef AMK_WAVE_DB
+#define AMK_WAVE_DB 0  // double-buffered op tiles in the wave kernel (experiment switch)
+#endif
 #ifndef AMK_TILE_UNROLL
 #define AMK_TILE_UNROLL 1  // op tiles of the wave kernel unrolled (experiment switch)
 #endif
@@ -768,6 +771,36 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       ap.reset();
       a.reset();
       bool esc = false;  // some op of this lane did not fit the packed view
+      if constexpr (AMK_WAVE_DB && PACKED && !GENERAL) {
+        // double-buffered op tiles: the next tile's loads in flight while this one is evaluated
+        uint32_t xa[OPL][DMAX], xb[OPL][DMAX];
+        auto ld = [&](uint32_t(&x)[OPL][DMAX], uint64_t g) {
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint32_t q[OPL] = {};
+            if (d < (int)nd) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
+          }
+        };
+        const uint64_t tx[OPL] = {};
+        uint64_t g = t0 + (uint64_t)lane * OPL;
+        if (g < off1) ld(xa, g);
+        for (uint64_t t = t0; !(AMK_SKIP & 4) && t < off1; t += TILE) {
+          const uint64_t gn = g + TILE;
+          if (gn < off1) ld(xb, gn);
+          const uint32_t ib = g < off1 ? pk_tile<DMAX, OPL, false>(u, pk, xa, tx, g, off0, off1, ap, esc) : 0u;
+          uint32_t word = ib << (OPL * (lane % LPW));
+#pragma unroll
+          for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
+          if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
+#pragma unroll
+          for (int k = 0; k < OPL; ++k)
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) xa[k][d] = xb[k][d];
+          g = gn;
+        }
+      } else {
 #pragma unroll AMK_TILE_UNROLL
       for (uint64_t t = t0; !(AMK_SKIP & 4) && t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
@@ -777,6 +810,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
 #pragma unroll
         for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
         if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
+      }
       }
       wave_sync();
       const bool full = !PACKED || __ballot(esc);
