@@ -176,7 +176,9 @@ SIGNATURES = [
     ("am_txid_create", c_int, [POINTER(c_void_p)]),
     ("am_txid_destroy", c_int, [c_void_p]),
     ("am_txid_intern", c_int, [c_void_p, c_char_p, c_uint64, POINTER(c_uint64)]),
+    ("am_txid_intern_op", c_int, [c_void_p, c_char_p, c_uint64, c_uint32, c_uint64, POINTER(c_uint64)]),
     ("am_txid_lookup", c_int, [c_void_p, c_char_p, c_uint64, POINTER(c_uint64)]),
+    ("am_txid_expire", c_int, [c_void_p, c_uint32, c_void_p, c_uint32, POINTER(c_uint64)]),
     ("am_txid_forget", c_int, [c_void_p, c_char_p, c_uint64]),
     ("am_txid_size", c_uint64, [c_void_p]),
     ("am_txid_canonical", c_int, [c_char_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]),

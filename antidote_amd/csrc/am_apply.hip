@@ -155,6 +155,20 @@ __global__ void k_fill_ids(am_op_log L, uint64_t *op_id, uint64_t *op_txid) {
   }
 }
 
+// the caller's key list: every key in range and none twice (a claim bit per store key); bad |= 1
+// for a key >= n_keys, 2 for a repeated key
+__global__ void k_check_keys(const uint64_t *keys, uint64_t m, uint64_t n_keys, uint32_t *claim, uint32_t *bad) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    if (k >= n_keys) {
+      atomicOr(bad, 1u);
+      continue;
+    }
+    const uint32_t bit = 1u << (k & 31);
+    if (atomicOr(&claim[k >> 5], bit) & bit) atomicOr(bad, 2u);
+  }
+}
+
 unsigned grid_threads(uint64_t n) { return (unsigned)((n + 255) / 256 < 65536 ? ((n + 255) / 256 ? (n + 255) / 256 : 1) : 65536); }
 unsigned grid_waves(uint64_t n) { return (unsigned)((n + 3) / 4 < 65536 ? ((n + 3) / 4 ? (n + 3) / 4 : 1) : 65536); }
 
@@ -362,9 +376,36 @@ int am_store_apply(am_ctx *c, am_store *st, uint64_t n_touched, const uint64_t *
     *applied = 1;
     return AM_OK;
   }
-  if (dev_new && (dev_new->n_dc != st->dev.n_dc || !dev_new->key_off)) {
-    am_set_error("am_store_apply: the new-op log must be CSR over the touched keys with the store's n_dc");
+  if (dev_new && (dev_new->n_dc != st->dev.n_dc || !dev_new->key_off || dev_new->n_keys != n_touched)) {
+    am_set_error("am_store_apply: the new-op log must be CSR over the %llu touched keys with the store's n_dc",
+                 (unsigned long long)n_touched);
     return AM_ERR_INVALID;
+  }
+  {  // the key list comes from the caller: in range and distinct, or nothing runs
+    AM_HIP(hipSetDevice(c->device));
+    const uint64_t words = (st->dev.n_keys + 31) / 32;
+    void *scr = nullptr;
+    if (int rc = am_dev_alloc(c, words * 4 + 256, &scr)) return rc;
+    uint32_t *bad = (uint32_t *)scr, *claim = bad + 64;
+    uint64_t w = 0;
+    int rc = hipMemsetAsync(scr, 0, words * 4 + 256, c->stream) == hipSuccess ? AM_OK : AM_ERR_HIP;
+    if (!rc) {
+      hipLaunchKernelGGL(k_check_keys, dim3(grid_threads(n_touched)), dim3(256), 0, c->stream, keys, n_touched,
+                         st->dev.n_keys, claim, bad);
+      rc = hipGetLastError() == hipSuccess ? AM_OK : AM_ERR_HIP;
+    }
+    if (!rc) rc = am_ctx_fetch(c, bad, 1, &w);
+    (void)hipStreamSynchronize(c->stream);
+    am_dev_release(c, scr);
+    if (rc) {
+      am_set_error("am_store_apply: key check failed");
+      return rc;
+    }
+    if (w & 3u) {
+      am_set_error("am_store_apply: %s", (w & 1u) ? "a touched key is outside the store's key space"
+                                                  : "a touched key appears twice in the list");
+      return AM_ERR_INVALID;
+    }
   }
   return am_store_apply_ex(c, st, n_touched, keys, dev_new, prune_mask, thr_vc, thr_pres, gc_flags, nullptr, applied);
 }

@@ -305,9 +305,15 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
         vq += wave_bcast(vincl, 63);
       }
     }
-    if (O.key_end) {  // slack: the free slots' var_off all end the key's words
-      const uint64_t cap_end = cnt[k + 1];
-      for (uint64_t p = q + lane(); O.var_off && p < cap_end; p += WAVE_SZ) O.var_off[p] = vq;
+    if (O.key_end) {  // slack: the free slots' var_off all end the key's words; their op
+      const uint64_t cap_end = cnt[k + 1];  // header words are defined (zero), not reused memory
+      for (uint64_t p = q + lane(); p < cap_end; p += WAVE_SZ) {
+        if (O.var_off) O.var_off[p] = vq;
+        O.op_meta[p] = 0;
+        O.commit_time[p] = 0;
+        O.p0[p] = 0;
+        O.p1[p] = 0;
+      }
       if (lane() == 0) O.key_end[k] = q;
     }
     if (lane() == 0) {

@@ -74,12 +74,14 @@ __global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, ui
     const bool setk = type == AM_AWSET || type == AM_MVREG;
     if (L.key_end && p >= L.key_end[k]) {  // a free slot: room for its records, as many as the
       uint64_t per = REC_SLACK;            // key's ops average (records <= effect words + 1)
+      const uint64_t o0 = L.key_off[k], e = L.key_end[k];
       if (setk && L.var_off) {
-        const uint64_t o0 = L.key_off[k], e = L.key_end[k];
         const uint64_t w = e > o0 ? (L.var_off[e] - L.var_off[o0] + (e - o0) - 1) / (e - o0) + 1 : 0;
         per = w > per ? w : per;
       }
-      cnt[p] = setk ? per : 0;
+      // a key with no ops yet carries the placeholder type (PN): its first ops may be of a set
+      // type, so its free slots keep set room too (no O(store) rebuild for a new set key)
+      cnt[p] = (setk || e == o0) ? per : 0;
       continue;
     }
     const uint32_t meta = L.op_meta[p];

@@ -13,8 +13,10 @@
 // byte string -- and interned into a dense u64 id, never reordered or relabeled.  Two TxIds
 // get the same id iff they are the same term (exact, no hashing).  Ids start at 1 and are
 // never reused; am_txid_forget drops a finished transaction's entry (its ops keep the id, and
-// no later read carries that TxId).  Floats compare by bits (a TxId holds none).  Maps and funs
+// no later read carries that TxId), and am_txid_expire drops the entries of ops the stable
+// snapshot covers (below).  Floats compare by bits (a TxId holds none).  Maps and funs
 // are AM_ERR_UNSUPPORTED.
+#include <map>
 #include <string>
 #include <unordered_map>
 
@@ -316,9 +318,22 @@ int canonical(const uint8_t *b, uint64_t len, std::string &out) {
 
 }  // namespace
 
+// An entry is HELD while a reader interned it (am_txid_intern, until am_txid_forget) and STAMPED
+// with its ops' commit time {DcId, CT} when ops interned it (am_txid_intern_op).  A stamped entry
+// that no reader holds is dropped by am_txid_expire once the stable snapshot covers its commit
+// time: the transaction committed (its ops reach the ops cache at commit) and every partition has
+// applied it, so no live reader carries that TxId -- ops replicated from other DCs, whose TxIds no
+// local coordinator ever forgets, leave the map this way.  Ids are never reused, so an op whose
+// entry was dropped can never equal a later reader's TxId.
+struct am_txid_ent {
+  uint64_t id = 0, ct = 0;
+  uint32_t dc = 0;
+  bool stamped = false, held = false;
+};
 struct am_txids {
   std::mutex mu;
-  std::unordered_map<std::string, uint64_t> ids;
+  std::unordered_map<std::string, am_txid_ent> ids;
+  std::map<uint32_t, std::multimap<uint64_t, std::string>> by_ct;  // stamped entries per DC (may hold stale keys)
   uint64_t next = 1;
 };
 
@@ -344,13 +359,31 @@ int am_txid_intern(am_txids *t, const uint8_t *term, uint64_t len, uint64_t *id)
     return rc;
   }
   std::lock_guard<std::mutex> g(t->mu);
-  auto it = t->ids.find(k);
-  if (it != t->ids.end()) {
-    *id = it->second;
-    return AM_OK;
+  am_txid_ent &e = t->ids[k];
+  if (!e.id) e.id = t->next++;
+  e.held = true;
+  *id = e.id;
+  return AM_OK;
+}
+
+int am_txid_intern_op(am_txids *t, const uint8_t *term, uint64_t len, uint32_t dc, uint64_t ct, uint64_t *id) {
+  if (!t || !id) return AM_ERR_INVALID;
+  std::string k;
+  const int rc = canonical(term, len, k);
+  if (rc != AM_OK) {
+    am_set_error("am_txid_intern_op: %s external term", rc == AM_ERR_UNSUPPORTED ? "unsupported" : "malformed");
+    return rc;
   }
-  *id = t->next++;
-  t->ids.emplace(std::move(k), *id);
+  std::lock_guard<std::mutex> g(t->mu);
+  auto it = t->ids.find(k);
+  if (it == t->ids.end()) it = t->ids.emplace(k, am_txid_ent{}).first;
+  am_txid_ent &e = it->second;
+  if (!e.id) e.id = t->next++;
+  if (!e.stamped || e.dc != dc || e.ct < ct) {  // every op of a transaction carries one commit time
+    e.stamped = true, e.dc = dc, e.ct = ct;
+    t->by_ct[dc].emplace(ct, k);
+  }
+  *id = e.id;
   return AM_OK;
 }
 
@@ -362,7 +395,7 @@ int am_txid_lookup(am_txids *t, const uint8_t *term, uint64_t len, uint64_t *id)
   std::lock_guard<std::mutex> g(t->mu);
   auto it = t->ids.find(k);
   if (it == t->ids.end()) return AM_CODEC_ABSENT;
-  *id = it->second;
+  *id = it->second.id;
   return AM_OK;
 }
 
@@ -373,6 +406,29 @@ int am_txid_forget(am_txids *t, const uint8_t *term, uint64_t len) {
   if (rc != AM_OK) return rc;
   std::lock_guard<std::mutex> g(t->mu);
   return t->ids.erase(k) ? AM_OK : AM_CODEC_ABSENT;
+}
+
+int am_txid_expire(am_txids *t, uint32_t n_dc, const uint64_t *stable_vc, uint32_t stable_pres, uint64_t *dropped) {
+  if (!t || (n_dc && !stable_vc) || n_dc > 32) return AM_ERR_INVALID;
+  std::lock_guard<std::mutex> g(t->mu);
+  uint64_t n = 0;
+  for (auto &dm : t->by_ct) {
+    const uint32_t dc = dm.first;
+    if (dc >= n_dc || !((stable_pres >> dc) & 1u)) continue;  // a DC the stable snapshot lacks
+    auto &idx = dm.second;
+    const uint64_t s = stable_vc[dc];
+    while (!idx.empty() && idx.begin()->first <= s) {
+      auto ie = idx.begin();
+      auto it = t->ids.find(ie->second);
+      if (it != t->ids.end() && it->second.stamped && it->second.dc == dc && it->second.ct == ie->first) {
+        if (it->second.held) it->second.stamped = false;  // a reader still holds it: forget drops it
+        else t->ids.erase(it), ++n;
+      }
+      idx.erase(ie);
+    }
+  }
+  if (dropped) *dropped = n;
+  return AM_OK;
 }
 
 uint64_t am_txid_size(am_txids *t) {

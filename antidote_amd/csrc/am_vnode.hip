@@ -164,27 +164,34 @@ int prune(am_vnode *v, const std::vector<uint64_t> &keys) {
 // arrays are reallocated, the host mirrors extended
 int grow_keys(am_vnode *v, uint64_t new_n) {
   if (new_n <= v->n_keys) return AM_OK;
-  am_store *ns = nullptr;
-  CapHint ch(v->ctx);
-  int rc = ch.upload(v, new_n);
-  if (!rc) rc = am_store_grow_keys(v->ctx, v->st, new_n, ch.p, &ns);
-  if (rc) return rc;
-  swap_store(v, ns);
-  ++v->rebuilds;
-  if ((rc = am_snapcache_grow(v->sc, new_n))) return rc;
+  // every fallible step first (the new GC arrays, the grown store, the grown snapshot cache);
+  // the vnode switches to them only when all succeeded, so a failure leaves it unchanged
   uint8_t *gm = nullptr, *gf = nullptr;
   uint64_t *tv = nullptr;
   uint32_t *tp = nullptr;
-  if (!rc) rc = am_dev_alloc(v->ctx, new_n + 16, (void **)&gm);
+  am_store *ns = nullptr;
+  int rc = am_dev_alloc(v->ctx, new_n + 16, (void **)&gm);
   if (!rc) rc = am_dev_alloc(v->ctx, new_n + 16, (void **)&gf);
   if (!rc) rc = am_dev_alloc(v->ctx, (size_t)v->n_dc * new_n * 8 + 16, (void **)&tv);
   if (!rc) rc = am_dev_alloc(v->ctx, new_n * 4 + 16, (void **)&tp);
+  if (!rc && (hipMemsetAsync(gm, 0, new_n + 16, v->ctx->stream) != hipSuccess ||
+              hipStreamSynchronize(v->ctx->stream) != hipSuccess)) {
+    am_set_error("grow_keys: clearing the GC mask failed");
+    rc = AM_ERR_HIP;
+  }
+  if (!rc) {
+    CapHint ch(v->ctx);
+    rc = ch.upload(v, new_n);
+    if (!rc) rc = am_store_grow_keys(v->ctx, v->st, new_n, ch.p, &ns);
+  }
+  if (!rc) rc = am_snapcache_grow(v->sc, new_n);  // extra empty keys are harmless if a later step fails
   if (rc) {
+    if (ns) am_store_destroy(ns);
     for (void *p : {(void *)gm, (void *)gf, (void *)tv, (void *)tp}) am_dev_release(v->ctx, p);
     return rc;
   }
-  AM_HIP(hipMemsetAsync(gm, 0, new_n + 16, v->ctx->stream));
-  AM_HIP(hipStreamSynchronize(v->ctx->stream));
+  swap_store(v, ns);
+  ++v->rebuilds;
   am_dev_release(v->ctx, v->gc_mask), am_dev_release(v->ctx, v->gc_flags);
   am_dev_release(v->ctx, v->thr_vc), am_dev_release(v->ctx, v->thr_pres);
   v->gc_mask = gm, v->gc_flags = gf, v->thr_vc = tv, v->thr_pres = tp;

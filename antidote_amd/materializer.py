@@ -99,10 +99,17 @@ class Store:
         import numpy as np
         L = self.mat.L
         m = len(keys)
+        ka = np.ascontiguousarray(keys, np.uint64)
+        n_keys = int(self.device_log().n_keys)
+        if m and (int(ka.max()) >= n_keys or len(np.unique(ka)) != m):
+            raise abi.AmError(f"am_store_apply: touched keys must be distinct and < {n_keys} (rc={abi.AM_ERR_INVALID})")
+        if new_log is not None and new_log.n_keys != m:
+            raise abi.AmError(f"am_store_apply: the new-op log has {new_log.n_keys} keys for {m} touched keys "
+                              f"(rc={abi.AM_ERR_INVALID})")
         bufs: List[_DevBuf] = []
         tmp_store = None
         try:
-            kb = _DevBuf.of(self.mat, np.ascontiguousarray(keys, np.uint64))
+            kb = _DevBuf.of(self.mat, ka)
             flags = _DevBuf(self.mat, max(m, 1))
             bufs += [kb, flags]
             mask = thr = pres = None

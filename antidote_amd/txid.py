@@ -37,8 +37,32 @@ class TxIds:
         return int(v.value)
 
     def intern(self, txid: Any) -> int:
-        """The id of a TxId term (etf.Pid / etf.Ref allowed)."""
+        """The id of a reader's TxId term (etf.Pid / etf.Ref allowed); held until forget()."""
         return self.intern_encoded(etf.encode(txid))
+
+    def intern_op_encoded(self, b: bytes, dc: int, ct: int) -> int:
+        v = ctypes.c_uint64()
+        abi.check(self.L.am_txid_intern_op(self.handle, b, len(b), dc, ct, ctypes.byref(v)), "am_txid_intern_op")
+        return int(v.value)
+
+    def intern_op(self, txid: Any, dc: int, ct: int) -> int:
+        """The id of an op's TxId (#clocksi_payload.txid), stamped with the op's commit time
+        {DcIndex, CT}: expire() drops it once the stable snapshot covers CT."""
+        return self.intern_op_encoded(etf.encode(txid), dc, ct)
+
+    def expire(self, stable: dict) -> int:
+        """Drop the unheld op entries the stable snapshot {DcIndex: T} (the GST) covers;
+        returns how many were dropped."""
+        import numpy as np
+        n_dc = (max(stable) + 1) if stable else 0
+        vc = np.zeros(max(n_dc, 1), np.uint64)
+        pres = 0
+        for d, t in stable.items():
+            vc[d] = t
+            pres |= 1 << d
+        n = ctypes.c_uint64()
+        abi.check(self.L.am_txid_expire(self.handle, n_dc, vc.ctypes.data, pres, ctypes.byref(n)), "am_txid_expire")
+        return int(n.value)
 
     def lookup_encoded(self, b: bytes):
         v = ctypes.c_uint64()
@@ -47,6 +71,10 @@ class TxIds:
             return None
         abi.check(rc, "am_txid_lookup")
         return int(v.value)
+
+    def lookup(self, txid: Any):
+        """The id of a TxId term, or None when it was never interned (or forgotten / expired)."""
+        return self.lookup_encoded(etf.encode(txid))
 
     def forget_encoded(self, b: bytes) -> bool:
         rc = self.L.am_txid_forget(self.handle, b, len(b))

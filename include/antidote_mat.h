@@ -539,14 +539,25 @@ int am_vnode_relabel(am_vnode *v, const uint64_t *old_labels, const uint64_t *ne
  * references included) to a dense u64 id, the op_txid / am_read_batch.txid words.  Every
  * encoding of one term gets one id (the bytes are canonicalised first); ids start at 1, are
  * never reordered, relabeled or reused.  am_txid_forget drops an ended transaction's entry.
- * Thread-safe.  Maps and funs: AM_ERR_UNSUPPORTED. */
+ * Thread-safe.  Maps and funs: AM_ERR_UNSUPPORTED.
+ * Lifetime: a reader's TxId (am_txid_intern) is HELD until am_txid_forget; an op's TxId
+ * (am_txid_intern_op, stamped with the op's commit_time {DcId, CT}, DcId as a DC index) is
+ * dropped by am_txid_expire once the stable snapshot covers CT and no reader holds it -- the
+ * transaction has committed everywhere, so no live read carries it (ops replicated from other
+ * DCs, whose TxIds no local coordinator forgets, leave the map this way).  Replaces the
+ * #clocksi_payload.txid bookkeeping of materializer_vnode:update/2 (src/materializer_vnode.erl:106-110)
+ * and the TxId test of is_op_in_snapshot/7 (src/clocksi_materializer.erl:232). */
 typedef struct am_txids am_txids;
 int am_txid_create(am_txids **out);
 int am_txid_destroy(am_txids *t);
 int am_txid_intern(am_txids *t, const uint8_t *term, uint64_t len, uint64_t *id);
-/* AM_CODEC_ABSENT when the TxId was never interned (or was forgotten) */
+int am_txid_intern_op(am_txids *t, const uint8_t *term, uint64_t len, uint32_t dc, uint64_t ct, uint64_t *id);
+/* AM_CODEC_ABSENT when the TxId was never interned (or was forgotten / expired) */
 int am_txid_lookup(am_txids *t, const uint8_t *term, uint64_t len, uint64_t *id);
 int am_txid_forget(am_txids *t, const uint8_t *term, uint64_t len);
+/* drop the unheld op entries whose commit time the stable snapshot (stable_vc[n_dc], presence
+ * bits stable_pres: the GST, stable_time_functions:get_min_time/1) covers; *dropped (or NULL) */
+int am_txid_expire(am_txids *t, uint32_t n_dc, const uint64_t *stable_vc, uint32_t stable_pres, uint64_t *dropped);
 uint64_t am_txid_size(am_txids *t);
 /* the canonical encoding the map keys on (131-prefixed); *out_len always set */
 int am_txid_canonical(const uint8_t *term, uint64_t len, uint8_t *buf, uint64_t cap, uint64_t *out_len);

@@ -133,6 +133,45 @@ def test_gpu_apply_overflow_leaves_store(mat):
         s0.close()
 
 
+def test_gpu_apply_rejects_bad_keys(mat):
+    """am_store_apply takes its touched-key list from the caller: a key outside the store or a
+    key listed twice is AM_ERR_INVALID from the C ABI (checked on the device before any kernel
+    indexes by it) and from Store.apply (checked on the host), and the store is unchanged; a
+    new-op log shaped for another number of keys is AM_ERR_INVALID too, not 'no room'."""
+    import ctypes
+
+    from antidote_amd.materializer import _DevBuf
+    rng = random.Random(9450)
+    n_dc, n_keys = 2, 6
+    types = [abi.AM_PN, abi.AM_LWW, abi.AM_AWSET] * 2
+    keys = [randlog.rand_key_ops(rng, types[k], n_dc, 4) for k in range(n_keys)]
+    s0 = mat.store(HostLog(n_dc, keys, key_types=types))
+    s1 = s0.reserve()
+    try:
+        before = s1.download()
+        for bad in ([0, n_keys], [1, 4, 1], [2 ** 40]):
+            with pytest.raises(abi.AmError):
+                s1.apply(bad)
+            kb = _DevBuf.of(mat, np.ascontiguousarray(bad, np.uint64))
+            fl = _DevBuf(mat, len(bad))
+            ap = ctypes.c_int(7)
+            try:
+                rc = mat.L.am_store_apply(mat.ctx, s1.handle, len(bad), kb.ptr, None, None, None, None, fl.ptr,
+                                          ctypes.byref(ap))
+            finally:
+                kb.free()
+                fl.free()
+            assert rc == abi.AM_ERR_INVALID and ap.value == 0, (bad, rc, ap.value)
+        with pytest.raises(abi.AmError):   # two new-op key entries for one touched key
+            s1.apply([3], new_log=HostLog(n_dc, [keys[3][:1], keys[4][:1]], key_types=[types[3], types[4]]))
+        _same_store(s1.download(), before, n_keys)
+        ok, _ = s1.apply([3], new_log=HostLog(n_dc, [keys[3][:1]], key_types=[types[3]]))
+        assert ok
+    finally:
+        s1.close()
+        s0.close()
+
+
 def test_gpu_vnode_inserts_in_place(mat):
     """A vnode's steady-state inserts (a few keys per batch, GC triggers included) take the
     in-place path: after the first insert builds the room, batches touching few keys do not

@@ -121,3 +121,48 @@ def test_canonical_forms_of_nested_and_improper_lists():
     # canonical bytes are a fixed point and decode to the same term
     c = txid.canonical(TXID_ETF)
     assert txid.canonical(c) == c and etf.decode(c) == TXID
+
+
+def test_replicated_op_txids_expire_at_the_stable_snapshot():
+    """Ops replicated from other DCs (inter_dc_dep_vnode -> materializer_vnode:update/2) carry
+    TxIds no local coordinator ever forgets.  Their entries are stamped with the op's commit
+    time {DcId, CT} and dropped once the GST covers it, so 10^5 such ops leave the map bounded
+    by the ops not yet stable; a reader's held TxId stays until forget(); dropped ids are
+    never handed out again."""
+    t = txid.TxIds()
+    remote = Pid("antidote@10.0.0.2", 40, 0, 1)
+    reader = (Atom("tx_id"), 5, Pid("antidote@127.0.0.1", 90, 0, 3))
+    rid = t.intern(reader)
+    t.intern_op(reader, 0, 50)               # the reader's own op, committed at {0, 50}
+    ids, peak = set(), 0
+    n, window = 100_000, 1000
+    for i in range(n):
+        dc = 1 + i % 2                       # two remote DCs, CT increasing per DC
+        ids.add(t.intern_op((Atom("tx_id"), 10_000 + i, remote), dc, 100 + i))
+        if i % window == window - 1:         # the GST advances behind the replication stream
+            t.expire({0: 0, 1: 100 + i - window // 2, 2: 100 + i - window // 2})
+            peak = max(peak, len(t))
+    assert len(ids) == n                     # distinct TxIds, distinct ids
+    assert peak <= window + 2, peak
+    assert t.lookup((Atom("tx_id"), 10_000, remote)) is None             # expired long ago
+    assert t.lookup((Atom("tx_id"), 10_000 + n - 1, remote)) is not None  # not yet stable
+    # the reader's entry survives a GST past its commit while held, and goes with forget()
+    assert t.expire({0: 10 ** 9, 1: 0, 2: 0}) == 0 and t.lookup(reader) == rid
+    assert t.forget(reader) and t.lookup(reader) is None
+    # everything stable: the map empties; a re-interned TxId gets a fresh id
+    t.expire({0: 10 ** 9, 1: 10 ** 9, 2: 10 ** 9})
+    assert len(t) == 0
+    again = t.intern_op((Atom("tx_id"), 10_000, remote), 1, 100)
+    assert again not in ids and again > max(ids)
+    t.close()
+
+
+def test_expire_needs_the_dc_in_the_stable_snapshot():
+    """A DC absent from the stable snapshot expires nothing (stable_time_functions drops DCs a
+    partition lacks: no bound on them yet)."""
+    t = txid.TxIds()
+    t.intern_op((Atom("tx_id"), 1, PID), 3, 10)
+    assert t.expire({0: 100, 1: 100}) == 0 and len(t) == 1
+    assert t.expire({3: 9}) == 0 and len(t) == 1
+    assert t.expire({3: 10}) == 1 and len(t) == 0
+    t.close()
