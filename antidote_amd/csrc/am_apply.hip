@@ -99,7 +99,9 @@ __global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter,
         for (uint32_t d = 0; d < L.n_dc; ++d)
           const_cast<uint32_t *>(L.pk_vc)[(uint64_t)d * ls + q] = S.pk_vc[(uint64_t)d * ss + p];
       if (L.var_off) const_cast<uint64_t *>(L.var_off)[q] = vb + (S.var_off ? S.var_off[p] - sv0 : 0);
+      if (L.gmask) const_cast<uint64_t *>(L.gmask)[q] = S.gmask ? S.gmask[p] : 0;
     }
+    for (uint64_t q = d0 + n + lane; L.gmask && q < cap_end; q += WAVE_SZ) const_cast<uint64_t *>(L.gmask)[q] = 0;
     if (L.var_off) {
       uint64_t *vo = const_cast<uint64_t *>(L.var_off);
       for (uint64_t q = d0 + n + lane; q < cap_end; q += WAVE_SZ) vo[q] = vb + nv;  // the free slots
@@ -218,13 +220,14 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   view.n_keys = m;
   view.key_off = V.off, view.key_end = V.end, view.key_id_base = V.idb, view.key_type = V.type, view.key_flags = V.flags;
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
+  view.gmask = nullptr;
   am_store *sub = nullptr;
   int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
                               false, nullptr, &sub);
   if (rc) return done(rc);
   const am_op_log &S = sub->dev;
   bool cols = !(S.snap_pres && !L.snap_pres) && !(S.var_off && !L.var_off) && !(L.pk_vc && !S.pk_vc) &&
-              !(S.rec_key_off && !L.rec_key_off);
+              !(S.rec_key_off && !L.rec_key_off) && !(S.gmask && !L.gmask);
   if (cols && ((S.op_id && !L.op_id) || (S.op_txid && !L.op_txid))) {  // turn the column on (O(store), once)
     const size_t na = L.snap_stride ? L.snap_stride : L.n_ops;
     void *ids = nullptr, *tx = nullptr;
@@ -344,6 +347,7 @@ int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint
   view.key_off = (uint64_t *)b, view.key_end = (uint64_t *)(b + o_end), view.key_id_base = (uint64_t *)(b + o_idb);
   view.key_type = (uint8_t *)(b + o_type), view.key_flags = (uint8_t *)(b + o_flags);
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
+  view.gmask = nullptr;
   hipLaunchKernelGGL(k_grow_view, dim3(grid_threads(n_new + 1)), dim3(256), 0, c->stream, L,
                      (const uint64_t *)st->counter, n_new, (uint64_t *)view.key_off, (uint64_t *)view.key_end,
                      (uint64_t *)view.key_id_base, (uint64_t *)(b + o_ctr), (uint8_t *)view.key_type,

@@ -39,12 +39,6 @@
 namespace amk_grp {
 using namespace amk;
 
-#ifndef AMK_VOPL8
-#define AMK_VOPL8 0
-#endif
-#ifndef AMK_SKIP
-#define AMK_SKIP 0  // timing experiments only: 1 records, 2 survivors, 4 op tiles
-#endif
 // phase timing of the wave kernel (experiments only, -DAMK_PHASE_PROF): per-wave cycles
 // spent from one phase boundary to the next, summed into amk_phase_cycles
 #ifdef AMK_PHASE_PROF
@@ -65,15 +59,6 @@ __device__ unsigned long long amk_phase_cycles[8];
 #define PH(i)
 #define PH_END()
 #define PH_DECL()
-#endif
-#ifndef AMK_WAVE_DB
-#define AMK_WAVE_DB 0  // double-buffered op tiles in the wave kernel (experiment switch)
-#endif
-#ifndef AMK_TILE_UNROLL
-#define AMK_TILE_UNROLL 1  // op tiles of the wave kernel unrolled (experiment switch)
-#endif
-#ifndef AMK_WAVE_OCC
-#define AMK_WAVE_OCC 4  // waves per SIMD the wave kernel is compiled for
 #endif
 constexpr int BLOCK = 256;
 constexpr int NW = BLOCK / WAVE;
@@ -525,7 +510,7 @@ struct WaveSmem {
 // full view's u64 columns 2 ops at D >= 8
 template <int DMAX, bool PACKED>
 constexpr int vopl() {
-  return PACKED ? (AMK_VOPL8 && DMAX <= 8 ? 8 : DMAX <= 8 ? 4 : DMAX <= 16 ? 2 : 1) : (DMAX < 8 ? 4 : DMAX <= 16 ? 2 : 1);
+  return PACKED ? (DMAX <= 8 ? 4 : DMAX <= 16 ? 2 : 1) : (DMAX < 8 ? 4 : DMAX <= 16 ? 2 : 1);
 }
 
 // A read the wave kernel can take with its base snapshot: no base pairs, or at most KB of
@@ -682,7 +667,7 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
 }
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
-__global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
+__global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
                                                                   am_sel S, am_retry next, uint32_t short_opl) {
   constexpr int OPL = vopl<DMAX, PACKED>();
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
@@ -771,38 +756,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       ap.reset();
       a.reset();
       bool esc = false;  // some op of this lane did not fit the packed view
-      if constexpr (AMK_WAVE_DB && PACKED && !GENERAL) {
-        // double-buffered op tiles: the next tile's loads in flight while this one is evaluated
-        uint32_t xa[OPL][DMAX], xb[OPL][DMAX];
-        auto ld = [&](uint32_t(&x)[OPL][DMAX], uint64_t g) {
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            uint32_t q[OPL] = {};
-            if (d < (int)nd) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
-#pragma unroll
-            for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
-          }
-        };
-        const uint64_t tx[OPL] = {};
-        uint64_t g = t0 + (uint64_t)lane * OPL;
-        if (g < off1) ld(xa, g);
-        for (uint64_t t = t0; !(AMK_SKIP & 4) && t < off1; t += TILE) {
-          const uint64_t gn = g + TILE;
-          if (gn < off1) ld(xb, gn);
-          const uint32_t ib = g < off1 ? pk_tile<DMAX, OPL, false>(u, pk, xa, tx, g, off0, off1, ap, esc) : 0u;
-          uint32_t word = ib << (OPL * (lane % LPW));
-#pragma unroll
-          for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
-          if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
-#pragma unroll
-          for (int k = 0; k < OPL; ++k)
-#pragma unroll
-            for (int d = 0; d < DMAX; ++d) xa[k][d] = xb[k][d];
-          g = gn;
-        }
-      } else {
-#pragma unroll AMK_TILE_UNROLL
-      for (uint64_t t = t0; !(AMK_SKIP & 4) && t < off1; t += TILE) {
+      for (uint64_t t = t0; t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
         const uint32_t ib =
             g < off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, off0, off1, stride, ap, a, esc) : 0u;
@@ -810,7 +764,6 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
 #pragma unroll
         for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
         if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
-      }
       }
       wave_sync();
       const bool full = !PACKED || __ballot(esc);
@@ -822,7 +775,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
       PH(1);
       // ---- 2. records of included ops -> newest birth / kill per group (the next chunk's
       //      loads in flight while one chunk is applied) ----
-      for (uint64_t q0 = qa; !(AMK_SKIP & 1);) {
+      for (uint64_t q0 = qa;;) {
         const uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
         u32x4 nxt[VRPT / 4];
 #pragma unroll
@@ -881,7 +834,7 @@ __global__ void __launch_bounds__(BLOCK, AMK_WAVE_OCC) k_grp_wave(am_op_log L, a
           wave_sync();
           continue;
         }
-      } else if (status == AM_OK && !(AMK_SKIP & 2)) {
+      } else if (status == AM_OK) {
         const uint32_t nwd = (G + 31) / 32;
         const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
         const uint32_t c = (uint32_t)__popc(aw);

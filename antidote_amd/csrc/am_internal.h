@@ -126,6 +126,12 @@ int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_
 uint32_t am_lane_accept(const am_op_log *L, const am_read_result *R, uint32_t types);
 int am_launch_lanes(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                     am_retry next, uint32_t accept);
+// Short bounded-counter reads (am_bcrows.hip): one 16-lane row per read of <= 64 ops, batch
+// clock, packed view, n_dc <= 16; the touched slots only (bitmap ranks, compact sums).  Longer
+// reads (and the few with an |amount| >= 2^56) go to `next`.
+bool am_bcrows_applies(const am_op_log *L, const am_read_batch *B, const am_read_result *R);
+int am_launch_bcrows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                     am_retry next);
 // Bounded-counter wave tier (am_bcwave.hip): one wave per read with LDS slot sums, reads
 // up to 32768 ops over the packed view (n_dc <= 16); the rest go to `next`.
 bool am_bcwave_applies(const am_op_log *L, const am_read_result *R);

@@ -23,12 +23,6 @@
 using namespace amk;
 using namespace amk_grp;
 
-// experiment switch (phase costs; default off): bit 0 skips the PN / LWW payload loads, bit 1
-// the set records, bit 2 the survivor gathers, bit 3 every output but the status
-#ifndef AMK_LANE_SKIP
-#define AMK_LANE_SKIP 0
-#endif
-
 namespace {
 
 constexpr uint32_t LBITS = 64;  // inclusion bits of a lane read: ops [off0 & ~(OPL-1), off1)
@@ -59,6 +53,10 @@ __device__ __forceinline__ uint32_t quad_sum_u32(uint32_t v) {
 __device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
   v = max(v, dpp32<0xB1>(v));
   return max(v, dpp32<0x4E>(v));
+}
+__device__ __forceinline__ uint32_t quad_min_u32(uint32_t v) {
+  v = min(v, dpp32<0xB1>(v));
+  return min(v, dpp32<0x4E>(v));
 }
 __device__ __forceinline__ uint64_t quad_min_u64(uint64_t v) {
   v = umin64(v, dpp64<0xB1>(v));
@@ -128,6 +126,55 @@ __device__ __forceinline__ void wave_gather(const am_op_log &L, const am_read_re
   }
 }
 
+// four records [q, q + 4) of a set read with records [rk0, rk1): an included op's birth sets
+// its group's born bit, its effective kill the killed bit (incl bit = op index + sh)
+__device__ __forceinline__ void rec_bits(u32x4 v, uint64_t q, uint64_t rk0, uint64_t rk1, uint64_t incl, uint32_t sh,
+                                         uint64_t &born, uint64_t &killed) {
+  const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = xs[k];
+    if (q + k < rk0 || q + k >= rk1 || x == 0xFFFFFFFFu) continue;
+    if (!((incl >> (AM_REC_OP(x) + sh)) & 1ull)) continue;
+    const uint64_t bit = 1ull << AM_REC_GRP(x);
+    if (x & AM_REC_KILL) killed |= bit;
+    else born |= bit;
+  }
+}
+
+// a lane read's outputs (materialize/4's {ok, Value, NewLastOp, LastOpCt, IsNewSS, Count} or
+// its error status): one coalesced store per column over the wave
+template <int DMAX>
+__device__ __forceinline__ void write_lane(const am_op_log &L, const am_read_result &R, const ReadU<DMAX> &u,
+                                           uint32_t nd, uint64_t n, uint64_t r, uint64_t idb, uint64_t off0,
+                                           uint64_t off1, uint32_t t, int32_t status, const Acc<DMAX> &a, uint64_t v0,
+                                           uint64_t v1, uint32_t vflag, uint32_t ns) {
+  R.status[r] = status;
+  R.flags[r] = (uint8_t)(a.flags & 0xFFu);
+  if (status != AM_OK) return;
+  R.new_last_op[r] = new_last_op_b(L, idb, off0, off1, a.min_excl);
+  const bool ign = u.base_ignore && a.count == 0;
+  const uint32_t opres = ign ? 0u : (a.pres | u.cpres);
+  R.last_ct_ignore[r] = ign ? 1 : 0;
+  R.last_ct_pres[r] = opres;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    if (d >= (int)nd) continue;
+    const uint64_t m = a.mx[d] > u.C0[d] ? a.mx[d] : u.C0[d];
+    R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? m : 0;
+  }
+  R.is_new_ss[r] = a.count > 0;
+  R.count[r] = a.count;
+  if (t == AM_PN || t == AM_LWW) R.value.v0[r] = (int64_t)v0;
+  if (t == AM_LWW) {
+    R.value.v1[r] = v1;
+    R.value.vflag[r] = (uint8_t)vflag;
+  }
+  if (t == AM_AWSET || t == AM_MVREG) R.value.set_len[r] = ns;
+}
+
+// ================================================================ general reads
+// Per-read clocks, cached bases, TxIds or op ids: one lane walks its read's ops in OPL-op tiles.
 template <int DMAX, int OPL>
 struct LTile {
   uint32_t x[OPL][DMAX];
@@ -135,17 +182,9 @@ struct LTile {
   uint64_t v0[OPL], v1[OPL];
 };
 
-#ifndef AMK_LANE_PH_UNROLL
-#define AMK_LANE_PH_UNROLL 1  // quad-scan phases unrolled (experiment switch)
-#endif
-// waves per SIMD the register allocation must allow (experiment switch; 1 = the compiler's choice)
-#ifndef AMK_LANE_MINW
-#define AMK_LANE_MINW 1
-#endif
-
-template <int DMAX, bool GENERAL>
-__global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
-                                                 am_retry next, uint32_t accept) {
+template <int DMAX>
+__global__ void __launch_bounds__(LBLOCK) k_lane_g(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                   am_retry next, uint32_t accept) {
   constexpr int OPL = lopl<DMAX>();
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -155,7 +194,6 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
   const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
   const uint64_t n = B.n_reads;
   ReadU<DMAX> u{};
-  if (!GENERAL) read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
 
   const uint64_t step = (uint64_t)gridDim.x * LBLOCK;
   for (uint64_t b0 = (uint64_t)blockIdx.x * LBLOCK + (threadIdx.x & ~(WAVE - 1)); b0 < nsel; b0 += step) {
@@ -203,7 +241,7 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
 
     // ---- this lane's read ----
     const bool scal = t == AM_PN || t == AM_LWW, setr = t == AM_AWSET || t == AM_MVREG;
-    if (GENERAL && take) read_inputs<DMAX, true, false>(L, nd, B, r, u);
+    if (take) read_inputs<DMAX, true, false>(L, nd, B, r, u);
     PkRead<DMAX> pk;
     pk_setup(u, nd, take ? L.key_tbase[key] : 0, pk);
     const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
@@ -211,22 +249,8 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
     // the first record vector of a set read is in flight with the ops
     const uint64_t q0 = rk0 & ~3ull;
     u32x4 rv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    if (!(AMK_LANE_SKIP & 2) && take && setr && rk1 > rk0) rv = *(const u32x4 *)(L.rec_g + q0);
+    if (take && setr && rk1 > rk0) rv = *(const u32x4 *)(L.rec_g + q0);
 
-    auto load = [&](LTile<DMAX, OPL> &T, uint64_t g) {
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        uint32_t q[OPL] = {};
-        if (d < (int)nd) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
-#pragma unroll
-        for (int k = 0; k < OPL; ++k) T.x[k][d] = q[k];
-      }
-#pragma unroll
-      for (int k = 0; k < OPL; ++k) T.tx[k] = 0, T.v0[k] = 0, T.v1[k] = 0;
-      if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, T.tx);
-      if (!(AMK_LANE_SKIP & 1) && scal) ld_n64<OPL>(L.p0 + g, T.v0);
-      if (!(AMK_LANE_SKIP & 1) && t == AM_LWW) ld_n64<OPL>(L.p1 + g, T.v1);
-    };
     AccP<DMAX> ap;
     Acc<DMAX> a;
     ap.reset();
@@ -237,103 +261,29 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
     lv.reset();
     bool esc = false;
     uint64_t incl = 0;
-    if constexpr (!GENERAL) {
-      // The scan in QUAD shape: the wave's 64 reads in 4 phases of 16; in phase ph quad q
-      // (lanes 4q..4q+3) scans read 16 ph + q, lane j of the quad holding ops [4j, 4j+4) of each
-      // 16-op tile, so each packed column / payload load is 64 / 128 contiguous bytes per quad
-      // (one lane per read reading its own 64-byte segments: 5.0 TB/s on C4's columns, this
-      // shape 6.3, scripts/bw_probe_c4.hip).  The quad's partials are combined by DPP and handed
-      // to the read's own lane (ds_bpermute), which carries on as before.
-      const uint32_t qj = lane & 3u;
-      const uint32_t tk = take ? (t | 0x100u) : 0u;
-#pragma unroll AMK_LANE_PH_UNROLL
-      for (uint32_t ph = 0; ph < 4; ++ph) {
-        const uint32_t src = 16u * ph + (lane >> 2);
-        const uint32_t qt = shfl_u32(tk, src);
-        const uint64_t qo0 = shfl_u64(off0, src), qo1 = shfl_u64(off1, src), qK = shfl_u64(pk.K, src);
-        const bool qtake = (qt >> 8) & 1u;
-        const uint32_t qty = qt & 0xFFu;
-        PkRead<DMAX> qpk;
-        pk_setup(u, nd, qK, qpk);
-        const uint64_t qt0 = qo0 & ~(uint64_t)(OPL - 1);  // the owner's inclusion-bit window
-        AccP<DMAX> qap;
-        qap.reset();
-        PnVal qpv;
-        LwwVal qlv;
-        qpv.reset();
-        qlv.reset();
-        bool qesc = false;
-        uint64_t qincl = 0;
-        for (uint64_t g = (qo0 & ~3ull) + 4 * qj; qtake && g < qo1; g += 16) {
-          uint32_t x[4][DMAX];
+    LTile<DMAX, OPL> cur;
+    for (uint64_t g = t0; take && g < off1; g += OPL) {
 #pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            u32x4 q = {0, 0, 0, 0};
-            if (d < (int)nd) q = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
-            x[0][d] = q.x, x[1][d] = q.y, x[2][d] = q.z, x[3][d] = q.w;
-          }
-          u64x2 a0 = {0, 0}, a1 = {0, 0}, c0 = {0, 0}, c1 = {0, 0};
-          if (!(AMK_LANE_SKIP & 1) && (qty == AM_PN || qty == AM_LWW))
-            a0 = *(const u64x2 *)(L.p0 + g), a1 = *(const u64x2 *)(L.p0 + g + 2);
-          if (!(AMK_LANE_SKIP & 1) && qty == AM_LWW) c0 = *(const u64x2 *)(L.p1 + g), c1 = *(const u64x2 *)(L.p1 + g + 2);
-          const uint64_t tx[4] = {0, 0, 0, 0};
-          const uint32_t ib = pk_tile<DMAX, 4, false>(u, qpk, x, tx, g, qo0, qo1, qap, qesc);
-          qincl |= (uint64_t)ib << (g - qt0);
-          const uint64_t pv0[4] = {a0.x, a0.y, a1.x, a1.y}, pv1[4] = {c0.x, c0.y, c1.x, c1.y};
+      for (int d = 0; d < DMAX; ++d) {
+        uint32_t q[OPL] = {};
+        if (d < (int)nd) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if ((ib >> k) & 1u) {
-              if (qty == AM_PN) qpv.add(pv0[k], 0);
-              else if (qty == AM_LWW) qlv.add(pv0[k], pv1[k]);
-            }
-        }
-        qincl = quad_or_u64(qincl);
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) qap.mx[d] = quad_max_u32(qap.mx[d]);
-        qap.count = quad_sum_u32(qap.count);
-        qap.flags = quad_or_u32(qap.flags | (qesc ? 0x200u : 0u));
-        qap.min_excl = quad_min_u64(qap.min_excl);
-        quad_step_i128<0xB1>(qpv.hi, qpv.lo);
-        quad_step_i128<0x4E>(qpv.hi, qpv.lo);
-        quad_step_lww<0xB1>(qlv);
-        quad_step_lww<0x4E>(qlv);
-        // PN and LWW reads are exclusive: one payload pair travels
-        const uint64_t w0 = qty == AM_LWW ? qlv.ts : (uint64_t)qpv.hi, w1 = qty == AM_LWW ? qlv.val : qpv.lo;
-        const uint32_t fl = qap.flags | (qlv.has ? 0x400u : 0u);
-        // the read's own lane (16 ph + q) takes its quad's values from quad lane 0
-        const uint32_t from = (lane >> 4) == ph ? 4u * (lane & 15u) : lane;
-        const uint64_t r_incl = shfl_u64(qincl, from), r_me = shfl_u64(qap.min_excl, from);
-        const uint64_t r_w0 = shfl_u64(w0, from), r_w1 = shfl_u64(w1, from);
-        const uint32_t r_cnt = shfl_u32(qap.count, from), r_fl = shfl_u32(fl, from);
-        uint32_t r_mx[DMAX];
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) r_mx[d] = d < (int)nd ? shfl_u32(qap.mx[d], from) : 0u;
-        if ((lane >> 4) == ph) {
-          incl = r_incl;
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) ap.mx[d] = r_mx[d];
-          ap.count = r_cnt;
-          ap.flags = r_fl & ~0x600u;
-          ap.min_excl = r_me;
-          esc = (r_fl & 0x200u) != 0;
-          if (t == AM_PN) pv.hi = (int64_t)r_w0, pv.lo = r_w1;
-          if (t == AM_LWW) lv.ts = r_w0, lv.val = r_w1, lv.has = (r_fl & 0x400u) ? 1u : 0u;
-        }
+        for (int k = 0; k < OPL; ++k) cur.x[k][d] = q[k];
       }
-    } else {
-      LTile<DMAX, OPL> cur;
-      for (uint64_t g = t0; take && g < off1; g += OPL) {
-        load(cur, g);
-        const uint32_t ib = pk_tile<DMAX, OPL, GENERAL>(u, pk, cur.x, cur.tx, g, off0, off1, ap, esc);
-        incl |= (uint64_t)ib << (g - t0);
-        if (scal) {
 #pragma unroll
-          for (int k = 0; k < OPL; ++k)
-            if ((ib >> k) & 1u) {
-              if (t == AM_PN) pv.add(cur.v0[k], 0);
-              else lv.add(cur.v0[k], cur.v1[k]);
-            }
-        }
+      for (int k = 0; k < OPL; ++k) cur.tx[k] = 0, cur.v0[k] = 0, cur.v1[k] = 0;
+      if (u.has_txid) ld_n64<OPL>(L.op_txid + g, cur.tx);
+      if (scal) ld_n64<OPL>(L.p0 + g, cur.v0);
+      if (t == AM_LWW) ld_n64<OPL>(L.p1 + g, cur.v1);
+      const uint32_t ib = pk_tile<DMAX, OPL, true>(u, pk, cur.x, cur.tx, g, off0, off1, ap, esc);
+      incl |= (uint64_t)ib << (g - t0);
+      if (scal) {
+#pragma unroll
+        for (int k = 0; k < OPL; ++k)
+          if ((ib >> k) & 1u) {
+            if (t == AM_PN) pv.add(cur.v0[k], 0);
+            else lv.add(cur.v0[k], cur.v1[k]);
+          }
       }
     }
     if (esc) {  // rare: ops outside the packed view, from the full columns
@@ -343,9 +293,9 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
         const uint32_t meta = L.op_meta[p];
-        const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
-        const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
-        if (!eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], sv, sp, txm, p, a)) continue;
+        const uint32_t sp = L.snap_pres ? L.snap_pres[p] : u.allmask;
+        const bool txm = u.has_txid && L.op_txid[p] == u.txid;
+        if (!eval_op<DMAX, true>(u, meta, L.commit_time[p], sv, sp, txm, p, a)) continue;
         if (scal) {
           if (t == AM_PN) pv.add(L.p0[p], 0);
           else lv.add(L.p0[p], L.p1[p]);
@@ -358,13 +308,11 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
     int32_t status = (a.flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
 
     // ---- set reads: records of included ops -> born / killed groups -> survivors ----
-    uint32_t ns = 0;
     uint64_t galive = 0, gsrc = 0, gdst = 0;  // this lane's survivors for the wave's gather
+    uint32_t ns = 0;
     if (take && setr) {
       uint64_t born = 0, killed = 0;
-      // 16 records per step: the first vector was prefetched with the ops, the other three
-      // are loaded together (an MV read of 16 ops has 31 records: two steps, not eight)
-      for (uint64_t q = q0; !(AMK_LANE_SKIP & 2) && q < rk1; q += 16) {
+      for (uint64_t q = q0; q < rk1; q += 16) {
         u32x4 cv[4];
         cv[0] = rv;
 #pragma unroll
@@ -372,36 +320,16 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
           cv[j] = q + 4 * j < rk1 ? *(const u32x4 *)(L.rec_g + q + 4 * j) : u32x4{~0u, ~0u, ~0u, ~0u};
         if (q + 16 < rk1) rv = *(const u32x4 *)(L.rec_g + q + 16);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t xs[4] = {cv[j].x, cv[j].y, cv[j].z, cv[j].w};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint64_t qq = q + 4 * j + k;
-            const uint32_t x = xs[k];
-            if (qq < rk0 || qq >= rk1 || x == 0xFFFFFFFFu) continue;
-            if (!((incl >> (AM_REC_OP(x) + sh)) & 1ull)) continue;
-            const uint64_t bit = 1ull << AM_REC_GRP(x);
-            if (x & AM_REC_KILL) killed |= bit;
-            else born |= bit;
-          }
-        }
+        for (int j = 0; j < 4; ++j) rec_bits(cv[j], q + 4 * j, rk0, rk1, incl, sh, born, killed);
       }
       if (status == AM_OK) {
         const uint64_t alive = born & ~killed;
         ns = (uint32_t)__popcll(alive);
         const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
-        if (ns > ocap) {
-          status = AM_ERR_CAPACITY;
-        } else if (!(AMK_LANE_SKIP & 4)) {
-          galive = alive, gsrc = rk0, gdst = ooff;
-        }
+        if (ns > ocap) status = AM_ERR_CAPACITY;
+        else galive = alive, gsrc = rk0, gdst = ooff;
       }
     }
-    // survivors of every set read of the wave in one gather: the wave's concatenated survivor
-    // list (read order, group order within a read) is split over all 64 lanes, so a wave issues
-    // up to 256 independent 16-byte group loads at once and writes each read's pairs with
-    // adjacent lanes (one lane per read looping over its survivors serialized a memory
-    // latency per four survivors)
     wave_gather(L, R, (uint32_t)__popcll(galive), galive, gsrc, gdst, lane);
 
     // ---- outputs ----
@@ -411,14 +339,14 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
       if (t == AM_PN) {
         int64_t hi = pv.hi;
         uint64_t lo = pv.lo;
-        const int64_t bv = (GENERAL && B.base.v0) ? B.base.v0[r] : 0;
+        const int64_t bv = B.base.v0 ? B.base.v0[r] : 0;
         add128(hi, lo, bv < 0 ? -1 : 0, (uint64_t)bv);
         if (status == AM_OK && hi != ((int64_t)lo < 0 ? -1 : 0)) status = AM_ERR_OVERFLOW;
         v0 = lo;
       } else if (t == AM_LWW) {
         uint64_t bts = 0, bval = 0;
         uint32_t bbin = 1;  // new() = {0, <<>>}
-        if (GENERAL && B.base.v0) {
+        if (B.base.v0) {
           bts = (uint64_t)B.base.v0[r];
           bval = B.base.v1 ? B.base.v1[r] : 0;
           bbin = B.base.vflag ? B.base.vflag[r] : 0;
@@ -428,62 +356,530 @@ __global__ void __launch_bounds__(LBLOCK, AMK_LANE_MINW) k_lane(am_op_log L, am_
         v1 = win ? lv.val : bval;
         vflag = win ? 0 : bbin;
       }
-      R.status[r] = status;
-      if (AMK_LANE_SKIP & 8) continue;
-      R.flags[r] = (uint8_t)(a.flags & 0xFFu);
-      if (status == AM_OK) {
-        R.new_last_op[r] = new_last_op(L, key, off0, off1, a.min_excl);
-        const bool ign = u.base_ignore && a.count == 0;
-        const uint32_t opres = ign ? 0u : (a.pres | u.cpres);
-        R.last_ct_ignore[r] = ign ? 1 : 0;
-        R.last_ct_pres[r] = opres;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          if (d >= (int)nd) continue;
-          const uint64_t m = a.mx[d] > u.C0[d] ? a.mx[d] : u.C0[d];
-          R.last_ct[(uint64_t)d * n + r] = ((opres >> d) & 1u) ? m : 0;
-        }
-        R.is_new_ss[r] = a.count > 0;
-        R.count[r] = a.count;
-        if (scal) R.value.v0[r] = (int64_t)v0;
-        if (t == AM_LWW) {
-          R.value.v1[r] = v1;
-          R.value.vflag[r] = (uint8_t)vflag;
-        }
-        if (setr) R.value.set_len[r] = ns;
-      }
+      write_lane(L, R, u, nd, n, r, L.key_id_base ? L.key_id_base[key] : 1, off0, off1, t, status, a, v0, v1, vflag,
+                 ns);
     }
   }
 }
 
-template <int D, bool GENERAL>
+// ================================================================ batch-clock reads
+// One MinSnapshotTime for the batch, base ignore, no TxIds (the bench's and a GST read's shape).
+// The work is VALU-issue-bound at this size (PMC, C4: waves issue ~90 % of the time at two waves
+// per SIMD), so the kernel is built around doing little per op:
+//   * persistent waves, one 64-read block at a time; block j+1's key metadata and block j+2's
+//     read indices are loaded behind block j's scan loads, and block j+1 is published to the
+//     other slot buffer before j's gather and output stores (a wave's loads and stores retire
+//     through one in-order counter), so a block starts with nothing to wait for;
+//   * publishing sorts the block's reads by type into the 64 scan positions: a phase (16
+//     positions) holds one or two types, and the payload (PN sum / LWW max) and record (sets)
+//     code of a type runs only in the phases that hold it (wave-uniform branches);
+//   * the scan is quad-shaped: the quad at position p scans that read's first 16-op tile, lane j
+//     ops [4j, 4j + 4) -- 64 contiguous bytes per packed column per quad -- with the ops'
+//     payload or records in the same loads; the loads of QPH phases are issued together;
+//   * positions, inclusion bits, groups and the oldest-excluded index are 32-bit in the scan
+//     (the quad takes reads of at most 16 ops and 32 groups; the thresholds S - K are computed
+//     once per read by its lane and published with it); a set read ORs its included ops'
+//     group masks (the gmask view: births | effective kills per op) instead of testing records;
+//   * a read the quad does not take (longer logs up to 64 ops / 64 groups, an escaped op) is
+//     finished by its own lane; results come back through LDS; survivors leave through one
+//     gather per wave; each lane writes its read's outputs (coalesced stores).
+#ifndef AMK_QPH
+#define AMK_QPH 4
+#endif
+template <int DMAX>
+constexpr int qph() {
+  return DMAX <= 4 ? AMK_QPH : DMAX <= 8 ? (AMK_QPH < 2 ? AMK_QPH : 2) : 1;
+}
+template <int DMAX>
+struct QSlot {  // the read at a scan position, for the quad that scans it
+  uint64_t off0, rk0;
+  uint32_t nops, nrec, tk, ctl;  // ctl: AM_FLAG_MISSING_DC_LOGGED | never << 31
+  uint32_t thr[DMAX];            // MinSnapshotTime - K per DC (pk_clamp)
+};
+struct QOwn {  // the lane's own read of a block (registers, from q_publish)
+  uint64_t off0, K, rk0, idb, ooff;
+  uint32_t nops, nrec, tk, r, ocap, pos;
+};
+template <int DMAX>
+struct QRes {  // the quad's results for the read at position p
+  uint64_t w0, w1;                 // PN 128-bit sum (hi, lo) | LWW (ts, value)
+  uint32_t incl, born, killed;     // inclusion bits from off0 & ~3; groups born / killed
+  uint32_t mex, count, flags;      // oldest excluded op (from off0 & ~3) or ~0; count; flags
+  uint32_t mx[DMAX];
+};
+constexpr uint32_t QGL = 256;  // survivor-list entries per gather round
+template <int DMAX>
+struct QSmem {
+  QSlot<DMAX> slot[WAVE];  // by scan position; rewritten for the next block once scanned
+  QRes<DMAX> res[WAVE];
+  uint64_t grk0[WAVE], gdst[WAVE];  // survivor gather: group base, output base by position
+  uint16_t glist[QGL];              // survivor j of the round: owner position << 6 | group
+};
+// tk: the read's type | taken | scanned by its quad
+constexpr uint32_t QT_TAKE = 0x100u, QT_QUAD = 0x200u, QF_ESC = 0x200u, QF_HAS = 0x400u;
+constexpr uint32_t QC_NEVER = 0x80000000u;
+
+// A block read's index, key and type, and its key's metadata, as loaded: every load of a lane
+// has one address and no predicate beyond validity (invalid lanes read row 0), and nothing
+// loaded is combined until it is used -- so a block's metadata stays in flight behind the
+// previous block's scan and the wave never waits for it early.
+struct QPre {
+  uint64_t key;
+  uint32_t r, t, ok;  // ok: i < nsel
+};
+struct QMeta {
+  uint64_t key, off0, off1, K, rk0, rk1, ooff, o1, idb;
+  uint32_t r, t, kt, kfl, G, ok;  // ok: i < nsel and key < n_keys
+};
+template <bool SEL>
+__device__ __forceinline__ QPre q_pre(const am_read_batch &B, const am_sel &S, uint32_t sel0, uint64_t nsel, uint64_t i) {
+  QPre p;
+  p.ok = i < nsel;
+  const uint64_t ii = p.ok ? i : 0;
+  p.r = SEL ? S.idx[sel0 + ii] : (uint32_t)ii;
+  p.key = B.key[p.r];
+  p.t = B.type[p.r];
+  return p;
+}
+__device__ __forceinline__ QMeta q_meta(const am_op_log &L, const am_read_result &R, const QPre &p) {
+  QMeta m;
+  m.key = p.key, m.r = p.r, m.t = p.t;
+  m.ok = p.ok && p.key < L.n_keys;
+  const uint64_t k = m.ok ? p.key : 0;
+  const uint64_t *ke = L.key_end ? L.key_end : L.key_off + 1;
+  const uint64_t *rke = L.rec_key_end ? L.rec_key_end : L.rec_key_off + 1;
+  m.off0 = L.key_off[k];
+  m.off1 = ke[k];
+  m.kt = L.key_type[k];
+  m.kfl = (L.key_flags ? L.key_flags : L.key_type)[k];  // (key_type: a dummy, unused)
+  m.K = L.key_tbase[k];
+  m.idb = (L.key_id_base ? L.key_id_base : L.key_off)[k];  // (key_off: a dummy, unused)
+  // set fields for every read: the block's reads cover one span of each column, so the
+  // lines are fetched whatever the types
+  m.G = L.key_ngrp[k];
+  m.rk0 = L.rec_key_off[k];
+  m.rk1 = rke[k];
+  const uint64_t *so = R.value.set_off ? R.value.set_off : L.key_off;  // (key_off: a dummy)
+  m.ooff = so[m.r];
+  m.o1 = so[m.r + 1];
+  return m;
+}
+
+// A block's reads -> their scan positions in slot[]: errors get their status, reads the tier
+// does not take go to `next` (one atomic per wave), the rest are placed by type (PN, LWW, AW, MV,
+// then the reads their own lanes finish, then the rest).  Returns the lane's position; *any
+// whether any read is taken.
+template <int DMAX>
+__device__ __forceinline__ QOwn q_publish(const am_op_log &L, const am_read_result &R, const ReadU<DMAX> &u,
+                                          uint32_t nd, const QMeta &m, bool inb, uint32_t accept, am_retry next,
+                                          QSlot<DMAX> *slot, uint32_t lane, bool &any) {
+  const uint64_t lt = (1ull << lane) - 1ull;
+  bool take = false, hand = false;
+  if (inb) {
+    int32_t st = AM_OK;
+    if (!m.ok || m.t < AM_PN || m.t > AM_BCOUNTER) st = AM_ERR_INVALID;
+    else if (m.off1 > m.off0 && (m.kt != m.t || (L.key_flags && (m.kfl & AM_KEY_MIXED_TYPES))))
+      st = AM_ERR_CORRUPTED_OPS_CACHE;
+    if (st == AM_OK) {
+      bool ok = ((accept >> m.t) & 1u) && m.off1 - (m.off0 & ~3ull) <= LBITS;
+      if (ok && (m.t == AM_AWSET || m.t == AM_MVREG)) ok = m.G != AM_NGRP_NONE && m.G <= LGRP;
+      take = ok;
+      hand = !ok;
+    } else {
+      R.status[m.r] = st;
+      R.flags[m.r] = 0;
+    }
+  }
+  const uint64_t hm = __ballot(hand);
+  if (hm) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(next.count, (uint32_t)__popcll(hm));
+    base = uniform_u32(base);
+    if (hand) next.list[base + (uint32_t)__popcll(hm & lt)] = m.r;
+  }
+  const bool setr = m.t == AM_AWSET || m.t == AM_MVREG;
+  const bool quad = take && m.off1 <= (m.off0 & ~3ull) + 16 && (!setr || (L.gmask && m.G <= AM_GMASK_MAX_GRP));
+  // scan position: quad reads by type, then the lane-finished reads, then the rest
+  const uint32_t cls = quad ? m.t - AM_PN : take ? 4u : 5u;
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t c = 0; c < 6; ++c) {
+    const uint64_t mc = __ballot(cls == c);
+    if (cls == c) pos += (uint32_t)__popcll(mc & lt);
+    if (cls > c) pos += (uint32_t)__popcll(mc);
+  }
+  QOwn o;
+  o.off0 = m.off0, o.K = m.K, o.rk0 = setr ? m.rk0 : 0, o.idb = L.key_id_base ? m.idb : 1, o.ooff = m.ooff;
+  o.nops = (uint32_t)(m.off1 - m.off0), o.nrec = setr ? (uint32_t)(m.rk1 - m.rk0) : 0u, o.r = m.r;
+  o.ocap = setr ? (uint32_t)min(m.o1 - m.ooff, (uint64_t)0xFFFFFFFFu) : 0u;
+  o.tk = take ? (m.t | QT_TAKE | (quad ? QT_QUAD : 0u)) : 0u;
+  o.pos = pos;
+  QSlot<DMAX> &w = slot[pos];
+  w.off0 = o.off0, w.rk0 = o.rk0, w.nops = o.nops, w.nrec = o.nrec, w.tk = o.tk;
+  if (quad) {  // the packed thresholds, once per read (am_wave.h pk_setup)
+    PkRead<DMAX> pk;
+    pk_setup(u, nd, m.K, pk);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) w.thr[d] = pk.thr[d];
+    w.ctl = pk.miss | (pk.never ? QC_NEVER : 0u);
+  }
+  any = __ballot(take) != 0;
+  return o;
+}
+
+// The wave's survivor gather through the LDS list: the read at position p with n survivors
+// (alive bits of its groups) owns entries excl .. excl + n - 1 of the wave's list; each round
+// lists 256 entries (position, group), then lane j takes entries j, j + 64, ...: the group pair
+// from grp[2 (rk0 + group)] into output slot gdst + entry.  All 64 lanes must be active.
+template <int DMAX>
+__device__ __forceinline__ void q_gather(const am_op_log &L, const am_read_result &R, QSmem<DMAX> &sm, uint64_t alive,
+                                         uint64_t rk0, uint64_t ooff, uint32_t pos, uint32_t lane) {
+  const uint32_t n = (uint32_t)__popcll(alive);
+  const uint32_t incl = wave_incl_scan_u32(n, lane), excl = incl - n;
+  const uint32_t T = lane_u32(incl, WAVE - 1);
+  if (T == 0) return;
+  sm.gdst[pos] = ooff - excl;
+  sm.grk0[pos] = rk0;
+  for (uint32_t base = 0; base < T; base += QGL) {
+    uint32_t k = excl;
+    for (uint64_t bits = alive; bits && k < base + QGL; bits &= bits - 1, ++k)
+      if (k >= base) sm.glist[k - base] = (uint16_t)(pos << 6 | (uint32_t)__builtin_ctzll(bits));
+    wave_sync();
+    constexpr int K = QGL / WAVE;
+    u64x2 ab[K];
+    uint64_t to[K];
+#pragma unroll
+    for (int e = 0; e < K; ++e) {  // unpredicated loads (entry T - 1 repeated past the end)
+      const uint32_t j = base + (uint32_t)e * WAVE + lane, jj = j < T ? j : T - 1;
+      const uint32_t x = sm.glist[jj - base], own = x >> 6;
+      to[e] = j < T ? sm.gdst[own] + j : ~0ull;
+      ab[e] = *(const u64x2 *)(L.grp + 2 * (sm.grk0[own] + (x & 63u)));
+    }
+#pragma unroll
+    for (int e = 0; e < K; ++e)
+      if (to[e] != ~0ull) R.value.set_a[to[e]] = ab[e].x, R.value.set_b[to[e]] = ab[e].y;
+    wave_sync();
+  }
+}
+
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return (uint64_t)hi << 32 | lo; }
+
+// the included ops' payload of an op tile (bit k of ib: op k of the lane): PN 128-bit sum, LWW max
+__device__ __forceinline__ void q_pn(uint32_t ib, u32x4 e0, u32x4 e1, PnVal &pv) {
+  const uint64_t v[4] = {u64of(e0.x, e0.y), u64of(e0.z, e0.w), u64of(e1.x, e1.y), u64of(e1.z, e1.w)};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t d = ((ib >> k) & 1u) ? (int64_t)v[k] : 0;
+    add128(pv.hi, pv.lo, d < 0 ? -1 : 0, (uint64_t)d);
+  }
+}
+__device__ __forceinline__ void q_lww(uint32_t ib, u32x4 e0, u32x4 e1, u32x4 e2, u32x4 e3, LwwVal &lv) {
+  const uint64_t ts[4] = {u64of(e0.x, e0.y), u64of(e0.z, e0.w), u64of(e1.x, e1.y), u64of(e1.z, e1.w)};
+  const uint64_t va[4] = {u64of(e2.x, e2.y), u64of(e2.z, e2.w), u64of(e3.x, e3.y), u64of(e3.z, e3.w)};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool in = (ib >> k) & 1u;
+    const bool gt = in && (!lv.has || ts[k] > lv.ts || (ts[k] == lv.ts && va[k] > lv.val));
+    lv.ts = gt ? ts[k] : lv.ts;
+    lv.val = gt ? va[k] : lv.val;
+    lv.has |= in ? 1u : 0u;
+  }
+}
+template <int DMAX, bool SEL>
+__global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                   am_retry next, uint32_t accept) {
+  constexpr int NPH = qph<DMAX>();
+  __shared__ QSmem<DMAX> smem[LBLOCK / WAVE];
+  QSmem<DMAX> &sm = smem[threadIdx.x / WAVE];
+  const uint32_t lane = threadIdx.x & (WAVE - 1), qj = lane & 3u, qq = lane >> 2;
+  const uint32_t nd = L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = SEL ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = SEL ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+  const uint64_t n = B.n_reads;
+  ReadU<DMAX> u{};
+  read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
+  const uint64_t tx0[4] = {0, 0, 0, 0};
+
+  const uint64_t step = (uint64_t)gridDim.x * LBLOCK;
+  const uint64_t first = (uint64_t)blockIdx.x * LBLOCK + (threadIdx.x & ~(WAVE - 1));
+  QSlot<DMAX> *const slot = sm.slot;
+  QPre pn = q_pre<SEL>(B, S, sel0, nsel, first + step + lane);
+  bool any = false;
+  QOwn own = q_publish<DMAX>(L, R, u, nd, q_meta(L, R, q_pre<SEL>(B, S, sel0, nsel, first + lane)),
+                             first + lane < nsel, accept, next, slot, lane, any);
+  wave_sync();
+  for (uint64_t b0 = first; b0 < nsel; b0 += step) {
+    QMeta m;
+    if (!any) {
+      m = q_meta(L, R, pn);
+      pn = q_pre<SEL>(B, S, sel0, nsel, b0 + 2 * step + lane);
+      own = q_publish<DMAX>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
+      wave_sync();
+      continue;
+    }
+    const QOwn me = own;
+
+    // ---- the quad scans: NPH phases' loads in flight together.  Unpredicated loads: a word a
+    //      read does not need is loaded from its column's first line (one line for the whole
+    //      chip, cached) and ignored, so the loads issue back to back with no branch between
+    //      them and the wave's later waits count them exactly ----
+#ifndef AMK_QPG_UNROLL
+#define AMK_QPG_UNROLL 4
+#endif
+#pragma unroll AMK_QPG_UNROLL
+    for (int pg = 0; pg < 4; pg += NPH) {
+      u32x4 xv[NPH][DMAX], wv[NPH][4];
+#pragma unroll
+      for (int h = 0; h < NPH; ++h) {
+        const QSlot<DMAX> &sl = slot[16 * (pg + h) + qq];
+        const uint32_t tk = sl.tk, ty = tk & 0xFFu;
+        const bool qt = (tk & QT_QUAD) != 0, setr = ty == AM_AWSET || ty == AM_MVREG;
+        const uint64_t o0 = sl.off0, o1 = o0 + sl.nops, g = (o0 & ~3ull) + 4 * qj;
+        const bool lo = qt && g < o1;
+        const uint64_t gg = lo ? g : 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          xv[h][d] = d < (int)nd ? *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + gg) : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // PN p0 | LWW p0, p1 | a set read's group masks
+          const bool v = lo && (e < 2 || ty == AM_LWW);
+          const uint64_t *col = setr ? L.gmask : (e < 2 ? L.p0 : L.p1);
+          wv[h][e] = *(const u32x4 *)((setr && e >= 2 ? L.p0 : col) + (v ? g + 2 * (e & 1) : 0));
+        }
+      }
+      if (pg == 0) {  // the next block's metadata, behind this block's scan loads
+        m = q_meta(L, R, pn);
+        pn = q_pre<SEL>(B, S, sel0, nsel, b0 + 2 * step + lane);
+      }
+#pragma unroll
+      for (int h = 0; h < NPH; ++h) {
+        const uint32_t i = 16 * (pg + h) + qq;
+        const QSlot<DMAX> &sl = slot[i];
+        const uint32_t tk = sl.tk, ty = tk & 0xFFu;
+        const bool qt = (tk & QT_QUAD) != 0;
+        // the phase's types (wave-uniform): code for a type runs only where it is present
+        const bool tb = __ballot(qt && ty == AM_PN) != 0;
+        const bool tl = __ballot(qt && ty == AM_LWW) != 0;
+        const bool ts = __ballot(qt && (ty == AM_AWSET || ty == AM_MVREG)) != 0;
+        if (!tb && !tl && !ts) continue;
+        const uint32_t rel0 = (uint32_t)(sl.off0 & 3u), n0 = sl.nops, ctl = sl.ctl;
+        // ---- ops [4 qj, 4 qj + 4) of the tile: is_op_in_snapshot/7 on the packed entries ----
+        uint32_t ib = 0, ev = 0, esc = 0, cnt = 0, mex = 0xFFFFFFFFu;
+        uint32_t mx[DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) mx[d] = 0;
+        if (qt) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t p = 4 * qj + (uint32_t)k;
+            const bool inr = p - rel0 < n0;  // (unsigned: p < rel0 wraps)
+            const uint32_t x0 = xv[h][0][k];
+            const bool e = x0 == AM_PK_ESC;
+            uint32_t over = 0;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(xv[h][d][k], sl.thr[d]);
+            const bool cand = inr && !e;
+            const bool in = cand && !(ctl & QC_NEVER) && over == 0;
+            ib |= (uint32_t)in << k;
+            ev |= (uint32_t)cand << k;
+            esc |= (uint32_t)(inr && e);
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) mx[d] = max(mx[d], in ? xv[h][d][k] : 0u);
+          }
+          cnt = (uint32_t)__popc(ib);
+          const uint32_t ex = ev & ~ib;
+          mex = ex ? 4 * qj + (uint32_t)__builtin_ctz(ex) : 0xFFFFFFFFu;
+        }
+        PnVal qpv;
+        LwwVal qlv;
+        qpv.reset();
+        qlv.reset();
+        if (tb && ty == AM_PN) q_pn(ib, wv[h][0], wv[h][1], qpv);
+        if (tl && ty == AM_LWW) q_lww(ib, wv[h][0], wv[h][1], wv[h][2], wv[h][3], qlv);
+        const uint32_t qincl = quad_or_u32(ib << (4 * qj));
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? quad_max_u32(mx[d]) : 0u;
+        cnt = quad_sum_u32(cnt);
+        const uint32_t fl = quad_or_u32((ev ? (ctl & AM_FLAG_MISSING_DC_LOGGED) : 0u) | (esc ? QF_ESC : 0u));
+        mex = quad_min_u32(mex);
+        if (tb) {
+          quad_step_i128<0xB1>(qpv.hi, qpv.lo);
+          quad_step_i128<0x4E>(qpv.hi, qpv.lo);
+        }
+        if (tl) {
+          quad_step_lww<0xB1>(qlv);
+          quad_step_lww<0x4E>(qlv);
+        }
+        // ---- set reads: the included ops' group masks -> born / killed groups ----
+        uint32_t born = 0, killed = 0;
+        if (ts) {
+          if (ty == AM_AWSET || ty == AM_MVREG) {
+            const uint32_t gw[8] = {wv[h][0].x, wv[h][0].y, wv[h][0].z, wv[h][0].w,
+                                    wv[h][1].x, wv[h][1].y, wv[h][1].z, wv[h][1].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const bool in = (ib >> k) & 1u;
+              born |= in ? gw[2 * k] : 0u;
+              killed |= in ? gw[2 * k + 1] : 0u;
+            }
+          }
+          born = quad_or_u32(born);
+          killed = quad_or_u32(killed);
+        }
+        if (qj == 0 && qt) {
+          QRes<DMAX> &o = sm.res[i];
+          o.w0 = ty == AM_LWW ? qlv.ts : (uint64_t)qpv.hi;
+          o.w1 = ty == AM_LWW ? qlv.val : qpv.lo;
+          o.incl = qincl, o.born = born, o.killed = killed, o.mex = mex, o.count = cnt;
+          o.flags = fl | (qlv.has ? QF_HAS : 0u);
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) o.mx[d] = mx[d];
+        }
+      }
+    }
+    // the next block's reads: statuses, hand-offs, positions (its metadata has arrived by now;
+    // the slots are free once scanned)
+    wave_sync();
+    own = q_publish<DMAX>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
+    wave_sync();
+
+    // ---- the lane's own read: its quad's results, or (a longer read) its own scan ----
+    const uint32_t tk = me.tk, t = tk & 0xFFu;
+    const bool tk_take = (tk & QT_TAKE) != 0;
+    const bool scal = t == AM_PN || t == AM_LWW, setr = t == AM_AWSET || t == AM_MVREG;
+    const uint64_t off0 = me.off0, off1 = off0 + me.nops, a0 = off0 & ~3ull, K = me.K;
+    const uint64_t rk0 = me.rk0, rk1 = rk0 + me.nrec;
+    AccP<DMAX> ap;
+    Acc<DMAX> a;
+    ap.reset();
+    a.reset();
+    PnVal pv;
+    LwwVal lv;
+    pv.reset();
+    lv.reset();
+    uint64_t incl = 0, born = 0, killed = 0;
+    bool esc = false;
+    if (tk & QT_QUAD) {
+      const QRes<DMAX> &o = sm.res[me.pos];
+      incl = o.incl, born = o.born, killed = o.killed;
+      ap.min_excl = o.mex == 0xFFFFFFFFu ? NONE : a0 + o.mex;
+      ap.count = o.count, ap.flags = o.flags & ~(QF_ESC | QF_HAS);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) ap.mx[d] = o.mx[d];
+      esc = (o.flags & QF_ESC) != 0;
+      if (t == AM_PN) pv.hi = (int64_t)o.w0, pv.lo = o.w1;
+      if (t == AM_LWW) lv.ts = o.w0, lv.val = o.w1, lv.has = (o.flags & QF_HAS) ? 1u : 0u;
+    } else if (tk_take) {  // longer logs of the lane tier (up to 64 ops / 64 groups)
+      PkRead<DMAX> pk;
+      pk_setup(u, nd, K, pk);
+      for (uint64_t g = a0; g < off1; g += 4) {
+        uint32_t x[4][DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          const u32x4 c = d < (int)nd ? *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g) : u32x4{0, 0, 0, 0};
+          x[0][d] = c.x, x[1][d] = c.y, x[2][d] = c.z, x[3][d] = c.w;
+        }
+        u32x4 e0 = {0, 0, 0, 0}, e1 = e0, e2 = e0, e3 = e0;
+        if (scal) e0 = *(const u32x4 *)(L.p0 + g), e1 = *(const u32x4 *)(L.p0 + g + 2);
+        if (t == AM_LWW) e2 = *(const u32x4 *)(L.p1 + g), e3 = *(const u32x4 *)(L.p1 + g + 2);
+        const uint32_t ib = pk_tile<DMAX, 4, false>(u, pk, x, tx0, g, off0, off1, ap, esc);
+        incl |= (uint64_t)ib << (g - a0);
+        if (t == AM_PN) q_pn(ib, e0, e1, pv);
+        if (t == AM_LWW) q_lww(ib, e0, e1, e2, e3, lv);
+      }
+      for (uint64_t q = rk0 & ~3ull; setr && q < rk1; q += 4)
+        rec_bits(*(const u32x4 *)(L.rec_g + q), q, rk0, rk1, incl, (uint32_t)(off0 - a0), born, killed);
+    }
+    if (esc) {  // rare: ops outside the packed view, from the full columns
+      uint64_t ek = 0;  // included set ops among them: the records are redone with them
+      for (uint64_t p = off0; p < off1; ++p) {
+        if (L.pk_vc[p] != AM_PK_ESC) continue;
+        uint64_t sv[DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+        const uint32_t meta = L.op_meta[p];
+        if (!eval_op<DMAX, false>(u, meta, L.commit_time[p], sv, u.allmask, false, p, a)) continue;
+        if (scal) {
+          if (t == AM_PN) pv.add(L.p0[p], 0);
+          else lv.add(L.p0[p], L.p1[p]);
+        } else if (!(meta & AM_META_BAD)) {
+          ek |= 1ull << (p - a0);
+        }
+      }
+      if (setr && ek) {
+        incl |= ek;
+        born = 0, killed = 0;
+        for (uint64_t q = rk0 & ~3ull; q < rk1; q += 4)
+          rec_bits(*(const u32x4 *)(L.rec_g + q), q, rk0, rk1, incl, (uint32_t)(off0 - a0), born, killed);
+      }
+    }
+    pk_fold(ap, K, u.allmask, a);
+    int32_t status = (a.flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+    uint64_t galive = 0;
+    uint32_t ns = 0;
+    const uint64_t ooff = me.ooff;
+    if (tk_take && setr && status == AM_OK) {
+      const uint64_t alive = born & ~killed;
+      ns = (uint32_t)__popcll(alive);
+      if (ns > me.ocap) status = AM_ERR_CAPACITY;
+      else galive = alive;
+    }
+    const uint64_t r = me.r, idb = me.idb;
+    q_gather<DMAX>(L, R, sm, galive, rk0, ooff, me.pos, lane);
+
+    if (tk_take) {
+      uint64_t v0 = 0, v1 = 0;
+      uint32_t vflag = 0;
+      if (t == AM_PN) {
+        if (status == AM_OK && pv.hi != ((int64_t)pv.lo < 0 ? -1 : 0)) status = AM_ERR_OVERFLOW;
+        v0 = pv.lo;
+      } else if (t == AM_LWW) {  // base new() = {0, <<>>}: any op wins
+        v0 = lv.has ? lv.ts : 0;
+        v1 = lv.has ? lv.val : 0;
+        vflag = lv.has ? 0u : 1u;
+      }
+      write_lane(L, R, u, nd, n, r, idb, off0, off1, t, status, a, v0, v1, vflag, ns);
+    }
+    wave_sync();  // the LDS area is rewritten by the next block
+  }
+}
+
+template <int D>
 int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
-             uint32_t accept) {
-  static int occ = 0;
+             uint32_t accept, bool general) {
+  static int occ_g = 0, occ_q = 0;
+  int &occ = general ? occ_g : occ_q;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane<D, GENERAL>, LBLOCK, 0) != hipSuccess || occ < 1)
-      occ = 2;
+    const hipError_t e = general ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane_g<D>, LBLOCK, 0)
+                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane_q<D, false>, LBLOCK, 0);
+    if (e != hipSuccess || occ < 1) occ = 2;
   }
   uint64_t blocks = (B->n_reads + LBLOCK - 1) / LBLOCK, cap = (uint64_t)ctx->n_cu * occ;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
-  hipLaunchKernelGGL((k_lane<D, GENERAL>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next,
-                     accept);
+  if (general)
+    hipLaunchKernelGGL((k_lane_g<D>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next, accept);
+  else if (S.idx)
+    hipLaunchKernelGGL((k_lane_q<D, true>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next,
+                       accept);
+  else
+    hipLaunchKernelGGL((k_lane_q<D, false>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next,
+                       accept);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }
 
-template <bool GENERAL>
 int launch_g(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
-             uint32_t accept) {
+             uint32_t accept, bool general) {
   const uint32_t nd = L->n_dc;
-  if (nd <= 1) return launch_d<1, GENERAL>(ctx, L, B, R, S, next, accept);
-  if (nd <= 2) return launch_d<2, GENERAL>(ctx, L, B, R, S, next, accept);
-  if (nd <= 3) return launch_d<3, GENERAL>(ctx, L, B, R, S, next, accept);
-  if (nd <= 4) return launch_d<4, GENERAL>(ctx, L, B, R, S, next, accept);
-  if (nd <= 8) return launch_d<8, GENERAL>(ctx, L, B, R, S, next, accept);
-  if (nd <= 16) return launch_d<16, GENERAL>(ctx, L, B, R, S, next, accept);
-  return launch_d<32, GENERAL>(ctx, L, B, R, S, next, accept);
+  if (nd <= 1) return launch_d<1>(ctx, L, B, R, S, next, accept, general);
+  if (nd <= 2) return launch_d<2>(ctx, L, B, R, S, next, accept, general);
+  if (nd <= 3) return launch_d<3>(ctx, L, B, R, S, next, accept, general);
+  if (nd <= 4) return launch_d<4>(ctx, L, B, R, S, next, accept, general);
+  if (nd <= 8) return launch_d<8>(ctx, L, B, R, S, next, accept, general);
+  if (nd <= 16) return launch_d<16>(ctx, L, B, R, S, next, accept, general);
+  return launch_d<32>(ctx, L, B, R, S, next, accept, general);
 }
 
 }  // namespace
@@ -500,6 +896,5 @@ uint32_t am_lane_accept(const am_op_log *L, const am_read_result *R, uint32_t ty
 
 int am_launch_lanes(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                     am_retry next, uint32_t accept) {
-  return am_batch_general(L, B) ? launch_g<true>(ctx, L, B, R, S, next, accept)
-                                : launch_g<false>(ctx, L, B, R, S, next, accept);
+  return launch_g(ctx, L, B, R, S, next, accept, am_batch_general(L, B));
 }

@@ -99,6 +99,24 @@ __global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, ui
   }
 }
 
+// the group-mask view (include/antidote_mat.h gmask): a key with at most AM_GMASK_MAX_GRP
+// groups gets its records folded per op -- births into bits 0-31, effective kills into 32-63
+// (the builder already dropped the ineffective kills: those slots are 0xFFFFFFFF).  One thread
+// per key walks its records (a key's records are few when it has so few groups); every other op
+// keeps the zero of the memset.
+__global__ void k_gmask(am_op_log L, uint64_t *gm) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < L.n_keys; k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t G = L.key_ngrp[k];
+    if (G == AM_NGRP_NONE || G > AM_GMASK_MAX_GRP) continue;
+    const uint64_t off0 = L.key_off[k], r1 = am_rkend(L, k);
+    for (uint64_t r = L.rec_key_off[k]; r < r1; ++r) {
+      const uint32_t x = L.rec_g[r];
+      if (x == 0xFFFFFFFFu) continue;
+      gm[off0 + AM_REC_OP(x)] |= 1ull << (AM_REC_GRP(x) + ((x & AM_REC_KILL) ? 32u : 0u));
+    }
+  }
+}
+
 __global__ void k_rec_key_off(const uint64_t *key_off, const uint64_t *key_end, uint64_t n_keys, const uint64_t *off,
                               uint64_t *rko, uint64_t *rke) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= n_keys; k += (uint64_t)gridDim.x * blockDim.x) {
@@ -184,6 +202,23 @@ int build_records(am_store *st) {
       rc = AM_ERR_HIP;
     }
   }
+  void *gmk = nullptr;  // the group-mask view, over the store's padded op columns
+  const size_t na = d.snap_stride ? d.snap_stride : d.n_ops;
+  if (!rc && n_rec) {
+    rc = am_dev_alloc(c, na * 8 + 32, &gmk);
+    if (!rc) {
+      st->allocs.push_back(gmk);
+      am_op_log v = d;
+      v.rec_key_off = (const uint64_t *)rko, v.rec_key_end = (const uint64_t *)rke;
+      v.rec_g = (const uint32_t *)rg, v.key_ngrp = (const uint32_t *)ng;
+      if (hipMemsetAsync(gmk, 0, na * 8 + 32, c->stream) != hipSuccess) rc = AM_ERR_HIP;
+      if (!rc) {
+        hipLaunchKernelGGL(k_gmask, dim3(grid_of(d.n_keys)), dim3(256), 0, c->stream, v, (uint64_t *)gmk);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) rc = AM_ERR_HIP;
+      }
+      if (rc) am_set_error("group-mask view: build pass failed");
+    }
+  }
   cleanup();
   if (rc) return rc;
   d.n_rec = n_rec;
@@ -192,6 +227,7 @@ int build_records(am_store *st) {
   d.rec_g = (const uint32_t *)rg;
   d.grp = (const uint64_t *)gp;
   d.key_ngrp = (const uint32_t *)ng;
+  d.gmask = (const uint64_t *)gmk;
   return AM_OK;
 }
 

@@ -137,13 +137,20 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   am_sel cur = S;
   if (type == AM_BCOUNTER) {
     AM_HIP(hipMemsetAsync(rows_buf, 0, 2 * sizeof(uint32_t), ctx->stream));
-    am_rows_cfg C;
-    C.short_max = ROWS_BC;
-    C.list = rows_buf + 64;
-    C.count = rows_buf + 1;
-    rc = am_launch_rows(ctx, L, B, R, S, type, C);
+    if (am_bcrows_applies(L, B, R)) {  // short reads: the touched slots only (am_bcrows.hip)
+      am_retry nx;
+      nx.count = rows_buf + 1;
+      nx.list = rows_buf + 64;
+      rc = am_launch_bcrows(ctx, L, B, R, S, nx);
+    } else {
+      am_rows_cfg C;
+      C.short_max = ROWS_BC;
+      C.list = rows_buf + 64;
+      C.count = rows_buf + 1;
+      rc = am_launch_rows(ctx, L, B, R, S, type, C);
+    }
     if (rc) return rc;
-    cur.idx = C.list;
+    cur.idx = rows_buf + 64;
     cur.range = rows_buf;
     if (grp_buf && am_bcwave_applies(L, R)) {  // wave per read up to its limit (am_bcwave.hip)
       AM_HIP(hipMemsetAsync(grp_buf, 0, 2 * sizeof(uint32_t), ctx->stream));

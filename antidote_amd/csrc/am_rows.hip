@@ -65,15 +65,11 @@ struct ROut {  // per-lane buffered outputs of read (batch base + lane)
   uint64_t v0, v1;
 };
 
-// waves per SIMD the register allocation must allow (experiment switch; 1 = the compiler's
-// choice).  At D = 16 the compiler takes ~350 VGPRs (one wave per SIMD); asked for two it fits
-// 224 without spilling, but C5's bounded-counter rows then ran 2.1x slower (3.3 -> 7.1 ms)
-#ifndef AMK_ROWS_MINW
-#define AMK_ROWS_MINW 1
-#endif
+// (at D = 16 the compiler takes ~350 VGPRs, one wave per SIMD; asked for two it fits 224
+// without spilling, but C5's bounded-counter rows then ran 2.1x slower: DESIGN.md 8)
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED>
-__global__ void __launch_bounds__(BLOCK, AMK_ROWS_MINW) k_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+__global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                 am_rows_cfg C) {
   constexpr bool BC = TYPE == AM_BCOUNTER;
   constexpr bool LDS = BC;

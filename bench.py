@@ -60,10 +60,12 @@ CONFIGS = {
     "c4": dict(type=0, n_dc=3, n_keys=8 << 20, ops=16, set_cap=16,
                desc="mixed 40% PN / 20% LWW / 20% AW-set / 20% MV, 8388608 keys x 16 ops per GPU "
                     "(64M keys at 8 GPUs), D=3"),
-    "c5": dict(type=abi.AM_SYNTH_MV_BC, n_dc=16, n_keys=2 << 20, zipf=1.1, total_ops=128 << 20, hot_cap=1 << 20,
+    # total_ops is the Zipf target BEFORE the hot-key cap: 187267328 is the smallest target (to
+    # 4096) whose capped lengths still sum to >= 2^27 (134218704 ops per GPU, 1.07G at 8 GPUs)
+    "c5": dict(type=abi.AM_SYNTH_MV_BC, n_dc=16, n_keys=2 << 20, zipf=1.1, total_ops=187267328, hot_cap=1 << 20,
                set_cap=8, desc="MV register + bounded counter (50/50), Zipf s=1.1 key popularity, 2097152 keys / "
-                               "99935993 ops per GPU (Zipf lengths for a 2^27-op target, hot keys capped at "
-                               "2^20; 16M keys at 8 GPUs), D=16"),
+                               "134218704 ops per GPU after the 2^20 hot-key cap (16M keys / 1.07G ops at 8 GPUs), "
+                               "D=16"),
 }
 
 
@@ -80,7 +82,8 @@ def bytes_per_op(type_: int, n_dc: int, packed: bool = True) -> int:
     return 1 + 8 + 8 * n_dc + payload
 
 
-REC_BYTES = 4  # one birth/kill record of the token-group view: rec_g u32 (am_group.hip)
+REC_BYTES = 4    # one birth/kill record of the token-group view: rec_g u32 (am_group.hip)
+GMASK_BYTES = 8  # one op's group masks (births | effective kills) of the gmask view (am_pack.hip)
 
 
 def bytes_per_key(type_: int, n_dc: int, set_len: float = 0.0) -> float:
@@ -124,11 +127,28 @@ def key_columns(mat, dlog, n_keys):
     return ko, kt
 
 
-def workload_bytes(cfg, dlog, ko, kt, reads, packed):
-    """Algorithmic bytes of one am_materialize over every key of the store."""
+def set_view_bytes(mat, dlog, ko, kt):
+    """Bytes of the set effects a read streams: a short grouped key (<= 16 ops from its aligned
+    start, <= 32 groups; the lane tier's quad path) ORs one 8-byte group-mask word per op, every
+    other grouped key reads its 4-byte records."""
+    n = len(kt)
+    ng = np.empty(n, np.uint32)
+    rko = np.empty(n + 1, np.uint64)
+    abi.check(mat.L.am_memcpy_d2h(mat.ctx, ng.ctypes.data, dlog.key_ngrp, ng.nbytes), "d2h key_ngrp")
+    abi.check(mat.L.am_memcpy_d2h(mat.ctx, rko.ctypes.data, dlog.rec_key_off, rko.nbytes), "d2h rec_key_off")
+    off0, off1 = ko[:-1].astype(np.int64), ko[1:].astype(np.int64)
+    nrec = np.diff(rko.astype(np.int64))
+    sets = (kt == abi.AM_AWSET) | (kt == abi.AM_MVREG)
+    quad = sets & (ng <= 32) & (off1 <= (off0 & ~3) + 16) & bool(dlog.gmask)
+    return float((off1 - off0)[quad].sum()) * GMASK_BYTES + float(nrec[~quad].sum()) * REC_BYTES
+
+
+def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None):
+    """Algorithmic bytes of one am_materialize over every key of the store (the layout model:
+    what the kernels must stream of this build's HBM layout)."""
     lens = np.diff(ko.astype(np.int64))
     records = packed and bool(dlog.rec_key_off)
-    total = float(dlog.n_rec) * REC_BYTES if records else float(dlog.n_var) * 8
+    total = set_view_bytes(mat, dlog, ko, kt) if records else float(dlog.n_var) * 8
     set_len = reads.set_len.cpu().numpy() if reads.set_len is not None else None
     for t in sorted(set(int(x) for x in np.unique(kt))):
         m = kt == t
@@ -137,6 +157,31 @@ def workload_bytes(cfg, dlog, ko, kt, reads, packed):
             else 0.0
         total += float(m.sum()) * (bytes_per_key(t, cfg["n_dc"], sl) + (8 if packed else 0))
     return total
+
+
+def logical_bytes(cfg, dlog, ko, kt, reads, cached=False):
+    """SURVEY.md 8(d)'s byte model, over the reference's per-op record rather than this build's
+    layout: B_op = 8 D (snapshot_time) + 8 (commit_time) + 1 (commit DC) + 8 (op id) + P_type
+    (PN 8; LWW 16; AW 8 elem + 8 per token + 4 CSR offset; MV 8 value + 8 token + 4 + 8 per
+    overridden token; bcounter 2 + 8) and B_key = 8 (op range) + the output (state + 8 D clock
+    + 8 new_last_op + 4 count + 1 flags) + (cached reads) the base (state + 8 D clock + 8 last_op).
+    Effect words are counted from the log's var_data (AW: 3 + tokens per entry, of which the
+    two counts are not payload)."""
+    D = cfg["n_dc"]
+    lens = np.diff(ko.astype(np.int64))
+    n_ops = {t: float(lens[kt == t].sum()) for t in range(1, 6)}
+    fixed = 8 * D + 8 + 1 + 8
+    total = sum(n_ops.values()) * fixed
+    total += n_ops[abi.AM_PN] * 8 + n_ops[abi.AM_LWW] * 16 + n_ops[abi.AM_BCOUNTER] * 10
+    total += n_ops[abi.AM_AWSET] * 4 + n_ops[abi.AM_MVREG] * 20   # CSR offsets; MV value + token
+    aw_words = float(dlog.n_var) * 8 - n_ops[abi.AM_AWSET] * 16   # AW elem + tokens, MV overridden
+    total += max(aw_words, 0.0)
+    set_len = reads.set_len.cpu().numpy().astype(np.float64) if reads.set_len is not None else np.zeros(len(kt))
+    state = np.where(kt == abi.AM_PN, 8.0, np.where(kt == abi.AM_LWW, 16.0, 16.0 * set_len))
+    per_key = 8 + (8 * D + 8 + 4 + 1) + state
+    if cached:
+        per_key = per_key + 8 * D + 8 + state
+    return total + float(per_key.sum())
 
 
 def cached_bytes(cfg, pre, reads):
@@ -215,16 +260,33 @@ def cpu_baseline(cfg, p, budget_s=10.0, cached=False):
             for t in ts:
                 t.join()
 
+    def timed(budget):
+        t0 = time.perf_counter()
+        passes = 0
+        while True:
+            one_pass()
+            passes += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        return passes, time.perf_counter() - t0
+
     one_pass()  # warm (page faults)
-    t0 = time.perf_counter()
-    passes = 0
+    passes, dt = timed(budget_s)
+    # the same port on ONE thread (single-threaded and all-core), over the first
+    # part of the sample (a few seconds)
+    s1, b1, r1, n1 = parts[0][0], parts[0][1], parts[0][2], parts[0][3]
+    n1 = max(1, min(n1, n1 * 4 // max(1, threads)))
+    ops1 = n1 * (parts[0][4] / max(1, parts[0][3]))
+    t1 = time.perf_counter()
+    p1 = 0
     while True:
-        one_pass()
-        passes += 1
-        if time.perf_counter() - t0 >= budget_s:
+        L.amo_materialize_range(ctypes.byref(s1), ctypes.byref(b1), 0, n1, ctypes.byref(r1))
+        p1 += 1
+        if time.perf_counter() - t1 >= budget_s / 3:
             break
-    dt = time.perf_counter() - t0
+    d1 = time.perf_counter() - t1
     return {"value": passes * n_ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
+            "single_thread": {"value": p1 * ops1 / d1, "cores": 1, "sample": f"{n1} keys (~{int(ops1)} ops)"},
             "sample": f"{len(k0s) * per} keys ({n_ops} ops) of the same workload"
                       f"{' with q=0.5 cached bases' if cached else ''}, {passes} passes in {dt:.1f}s, "
                       f"C restatement of clocksi_materializer (oracle/am_oracle.c), not BEAM"}
@@ -397,32 +459,33 @@ def main():
     gst_vc = read_vc.cpu().numpy().view(np.uint64)
     assert [int(x) for x in gst_vc] == [int(clock[d]) for d in range(n_dc)], "GST mismatch"
 
-    # ---- the read batch, timed alone with HIP events on the library's stream ----
+    # ---- per-step HIP-event times (median and mean), and the read call alone,
+    #      each timed with HIP events on the library's stream ----
     kern_iters = max(5, args.steps)
-    if args.base == "cached":
-        kern_s = 0.0
-        for _ in range(kern_iters):
-            populate()
-            barrier()
-            abi.check(mat.L.am_timer_start(mat.ctx), "timer")
-            cached_read()
-            ms = ctypes.c_float()
-            abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
-            kern_s += ms.value
-        kern_ms = kern_s / kern_iters
-    else:
+
+    def event_ms(fn, pre_fn=None):
+        if pre_fn is not None:
+            pre_fn()
         barrier()
         abi.check(mat.L.am_timer_start(mat.ctx), "timer")
-        for _ in range(kern_iters):
-            materialize(mat, dlog, reads)
-        ms = ctypes.c_float()
-        abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms)), "timer")
-        kern_ms = ms.value / kern_iters
+        fn()
+        ms_ = ctypes.c_float()
+        abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms_)), "timer")
+        return float(ms_.value)
+
+    if args.base == "cached":
+        step_ev = [event_ms(lambda: (gst(), cached_read()), populate) for _ in range(args.steps)]
+        kern_ev = [event_ms(cached_read, populate) for _ in range(kern_iters)]
+    else:
+        step_ev = [event_ms(step) for _ in range(args.steps)]
+        kern_ev = [event_ms(lambda: materialize(mat, dlog, reads)) for _ in range(kern_iters)]
+    kern_ms = float(np.mean(kern_ev))
     packed = bool(dlog.pk_vc)
-    alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed)
+    alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed, mat)
     if args.base == "cached":
         alg_bytes += cached_bytes(cfg, pre, reads)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    logical = logical_bytes(cfg, dlog, ko, kt, reads, cached=args.base == "cached")
 
     total_ops = world * n_ops * args.steps
     value = total_ops / dt
@@ -436,6 +499,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
+        "step_ms_hip_events": {"median": float(np.median(step_ev)), "mean": float(np.mean(step_ev)),
+                               "min": float(np.min(step_ev)), "n": len(step_ev)},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -450,11 +515,19 @@ def main():
                            "timing of each step",
                    "base": args.base},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config if args.base == "fresh" else args.config + "_cached", workload),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
+                              "packed commit vectors 4*D per op, payload, 4 B per token-group record or 8 B per "
+                              "group-mask op, per-read metadata and outputs", "traffic": load_traffic(args.config if args.base == "fresh" else args.config + "_cached", workload),
                      "kernel": ("am_snapcache_read (select + materialize tiers + store)" if args.base == "cached"
                                 else "k_stream" if single else
                                 "am_materialize (all tiers: k_stream, k_rows, k_grp_*, k_sets, k_big_*)"),
                      "kernel_ms": kern_ms,
+                     "kernel_ms_median": float(np.median(kern_ev)),
+                     "logical": {"model": "SURVEY.md 8(d) B_op / B_key (the reference's per-op record: "
+                                          "8*D + 17 + P_type per op)", "bytes_per_launch": logical,
+                                 "bytes_per_s": logical / (kern_ms * 1e-3),
+                                 "frac_of_peak": logical / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
                      "alg_bytes_per_launch": alg_bytes,
                      "layout": "packed (u32 commit vectors relative to a per-key time base); set effects as u32 token-group records"
                      if packed else "full"},

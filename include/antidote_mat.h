@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 5
+#define AM_ABI_VERSION 6
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -200,7 +200,13 @@ typedef struct am_op_log {
    * key_end when present, else key_off[k+1]. */
   const uint64_t *key_end;     /* [n_keys] or NULL                                   */
   const uint64_t *rec_key_end; /* [n_keys] or NULL                                   */
+  /* Group-mask view (built with the token-group view): for the ops of a grouped key with at
+   * most 32 groups, gmask[p] = the groups op p births (bits 0-31) | the groups it EFFECTIVELY
+   * kills (bits 32-63) -- the key's records folded per op, so a short read ORs one word per
+   * included op instead of testing records; 0 for every other op.  NULL in host logs. */
+  const uint64_t *gmask;       /* [n_ops] or NULL                                    */
 } am_op_log;
+#define AM_GMASK_MAX_GRP 32u
 #define AM_REC_KILL (1u << 16)
 #define AM_REC_OP(m) ((m) & 0xFFFFu)
 #define AM_REC_GRP(m) ((m) >> 17)

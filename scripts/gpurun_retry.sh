@@ -8,7 +8,7 @@ for i in 1 2 3 4 5 6; do
   rc=$?
   if grep -q "status=transient" "$LOG" || [ $rc -eq 3 ]; then
     echo "[retry $i: infrastructure, nothing ran]" >> "$LOG.retries"
-    sleep 60
+    sleep 120
     continue
   fi
   exit $rc

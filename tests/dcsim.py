@@ -146,12 +146,33 @@ class OracleBackend:
     def __init__(self, n_dc, keys):
         self.n_dc, self.keys = n_dc, keys
         self.st = [R.VnodeState() for _ in range(n_dc)]
+        self.log: List[List[Tuple]] = [[] for _ in range(n_dc)]   # the DC's logging_vnode, in commit order
+        self.stable = [dict() for _ in range(n_dc)]               # meta_data_sender's last stable result
 
     def deliver(self, dc, ops):
         for key, type_, eff, snap, origin, ct, txid in ops:
+            self.log[dc].append((key, type_, eff, snap, origin, ct, txid))
             p = R.Payload(key=key, type=type_, op_param=_oracle_effect(type_, eff), snapshot_time=dict(snap),
                           commit_time=(origin, ct), txid=txid)
             R.op_insert_gc(key, p, self.st[dc])
+
+    def restart(self, dc):
+        """Kill and restart the DC's node: the ops cache is gone and load_from_log_to_tables/2 ->
+        load_ops/2 replays the log through op_insert_gc/3 (src/materializer_vnode.erl:288-319)."""
+        log, self.log[dc] = self.log[dc], []
+        self.st[dc] = R.VnodeState()
+        self.deliver(dc, log)
+
+    def read_many(self, dc, keys, clock):
+        return [self.read(dc, k, clock) for k in keys]
+
+    def gst(self, dc, parts, gr):
+        """stable_time_functions:get_min_time/1 over the partitions' stable clocks, the monotone
+        meta_data_sender:update_stable/3, and dc_utilities:get_stable_snapshot/0 (gr: the min
+        broadcast to every DC)."""
+        merged = R.get_min_time({i: dict(c) for i, c in enumerate(parts)})
+        _, self.stable[dc] = R.update_stable(self.stable[dc], merged)
+        return R.gst_gr(dict(self.stable[dc])) if gr else dict(self.stable[dc])
 
     def read(self, dc, key, clock):
         r = R.internal_read(key, self.keys[key], dict(clock), R.IGNORE, False, self.st[dc])
@@ -190,6 +211,8 @@ class GpuBackend:
         self.vn = [mat.vnode(n_dc, len(keys)) for _ in range(n_dc)]
         self.codec = [Codec() for _ in range(n_dc)]
         self.txids = [TxIds() for _ in range(n_dc)]
+        self.log: List[List[List[Any]]] = [[[] for _ in keys] for _ in range(n_dc)]  # per DC, per key, log order
+        self.last = [None] * n_dc   # the device GST state per DC: (last_vc, last_pres)
 
     def _labels(self, dc, type_, eff):
         if type_ == BCOUNTER:
@@ -204,10 +227,67 @@ class GpuBackend:
         from antidote_amd.oplog import Op
         per_key: List[List[Any]] = [[] for _ in self.keys]
         for key, type_, eff, snap, origin, ct, txid in ops:
+            # an op's TxId is stamped with its commit time: the map drops it once stable (am_txid)
             per_key[self.kidx[key]].append(Op(type=type_, commit_dc=origin, commit_time=ct, snap=dict(snap),
                                               effect=self._labels(dc, type_, eff),
-                                              txid=self.txids[dc].intern(txid) if txid is not None else None))
+                                              txid=self.txids[dc].intern_op(txid, origin, ct) if txid is not None
+                                              else None))
+        for k, ops_k in enumerate(per_key):
+            self.log[dc][k] += ops_k
         self.vn[dc].insert(per_key, self.ktypes)
+
+    def restart(self, dc):
+        """The vnode is destroyed and rebuilt from the log: Materializer.load_ops (am_vnode_insert_host
+        of every logged op, load_ops/2)."""
+        self.vn[dc].close()
+        self.vn[dc] = self.mat.load_ops(self.n_dc, self.log[dc], self.ktypes)
+
+    def read_many(self, dc, keys, clock):
+        """One read batch over several keys at one snapshot (one am_vnode_read_host call, as
+        read_objects batches a transaction's reads)."""
+        from antidote_amd.oplog import Read
+        hb = self.vn[dc].read([Read(self.kidx[k], self.keys[k], dict(clock)) for k in keys],
+                              set_capacity=[4096] * len(keys))
+        out = []
+        for i, k in enumerate(keys):
+            r = hb.result(i)
+            assert r[0] == "ok", r
+            out.append(self._terms(dc, self.keys[k], r[1]))
+        return out
+
+    def gst(self, dc, parts, gr):
+        """The device GST path: am_gst_local_min over the partitions' stable clocks (one node: its
+        lanes are the all-reduce's result) and am_gst_finalize (monotone update; gr broadcast)."""
+        import numpy as np
+        import torch
+
+        from antidote_amd import abi
+        nd, npart = self.n_dc, len(parts)
+        vc = np.zeros((npart, nd), np.uint64)
+        pres = np.zeros(npart, np.uint32)
+        for i, c in enumerate(parts):
+            for d, t in c.items():
+                vc[i, d] = t
+                pres[i] |= 1 << d
+        if self.last[dc] is None:
+            self.last[dc] = (torch.zeros(nd, dtype=torch.int64, device="cuda"),
+                             torch.zeros(1, dtype=torch.int32, device="cuda"))
+        d_vc = torch.from_numpy(vc.view(np.int64)).cuda()
+        d_pres = torch.from_numpy(pres.view(np.int32)).cuda()
+        lanes = torch.zeros(nd + 1, dtype=torch.int64, device="cuda")
+        o_vc = torch.zeros(nd, dtype=torch.int64, device="cuda")
+        o_p = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ch = torch.zeros(1, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        L, ctx = self.mat.L, self.mat.ctx
+        abi.check(L.am_gst_local_min(ctx, nd, npart, d_vc.data_ptr(), d_pres.data_ptr(), None, lanes.data_ptr()),
+                  "am_gst_local_min")
+        abi.check(L.am_gst_finalize(ctx, nd, lanes.data_ptr(), self.last[dc][0].data_ptr(),
+                                    self.last[dc][1].data_ptr(), 1 if gr else 0, o_vc.data_ptr(), o_p.data_ptr(),
+                                    ch.data_ptr()), "am_gst_finalize")
+        self.mat.sync()
+        out, p = o_vc.cpu().numpy().view(np.uint64), int(o_p.item()) & 0xFFFFFFFF
+        return {d: int(out[d]) for d in range(nd) if (p >> d) & 1}
 
     def _read_labels(self, dc, key, clock):
         from antidote_amd.oplog import Read
@@ -296,6 +376,7 @@ class Cluster:
         self.down = set()
         self.txn_seq = 0
         self.bc_queue: Dict[Tuple[int, str], List[int]] = {}
+        self.partial: List[List[Tuple]] = [[] for _ in range(n_dc)]   # delivered, their txn not complete
 
     def token(self):
         return bytes(self.rng.getrandbits(8) for _ in range(20))
@@ -318,8 +399,18 @@ class Cluster:
         self.pending[dest] = keep
         if go:
             self.b.deliver(dest, go)
-            for item in go:
-                self.seen[dest][item[4]] = max(self.seen[dest][item[4]], item[5])
+        for item in go + self.partial[dest]:   # a partly delivered transaction is complete now
+            self.seen[dest][item[4]] = max(self.seen[dest][item[4]], item[5])
+        self.partial[dest] = []
+
+    def deliver_some(self, dest, count):
+        """Deliver the next `count` held ops to dest WITHOUT making their transaction visible
+        (the DC's clock does not advance until the rest arrives): the ops sit in the ops cache,
+        and a read at the DC's snapshot must exclude all of them (is_op_in_snapshot/7)."""
+        go, self.pending[dest] = self.pending[dest][:count], self.pending[dest][count:]
+        if go:
+            self.b.deliver(dest, go)
+            self.partial[dest] += go
 
     def wait_for(self, dc, clock):
         if clock:
@@ -351,6 +442,11 @@ class Cluster:
     def read(self, dc, key, clock):
         self.wait_for(dc, clock)
         return self.b.read(dc, key, self.view(dc, clock))
+
+    def gst_clock(self, dc, gr):
+        """The DC's stable snapshot from its partitions' stable clocks (here the DC's one partition
+        holds what it has applied)."""
+        return self.b.gst(dc, [self.view(dc)], gr)
 
     # bcounter_mgr (src/bcounter_mgr.erl:111-205)
     def bc_refused(self, dc, key, amount):
@@ -477,9 +573,28 @@ def run_case(case, backend_factory) -> List[Tuple[str, Any, Any]]:
                     clocks[a["save"]] = ct
             elif "read" in s:
                 a = s["read"]
-                st = cl.read(a["dc"], a["key"], clk(a.get("clock")))
+                if a.get("at") in ("gst", "gst_gr"):   # a read at the stable snapshot itself
+                    snap = cl.gst_clock(a["dc"], a["at"] == "gst_gr")
+                    st = b.read(a["dc"], a["key"], snap)
+                else:
+                    snap = cl.view(a["dc"], clk(a.get("clock")))
+                    st = cl.read(a["dc"], a["key"], clk(a.get("clock")))
                 if "expect" in a:
                     checks.append((where, crdt_value(keys[a["key"]], st), jterm(a["expect"])))
+                if "save" in a:
+                    clocks[a["save"]] = dict(snap)
+            elif "read_objects" in s:   # one batch, one snapshot
+                a = s["read_objects"]
+                cl.wait_for(a["dc"], clk(a.get("clock")))
+                vals = [crdt_value(keys[k], x) for k, x in
+                        zip(a["keys"], b.read_many(a["dc"], a["keys"], cl.view(a["dc"], clk(a.get("clock")))))]
+                if "expect" in a:
+                    checks.append((where, vals, jterm(a["expect"])))
+            elif "deliver" in s:
+                a = s["deliver"]
+                cl.deliver_some(a["dc"], a["count"])
+            elif "restart" in s:
+                b.restart(s["restart"]["dc"])
             elif "hold" in s:
                 cl.hold = s["hold"]
                 if not cl.hold:

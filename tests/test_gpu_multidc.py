@@ -13,6 +13,7 @@ from tests.kat_util import load
 pytestmark = pytest.mark.gpu
 
 SUITES = load("multidc_suites.json")
+SUITES["cases"] = SUITES["cases"] + load("txn_suites.json")["cases"]
 
 
 @pytest.fixture(scope="module")

@@ -7,6 +7,7 @@ from tests import dcsim
 from tests.kat_util import load
 
 SUITES = load("multidc_suites.json")
+SUITES["cases"] = SUITES["cases"] + load("txn_suites.json")["cases"]
 
 
 @pytest.mark.parametrize("case", SUITES["cases"], ids=lambda c: c["name"])
