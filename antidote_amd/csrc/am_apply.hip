@@ -120,7 +120,7 @@ __global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter,
         uint32_t *rg = const_cast<uint32_t *>(L.rec_g);
         for (uint64_t r = lane; r < nr; r += WAVE_SZ) rg[r0 + r] = S.rec_g[sr0 + r];
         uint64_t *gp = const_cast<uint64_t *>(L.grp);
-        const uint32_t ngc = ng == AM_NGRP_NONE ? 0u : ng;
+        const uint32_t ngc = am_ngrp_count(ng);
         for (uint32_t g = lane; g < ngc; g += WAVE_SZ) {
           gp[2 * (r0 + g)] = S.grp[2 * (sr0 + g)];
           gp[2 * (r0 + g) + 1] = S.grp[2 * (sr0 + g) + 1];

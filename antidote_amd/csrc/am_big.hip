@@ -46,6 +46,9 @@ struct BigRead {
   uint64_t cap;     // record capacity (power of two: the global sort pads to it)
   uint64_t h0;      // first hash slot
   uint64_t hmask;   // hash slots - 1
+  uint64_t bm0;     // grouped mode: first word of the born | killed group bitmaps
+  uint32_t G;       // grouped mode: the key's groups (chunked token-group view)
+  uint32_t grouped;
 };
 
 struct BigAcc {
@@ -67,6 +70,7 @@ struct BigRec {
   uint32_t *bs;       // birth: index in the effect's token list (base: in the base list)
   uint64_t *ot;       // finish: AW survivor tokens (global-scratch sort)
   int32_t *oi;        // finish: AW survivor index (global-scratch sort payload)
+  uint32_t *bm;       // grouped mode: per read born [gw] | killed [gw] bitmaps
   uint8_t *dead;
   uint64_t *ka, *kb;  // exported kills: kill key
   int32_t *kp;
@@ -112,7 +116,12 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
     const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
     const uint64_t nch = off1 > t0 ? (off1 - t0 + CHUNK - 1) / CHUNK : 1;
     // births: AW <= add tokens <= W, MV <= ops; kills <= W; + base pairs
-    const uint64_t cap = TYPE == AM_BCOUNTER ? 1 : next_pow2((W > off1 - off0 ? W : off1 - off0) + nbase + 1);
+    // grouped mode: an MV key with the chunked token-group view and no base pairs
+    const uint32_t ng = (TYPE == AM_MVREG && L.key_ngrp && L.rec_g) ? L.key_ngrp[key] : AM_NGRP_NONE;
+    const bool grouped = am_ngrp_big(ng) && nbase == 0;
+    const uint32_t G = grouped ? am_ngrp_count(ng) : 0u;
+    const uint64_t cap =
+        (TYPE == AM_BCOUNTER || grouped) ? 1 : next_pow2((W > off1 - off0 ? W : off1 - off0) + nbase + 1);
     if (TYPE == AM_BCOUNTER) {  // slots start from the base snapshot's orddicts
       const uint32_t nd = L.n_dc, np = nd * nd;
       for (uint32_t i = 0; i < SL.ns; ++i) {
@@ -126,9 +135,11 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
     }
     BigRead x;
     x.r = r, x.off0 = off0, x.off1 = off1, x.chunk0 = 0, x.rec0 = 0, x.cap = cap, x.h0 = 0, x.hmask = 2 * cap - 1;
+    x.bm0 = 0, x.G = G, x.grouped = grouped ? 1u : 0u;
     br[b] = x;
     sz[b] = nch;
     sz[(uint64_t)nbig + b] = cap;
+    sz[2 * (uint64_t)nbig + b] = grouped ? 2 * (uint64_t)((G + 31) / 32) : 0;
     BigAcc a;
     a.count = a.flags = a.pres = a.nbirth = a.nkill = a.pad0 = 0;
     a.min_excl = NONE;
@@ -137,14 +148,14 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
   }
 }
 
-// one workgroup of 1024: exclusive scans of chunks and caps; totals[0..1]
+// one workgroup of 1024: exclusive scans of chunks, caps and bitmap words; totals[0..2]
 __global__ void __launch_bounds__(1024) k_big_offsets(const uint32_t *nbig_p, BigRead *br, const uint64_t *sz,
                                                       uint64_t *totals) {
   __shared__ uint64_t part[1024];
   const uint32_t nbig = *nbig_p, tid = threadIdx.x;
   const uint32_t per = (nbig + 1023) / 1024;
   const uint32_t b0 = tid * per < nbig ? tid * per : nbig, b1 = b0 + per < nbig ? b0 + per : nbig;
-  for (int f = 0; f < 2; ++f) {
+  for (int f = 0; f < 3; ++f) {
     const uint64_t *v = sz + (uint64_t)f * nbig;
     uint64_t s = 0;
     for (uint32_t b = b0; b < b1; ++b) s += v[b];
@@ -159,7 +170,8 @@ __global__ void __launch_bounds__(1024) k_big_offsets(const uint32_t *nbig_p, Bi
     uint64_t run = part[tid] - s;
     for (uint32_t b = b0; b < b1; ++b) {
       if (f == 0) br[b].chunk0 = run;
-      else br[b].rec0 = run, br[b].h0 = 2 * run;
+      else if (f == 1) br[b].rec0 = run, br[b].h0 = 2 * run;
+      else br[b].bm0 = run;
       run += v[b];
     }
     if (tid == 1023) totals[f] = part[1023];
@@ -237,6 +249,64 @@ struct ChunkSink {
   }
 };
 
+// ---- grouped mode (chunked token-group view, am_grpbig.hip): a group survives iff its birth
+//      is included and no kill of it is (effective kills follow the birth), so births and kills
+//      are sets.  A chunk collects its included births and kills in two LDS hash sets and
+//      exports only what it cannot settle itself: a group born and killed within the chunk is
+//      dead (one birth per group), so neither bit leaves; the rest are ORed into the read's
+//      born / killed bitmaps.  An MV override chain leaves about one bit of each per chunk. ----
+constexpr uint32_t GH = LK;          // slots per hash set (two sets in ChunkSmem::lk_a)
+constexpr uint32_t GH_EMPTY = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t gslot(uint32_t g) { return (g * 0x9E3779B1u) >> 21; }  // 11 bits
+static_assert(GH == 2048, "gslot yields 11 bits");
+__device__ __forceinline__ bool gset_insert(uint32_t *h, uint32_t g) {
+  const uint32_t s0 = gslot(g);
+  for (uint32_t pr = 0; pr < 32; ++pr) {
+    const uint32_t sl = (s0 + pr) & (GH - 1);
+    const uint32_t old = atomicCAS(&h[sl], GH_EMPTY, g);
+    if (old == GH_EMPTY || old == g) return true;
+  }
+  return false;
+}
+__device__ __forceinline__ bool gset_has(const uint32_t *h, uint32_t g) {
+  const uint32_t s0 = gslot(g);
+  for (uint32_t pr = 0; pr < 32; ++pr) {
+    const uint32_t x = h[(s0 + pr) & (GH - 1)];
+    if (x == g) return true;
+    if (x == GH_EMPTY) return false;
+  }
+  return false;
+}
+// the records of chunk ops [lo, hi) (incl: their inclusion bits from lo); hs = 2 * GH u32 of
+// LDS at GH_EMPTY; bm = the read's born [gw] | killed [gw] words
+__device__ void grouped_records(const am_op_log &L, uint64_t key, const BigRead &R0, uint64_t lo, uint64_t hi,
+                                const uint32_t *incl, uint32_t *hs, uint32_t *bm, uint32_t tid) {
+  uint32_t *hb = hs, *hk = hs + GH;
+  const uint32_t gw = (R0.G + 31) / 32;
+  const uint64_t rk0 = L.rec_key_off[key];
+  const uint64_t ka = (lo > R0.off0 ? lo : R0.off0) - R0.off0, kb = hi - R0.off0;  // key op range
+  for (uint64_t hc = ka / AM_BIG_CHUNK; hc <= (kb - 1) / AM_BIG_CHUNK; ++hc) {
+    const uint64_t a0 = rk0 + L.rec_g[rk0 + hc], a1 = rk0 + L.rec_g[rk0 + hc + 1];
+    for (uint64_t q = a0 + tid; q < a1; q += BLOCK) {
+      const uint32_t x = L.rec_g[q];
+      if (x == 0xFFFFFFFFu) continue;  // an ineffective kill
+      const uint64_t op = hc * AM_BIG_CHUNK + AM_BREC_OP(x);
+      if (op < ka || op >= kb) continue;
+      const uint32_t bit = (uint32_t)(op + R0.off0 - lo);
+      if (!((incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
+      const uint32_t g = AM_BREC_GRP(x);
+      const bool kill = (x & AM_BREC_KILL) != 0;
+      if (!gset_insert(kill ? hk : hb, g)) atomicOr(bm + (kill ? gw : 0u) + (g >> 5), 1u << (g & 31));
+    }
+  }
+  __syncthreads();
+  for (uint32_t sl = tid; sl < GH; sl += BLOCK) {
+    const uint32_t b = hb[sl], k = hk[sl];
+    if (b != GH_EMPTY && !gset_has(hk, b)) atomicOr(bm + (b >> 5), 1u << (b & 31));
+    if (k != GH_EMPTY && !gset_has(hb, k)) atomicOr(bm + gw + (k >> 5), 1u << (k & 31));
+  }
+}
+
 template <int DMAX, int TYPE, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
                                                      const BigRead *br, BigAcc *accs, BigRec G, BigSlots SL,
@@ -274,6 +344,9 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
 
     if (tid < 8) s.ctr[tid] = 0;
     constexpr bool MVH = TYPE == AM_MVREG;
+    const bool grouped = TYPE == AM_MVREG && R0.grouped;  // the chunk's inclusion bits, then records
+    uint32_t *sincl = reinterpret_cast<uint32_t *>(s.lb_p);
+    if (grouped && tid < CHUNK / 32) sincl[tid] = 0;
     if (MVH)
       for (uint32_t i = tid; i < LK; i += BLOCK) s.lk_a[i] = HKEY_EMPTY, s.lk_p[i] = (int32_t)0x80000000;
     ChunkSink sink{&s, G, acc, R0.rec0, MVH};
@@ -328,6 +401,10 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
           if (eval_op<DMAX, true>(u, (meta4 >> (8 * k)) & 0xFFu, ct[k], sv[k], sp[k], txm, p, a)) ib |= 1u << k;
         }
       }
+      if (grouped) {
+        if (ib) atomicOr(&sincl[(uint32_t)(g - lo) >> 5], ib << ((uint32_t)(g - lo) & 31u));
+        ib = 0;
+      }
 #pragma unroll
       for (int k = 0; k < OPL; ++k) {
         if (!((ib >> k) & 1u)) continue;
@@ -368,6 +445,11 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
         if (d < (int)nd && mx[d]) atomicMax(&acc->mx[d], (unsigned long long)mx[d]);
     }
 
+    if (TYPE == AM_MVREG && grouped) {  // grouped mode: the chunk's records -> group bitmaps
+      grouped_records(L, B.key[r], R0, lo, hi, sincl, reinterpret_cast<uint32_t *>(s.lk_a), G.bm + R0.bm0, tid);
+      __syncthreads();
+      continue;
+    }
     if (TYPE == AM_BCOUNTER) {  // flush the chunk's slot sums into the read's global slots
       for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
         const uint64_t q = (uint64_t)b * SL.ns + i;
@@ -515,6 +597,37 @@ __global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch
         else if (tid == 0) R.value.set_len[r] = ne;
         __syncthreads();
       }
+    } else if (TYPE == AM_MVREG && status == AM_OK && R0.grouped) {
+      // grouped mode: survivors = born & ~killed, already in output order (group order)
+      const uint32_t gw = (R0.G + 31) / 32, lane = tid & 63u, wv = tid >> 6;
+      const uint32_t *born = G.bm + R0.bm0, *killed = born + gw;
+      const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
+      const uint64_t rk0 = L.rec_key_off[B.key[r]];
+      uint32_t base = 0;
+      for (uint32_t w0 = 0; w0 < gw; w0 += BLOCK) {
+        const uint32_t w = w0 + tid;
+        const uint32_t a = w < gw ? (born[w] & ~killed[w]) : 0u;
+        const uint32_t c = (uint32_t)__popc(a);
+        const uint32_t inc = wave_incl_scan_u32(c, lane);
+        if (lane == 63) s.ctr[wv] = inc;
+        __syncthreads();
+        uint32_t woff = 0, tot = 0;
+        for (uint32_t v = 0; v < BLOCK / WAVE; ++v) {
+          if (v < wv) woff += s.ctr[v];
+          tot += s.ctr[v];
+        }
+        uint64_t o = base + woff + inc - c;
+        for (uint32_t bits = a; bits; bits &= bits - 1, ++o) {
+          if (o >= ocap) break;
+          const uint64_t g = (uint64_t)w * 32 + (uint32_t)__builtin_ctz(bits);
+          const u64x2 pr = *(const u64x2 *)(L.grp + 2 * (rk0 + g));
+          R.value.set_a[ooff + o] = pr.x, R.value.set_b[ooff + o] = pr.y;
+        }
+        base += tot;
+        __syncthreads();
+      }
+      if (base > ocap) status = AM_ERR_CAPACITY;
+      else if (tid == 0) R.value.set_len[r] = base;
     } else if (status == AM_OK) {
       // count survivors, then gather them (LDS, or the read's kill records as scratch)
       uint32_t alive = 0;
@@ -640,7 +753,7 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   SL.ns = TYPE == AM_BCOUNTER ? L->n_dc * L->n_dc + L->n_dc : 0;
   const size_t o_acc = am_round_up((size_t)nbig * sizeof(BigRead), 256);
   const size_t o_sz = o_acc + am_round_up((size_t)nbig * sizeof(BigAcc), 256);
-  const size_t o_tot = o_sz + am_round_up((size_t)nbig * 16, 256);
+  const size_t o_tot = o_sz + am_round_up((size_t)nbig * 24, 256);
   const size_t o_slo = o_tot + 256, nsl = (size_t)nbig * SL.ns;
   const size_t o_shi = o_slo + am_round_up(nsl * 8, 256), o_spr = o_shi + am_round_up(nsl * 8, 256);
   void *meta = nullptr;
@@ -659,15 +772,16 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   AM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_big_offsets, dim3(1), dim3(1024), 0, ctx->stream, retry.count, br, sz, tot);
   AM_HIP(hipGetLastError());
-  rc = am_ctx_fetch(ctx, tot, 2, h);
+  uint64_t t3[3];
+  rc = am_ctx_fetch(ctx, tot, 3, t3);
   if (rc) return rc;
-  const uint64_t n_chunks = h[0], n_rec = h[1];
+  const uint64_t n_chunks = t3[0], n_rec = t3[1], n_bm = t3[2];
   // records: births (a, b, p, sub, dead), kills (a, b, p) -- n_rec each; hash 2*n_rec
   // slots; the finish pass's AW token / index scratch -- n_rec each
   const size_t rb = am_round_up(n_rec * 8, 256), r4 = am_round_up(n_rec * 4, 256), r1 = am_round_up(n_rec, 256);
-  const size_t hb = am_round_up(2 * n_rec * 4, 256);
+  const size_t hb = am_round_up(2 * n_rec * 4, 256), bmb = am_round_up(n_bm * 4 + 4, 256);
   void *recs = nullptr;
-  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 5 * rb + 4 * r4 + r1 + hb, &recs);
+  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 5 * rb + 4 * r4 + r1 + hb + bmb, &recs);
   if (rc) return rc;
   char *q = (char *)recs;
   BigRec G;
@@ -681,7 +795,9 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   G.ot = (uint64_t *)q, q += rb;
   G.oi = (int32_t *)q, q += r4;
   G.dead = (uint8_t *)q, q += r1;
-  G.H = (uint32_t *)q;
+  G.H = (uint32_t *)q, q += hb;
+  G.bm = (uint32_t *)q;
+  if (n_bm) AM_HIP(hipMemsetAsync(G.bm, 0, n_bm * 4, ctx->stream));
   AM_HIP(hipMemsetAsync(G.dead, 0, n_rec, ctx->stream));
   AM_HIP(hipMemsetAsync(G.H, 0xFF, 2 * n_rec * 4, ctx->stream));
   const uint32_t nd = L->n_dc;

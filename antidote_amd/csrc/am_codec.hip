@@ -509,8 +509,8 @@ __global__ void k_store_relabel(am_op_log L, uint64_t *p0, uint64_t *p1, uint64_
       }
     }
     if (grp && L.key_ngrp && L.rec_key_off && t != AM_LWW) {
-      const uint32_t ng = L.key_ngrp[k];
-      if (ng == AM_NGRP_NONE) continue;
+      const uint32_t ng = am_ngrp_count(L.key_ngrp[k]);
+      if (ng == 0) continue;
       const uint64_t r0 = L.rec_key_off[k];
       for (uint32_t j = lane; j < ng; j += 64) {
         relabel_word(grp + 2 * (r0 + j), old, nw, n);

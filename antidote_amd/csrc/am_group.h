@@ -568,6 +568,26 @@ __device__ __forceinline__ uint32_t base_group(const am_op_log &L, uint64_t rk0,
   return ~0u;
 }
 
+// group-index hints of a snapshot-cache read (am_ctx::grp_hint_in / grp_hint_out)
+struct GrpHint {
+  const uint32_t *in;  // [base word] the pair's group when it was cached, or null
+  uint32_t *out;       // [result word] the output pair's group, or null
+};
+
+// base pair (a, b)'s group through its hint: one load of the hinted group's pair; a hint
+// whose pair does not match (the log changed since the snapshot was cached, or a tier that
+// writes no hints produced the snapshot) falls back to the search.  Groups have distinct kill
+// keys (AW (elem, token), MV token), so a matching pair is the group base_group finds.
+template <int TYPE>
+__device__ __forceinline__ uint32_t hinted_group(const am_op_log &L, uint64_t rk0, uint32_t G, uint64_t a, uint64_t b,
+                                                 uint32_t hint) {
+  if (hint < G) {
+    const u64x2 q = *(const u64x2 *)(L.grp + 2 * (rk0 + hint));
+    if (q.y == b && (q.x == a || (TYPE == AM_MVREG && q.x == ~0ull))) return hint;
+  }
+  return base_group<TYPE>(L, rk0, G, a, b);
+}
+
 // Step 4b of k_grp_wave: the read's value from a cached base.  materialize/4 folds the
 // included candidates (ops not in the base, src/clocksi_materializer.erl:216-268) over the
 // base state in log order; in closed form (causal logs: a remove follows the add it observed)
@@ -579,9 +599,9 @@ __device__ __forceinline__ uint32_t base_group(const am_op_log &L, uint64_t rk0,
 // output position is its rank in its own list plus a binary-search count in the other.
 // Returns false (nothing written) when the new survivors exceed KB.
 template <int TYPE>
-__device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_result &R, WaveSmem &s, uint64_t rk0,
-                           uint32_t G, uint32_t nb, uint64_t boff, uint64_t ooff, uint32_t ocap, uint32_t lane,
-                           uint32_t &nout, int32_t &status) {
+__device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_result &R, GrpHint H, WaveSmem &s,
+                           uint64_t rk0, uint32_t G, uint32_t nb, uint64_t boff, uint64_t ooff, uint32_t ocap,
+                           uint32_t lane, uint32_t &nout, int32_t &status) {
   const uint32_t nwd = (G + 31) / 32;
   const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
   const uint32_t c = (uint32_t)__popc(aw);
@@ -610,6 +630,7 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
   }
   // base pairs (lanes j, j + 64): alive unless an included candidate killed their group
   u64x2 bp[2] = {{0, 0}, {0, 0}};
+  uint32_t bg[2] = {~0u, ~0u};
   uint64_t am[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -618,8 +639,10 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
     if (jb < nb) {
       bp[h].x = B.base.set_a[boff + jb], bp[h].y = B.base.set_b[boff + jb];
       bka[jb] = bp[h].x, bkb[jb] = bp[h].y;
-      const uint32_t g = base_group<TYPE>(L, rk0, G, bp[h].x, bp[h].y);
+      const uint32_t g = H.in ? hinted_group<TYPE>(L, rk0, G, bp[h].x, bp[h].y, H.in[boff + jb])
+                              : base_group<TYPE>(L, rk0, G, bp[h].x, bp[h].y);
       alive = g == ~0u || !((s.killed[g >> 5] >> (g & 31)) & 1u);
+      bg[h] = g;
     }
     am[h] = __ballot(alive);
   }
@@ -649,6 +672,7 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
       }
       const uint64_t o = ooff + i + alive_below(lo);
       R.value.set_a[o] = np[h].x, R.value.set_b[o] = np[h].y;
+      if (H.out) H.out[o] = list[i];
     }
     const uint32_t jb = lane + 64u * h;
     if (jb < nb && ((am[h] >> lane) & 1ull)) {  // + new survivors with a key not above it
@@ -660,6 +684,7 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
       }
       const uint64_t o = ooff + alive_below(jb) + lo;
       R.value.set_a[o] = bp[h].x, R.value.set_b[o] = bp[h].y;
+      if (H.out) H.out[o] = bg[h];
     }
   }
   wave_sync();
@@ -668,7 +693,8 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
 
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
 __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
-                                                                  am_sel S, am_retry next, uint32_t short_opl) {
+                                                                  am_sel S, am_retry next, uint32_t short_opl,
+                                                                  GrpHint H) {
   constexpr int OPL = vopl<DMAX, PACKED>();
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
   constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
@@ -828,7 +854,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         // 4b. a cached base (vector_orddict snapshot): merge its pairs not killed by an
         //     included candidate with the new survivors (base_merge); a read that outgrows the
         //     LDS lists goes to the next tier untouched
-        if (!base_merge<TYPE>(L, B, R, s, rk0, G, nb, uniform_u64(s.slot[j].boff), uniform_u64(s.slot[j].ooff),
+        if (!base_merge<TYPE>(L, B, R, H, s, rk0, G, nb, uniform_u64(s.slot[j].boff), uniform_u64(s.slot[j].ooff),
                               uniform_u32(s.slot[j].ocap), lane, ns, status)) {
           if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
           wave_sync();
@@ -853,6 +879,8 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           if (j2 < nput) p2 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j2]));
           if (j1 < nput) R.value.set_a[ooff + j1] = p1.x, R.value.set_b[ooff + j1] = p1.y;
           if (j2 < nput) R.value.set_a[ooff + j2] = p2.x, R.value.set_b[ooff + j2] = p2.y;
+          if (H.out && j1 < nput) H.out[ooff + j1] = s.list[j1];
+          if (H.out && j2 < nput) H.out[ooff + j2] = s.list[j2];
         }
         if (ns > ocap) status = AM_ERR_CAPACITY;
       }
@@ -1059,7 +1087,7 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     if (blocks > cap) blocks = cap;
     if (blocks == 0) return AM_OK;
     hipLaunchKernelGGL((k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), smem,
-                       ctx->stream, *L, *B, *R, S, next, short_opl);
+                       ctx->stream, *L, *B, *R, S, next, short_opl, GrpHint{ctx->grp_hint_in, ctx->grp_hint_out});
   } else if (tier == AM_GRP_ROW) {
     static int occ = 0;
     if (!occ) {

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t
     const uint64_t r0 = uniform_u64(rcnt[off0]), r1 = uniform_u64(rcnt[off1]);
     const uint64_t n = r1 - r0;
     const bool set = type == AM_AWSET || type == AM_MVREG;
-    if (!set || n > RCAP || off1 - off0 >= 65536 || (kfl & AM_KEY_MIXED_TYPES)) {
+    if (!set || n > RCAP || off1 - off0 >= 65536 || (kfl & AM_KEY_MIXED_TYPES) || am_big_grp_key(L, k)) {
       if (threadIdx.x == 0) ngrp[k] = AM_NGRP_NONE;
       continue;
     }

@@ -13,7 +13,7 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_N_SCR = 8 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_HINT = 8, AM_SCR_SIZES = 9, AM_N_SCR = 10 };
 
 struct am_ctx {
   int device = 0;
@@ -35,6 +35,13 @@ struct am_ctx {
   // servers, include/antidote.hrl:28) serialize instead of sharing scratch; recursive
   // because composite calls (am_vnode_*, the *_host wrappers) re-enter.
   std::recursive_mutex mu;
+  // Group-index hints of a snapshot-cache read (am_snapcache.hip sets them around its
+  // am_launch_materialize call, null otherwise): grp_hint_in[w] = the token group of cached
+  // base word w in the log it was cached from (used only after its pair matches the group's
+  // pair in the current log, so a stale hint costs a search, never a wrong answer);
+  // grp_hint_out[o] = the group of result word o, written by the wave kernel.
+  const uint32_t *grp_hint_in = nullptr;
+  uint32_t *grp_hint_out = nullptr;
 };
 #define AM_LOCK(ctxp) std::lock_guard<std::recursive_mutex> am_lock_((ctxp)->mu)
 
@@ -140,6 +147,9 @@ int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am
 // the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
                           uint32_t *key_ngrp);
+// the chunked token-group view of the hot MV keys (am_grpbig.hip), after am_launch_group_build
+int am_launch_group_build_big(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
+                              uint32_t *key_ngrp);
 int am_store_pack(am_store *st);  // builds the packed streaming view (am_pack.hip)
 // am_store_update over a log view (am_gc.hip): counter = OpCounter per key or null; slack =>
 // the new store has room for appends (key_end / rec_key_end set, am_store_apply), at least
@@ -179,6 +189,22 @@ int am_launch_rows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
 // not materialized but marked in H.mask for the row tier
 int am_launch_stream_skip(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                           uint32_t type, const am_rows_cfg &H);
+// a key's group count (0 for an ungrouped key) and whether its view is the chunked one
+__host__ __device__ __forceinline__ uint32_t am_ngrp_count(uint32_t ng) {
+  return ng == AM_NGRP_NONE ? 0u : (ng & ~AM_NGRP_BIG);
+}
+__host__ __device__ __forceinline__ bool am_ngrp_big(uint32_t ng) {
+  return ng != AM_NGRP_NONE && (ng & AM_NGRP_BIG) != 0;
+}
+// a key that gets the chunked token-group view when its log allows (include/antidote_mat.h):
+// an MV register with more than AM_GRP_MAX_REC ops, all of one type
+__host__ __device__ __forceinline__ bool am_big_grp_key(const am_op_log &L, uint64_t k) {
+  return L.key_type[k] == AM_MVREG && am_kend(L, k) - L.key_off[k] > AM_GRP_MAX_REC &&
+         !(L.key_flags && (L.key_flags[k] & AM_KEY_MIXED_TYPES));
+}
+// the chunk table's words
+__host__ __device__ __forceinline__ uint64_t am_big_hdr(uint64_t ops) { return (ops + AM_BIG_CHUNK - 1) / AM_BIG_CHUNK + 1; }
+
 // the batch uses partial clocks, op ids, TxIds, cached bases or per-read clocks
 inline bool am_batch_general(const am_op_log *L, const am_read_batch *B) {
   return L->snap_pres || L->op_id || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock || B->base.v0 ||

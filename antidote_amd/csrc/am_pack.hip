@@ -85,11 +85,12 @@ __global__ void k_rec_count(am_op_log L, const uint32_t *okey, uint64_t *cnt, ui
       continue;
     }
     const uint32_t meta = L.op_meta[p];
-    uint64_t c = 0;
+    // a hot MV key's chunked view starts with its chunk table (include/antidote_mat.h)
+    uint64_t c = (p == L.key_off[k] && am_big_grp_key(L, k)) ? am_big_hdr(am_kend(L, k) - p) : 0;
     if (setk && !(meta & AM_META_BAD)) {
       CountSink cs;
       if (op_effects(L, p, type, meta, cs)) {
-        c = cs.n;
+        c += cs.n;
       } else {  // Type:update/2 raises on this effect: flagged, escaped, no records
         if (pk_vc) pk_vc[p] = AM_PK_ESC;
         op_meta[p] = (uint8_t)(meta | AM_META_BAD);
@@ -197,6 +198,7 @@ int build_records(am_store *st) {
     v.rec_key_off = (const uint64_t *)rko;
     v.rec_key_end = (const uint64_t *)rke;
     rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng);
+    if (!rc) rc = am_launch_group_build_big(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng);
     if (!rc && (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)) {
       am_set_error("token-group view: build pass failed");
       rc = AM_ERR_HIP;

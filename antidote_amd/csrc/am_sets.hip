@@ -149,7 +149,11 @@ __global__ void __launch_bounds__(BLOCK) k_sets(am_op_log L, am_read_batch B, am
       continue;
     }
     // A log far beyond the LDS tier goes straight to the big-read path (am_big.hip).
-    if (retry.list && off1 - off0 > BIG_OPS) {
+    // So does a hot MV key with the chunked token-group view (its grouped mode there streams u32
+    // records instead of var_data).
+    const bool big_grp = TYPE == AM_MVREG && L.key_ngrp && am_ngrp_big(uniform_u32(L.key_ngrp[key])) &&
+                         !(B.base.set_off && B.base.set_len[r]);
+    if (retry.list && (off1 - off0 > BIG_OPS || big_grp)) {
       if (tid == 0) retry.list[atomicAdd(retry.count, 1u)] = (uint32_t)r;
       continue;
     }

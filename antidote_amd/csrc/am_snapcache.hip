@@ -47,6 +47,7 @@ struct am_snapcache {
   uint32_t *plen = nullptr;    // [n_keys][CAP]
   uint64_t *pool_a = nullptr, *pool_b = nullptr;  // set pairs (a, b); bcounter slot values in a
   uint8_t *pool_p = nullptr;                      // bcounter slot presence
+  uint32_t *pool_g = nullptr;                     // set pairs: token-group hint (am_ctx::grp_hint_in)
   uint64_t pool_cap = 0;                          // words
   uint64_t *ctr = nullptr;     // device [0] pool words used
   std::vector<void *> allocs;
@@ -75,6 +76,7 @@ struct ScView {  // kernel-side copy of the cache pointers
   uint32_t *plen;
   uint64_t *pool_a, *pool_b;
   uint8_t *pool_p;
+  uint32_t *pool_g;
   uint64_t pool_cap;
   uint64_t *ctr;
 };
@@ -84,8 +86,6 @@ struct ScSel {
   uint64_t *base_vc, *v1, *set_off;
   uint32_t *base_pres, *set_len;
   int64_t *base_last_op, *v0;
-  uint64_t *cp_dst;  // k_sc_store -> k_sc_copy: the stored snapshot's value words go to pool
-  uint32_t *cp_len;  //   words [cp_dst, cp_dst + cp_len) from the read's result CSR (0: none)
 };
 // prune thresholds emitted by snapshot_insert_gc (optional)
 struct ScGc {
@@ -206,29 +206,35 @@ __device__ __forceinline__ uint32_t value_words(const am_read_result &R, uint64_
   return 0;
 }
 
-__global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_result R, ScSel S, const uint8_t *should_gc,
-                           ScGc G) {
+// One wave per 64 reads.  The pool room of the wave's stored snapshots is claimed with one
+// atomic per wave (a scan of the word counts), and the wave then copies every stored
+// snapshot's value words (set pairs, bounded-counter entries, group hints) from the read's
+// result CSR into the pool, a read at a time, coalesced.
+__global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_result R, ScSel S,
+                                                  const uint8_t *should_gc, ScGc G, const uint32_t *hint) {
   const uint32_t nd = C.n_dc;
   const uint64_t n = B.n_reads;
-  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint8_t code = S.code[r];
-    if (code == SEL_BAD) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t rb = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); rb < n; rb += step) {
+    const uint64_t r = rb + lane;
+    bool act = r < n;  // this lane's read goes on to the write-back
+    const uint8_t code = act ? S.code[r] : (uint8_t)SEL_BAD;
+    if (act && code == SEL_BAD) {
       if (R.status[r] == AM_OK) R.status[r] = AM_ERR_INVALID;
-      continue;
-    }
-    if (code == SEL_DUP) {
+      act = false;
+    } else if (act && code == SEL_DUP) {
       R.status[r] = AM_ERR_INVALID;
-      continue;
+      act = false;
+    } else if (act && code == SEL_COLD) {
+      R.status[r] = AM_ERR_COLD_PATH;  // get_from_snapshot_log: the log path, not the cache
+      act = false;
     }
-    if (code == SEL_COLD) {
-      R.status[r] = AM_ERR_COLD_PATH;
-      continue;
-    }
-    const uint64_t key = B.key[r];
-    const uint32_t t = B.type[r];
+    const uint64_t key = act ? B.key[r] : 0;
+    const uint32_t t = act ? B.type[r] : 0u;
     const uint64_t s0 = key * CAP;
-    uint32_t ne = C.cnt[key];
-    if (code == SEL_NEW_DICT) {  // store_snapshot(TxId, Key, Empty, vectorclock:new(), false)
+    uint32_t ne = act ? C.cnt[key] : 0u;
+    if (act && code == SEL_NEW_DICT) {  // store_snapshot(TxId, Key, Empty, vectorclock:new(), false)
       C.pres[s0] = 0;
       for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = 0;
       C.last_op[s0] = 0;
@@ -242,87 +248,95 @@ __global__ void k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_resul
     }
     // materialize_snapshot/7: number_of_ops == 0 returns the base; errors and
     // CommitTime == ignore return without caching
-    if (R.status[r] != AM_OK || am_kend(L, key) == L.key_off[key] || R.last_ct_ignore[r]) continue;
-    const bool sg = should_gc && should_gc[r];
-    if (!((R.is_new_ss[r] && S.newest[r] && R.count[r] >= MIN_OP_STORE_SS) || sg)) continue;
+    act = act && R.status[r] == AM_OK && am_kend(L, key) != L.key_off[key] && !R.last_ct_ignore[r];
+    const bool sg = act && should_gc && should_gc[r];
+    act = act && ((R.is_new_ss[r] && S.newest[r] && R.count[r] >= MIN_OP_STORE_SS) || sg);
     // internal_store_ss/4: ShouldInsert = NewLastOp - first.last_op_id >= MIN_OP_STORE_SS
-    const int64_t nlo = R.new_last_op[r];
-    if (!(nlo - C.last_op[s0] >= (int64_t)MIN_OP_STORE_SS || sg)) continue;
+    const int64_t nlo = act ? R.new_last_op[r] : 0;
+    act = act && (nlo - C.last_op[s0] >= (int64_t)MIN_OP_STORE_SS || sg);
     // vector_orddict:insert_bigger: prepend iff not vectorclock:le(New, First)
-    const uint32_t np = R.last_ct_pres[r];
-    const uint32_t fp = C.pres[s0];
-    bool le = true;
-    for (uint32_t d = 0; d < nd && le; ++d) {
-      const uint64_t x = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
-      le = x <= clk(C.vc + s0 * nd, fp, d);
+    const uint32_t np = act ? R.last_ct_pres[r] : 0u;
+    bool ins = false;
+    if (act) {
+      const uint32_t fp = C.pres[s0];
+      bool le = true;
+      for (uint32_t d = 0; d < nd && le; ++d) {
+        const uint64_t x = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
+        le = x <= clk(C.vc + s0 * nd, fp, d);
+      }
+      ins = !le;
     }
-    bool ins = !le;
     // the value words' room in the pool (sized on the host before the batch; offset 0 is never
     // handed out): if it is ever missing the snapshot is not cached at all -- the read's own
     // result stands -- rather than cached with an empty value (ctr[1] records the event)
     const uint32_t w = ins ? value_words(R, r, t, nd) : 0u;
+    const uint32_t inc = wave_incl_scan_u32(w, lane);
+    const uint32_t tot = (uint32_t)__shfl((int)inc, 63, WAVE);
     uint64_t off = 0;
-    if (w) {
-      off = atomicAdd((unsigned long long *)C.ctr, (unsigned long long)w);
-      if (off == 0 || off + w > C.pool_cap) {
-        atomicOr((unsigned long long *)(C.ctr + 1), 1ull);
-        ins = false;
-        off = 0;
+    if (tot) {
+      uint64_t base = 0;
+      if (lane == 63) base = atomicAdd((unsigned long long *)C.ctr, (unsigned long long)tot);
+      base = shfl_u64(base, 63);
+      if (w) {
+        off = base + inc - w;
+        if (off == 0 || off + w > C.pool_cap) {
+          atomicOr((unsigned long long *)(C.ctr + 1), 1ull);
+          ins = false;
+          off = 0;
+        }
       }
     }
-    // snapshot_insert_gc/4: at SNAPSHOT_THRESHOLD entries (or ShouldGC) keep the newest
-    // SNAPSHOT_MIN and prune the ops below their vectorclock:min
-    const uint32_t grown = ne + (ins ? 1u : 0u);
-    const bool gc = grown >= CAP || sg;
-    const uint32_t keep = gc ? (grown < SMIN ? grown : SMIN) : grown;
-    if (ins) {
-      for (uint32_t e = keep - 1; e >= 1; --e) {  // shift right by one (newest first)
-        const uint64_t dst = s0 + e, src = s0 + e - 1;
-        for (uint32_t d = 0; d < nd; ++d) C.vc[dst * nd + d] = C.vc[src * nd + d];
-        C.pres[dst] = C.pres[src];
-        C.last_op[dst] = C.last_op[src];
-        C.v0[dst] = C.v0[src];
-        C.v1[dst] = C.v1[src];
-        C.vflag[dst] = C.vflag[src];
-        C.poff[dst] = C.poff[src];
-        C.plen[dst] = C.plen[src];
+    if (act) {
+      // snapshot_insert_gc/4: at SNAPSHOT_THRESHOLD entries (or ShouldGC) keep the newest
+      // SNAPSHOT_MIN and prune the ops below their vectorclock:min
+      const uint32_t grown = ne + (ins ? 1u : 0u);
+      const bool gc = grown >= CAP || sg;
+      const uint32_t keep = gc ? (grown < SMIN ? grown : SMIN) : grown;
+      if (ins) {
+        for (uint32_t e = keep - 1; e >= 1; --e) {  // shift right by one (newest first)
+          const uint64_t dst = s0 + e, src = s0 + e - 1;
+          for (uint32_t d = 0; d < nd; ++d) C.vc[dst * nd + d] = C.vc[src * nd + d];
+          C.pres[dst] = C.pres[src];
+          C.last_op[dst] = C.last_op[src];
+          C.v0[dst] = C.v0[src];
+          C.v1[dst] = C.v1[src];
+          C.vflag[dst] = C.vflag[src];
+          C.poff[dst] = C.poff[src];
+          C.plen[dst] = C.plen[src];
+        }
+        for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
+        C.pres[s0] = np;
+        C.last_op[s0] = nlo;
+        C.v0[s0] = (t == AM_PN || t == AM_LWW) ? R.value.v0[r] : 0;
+        C.v1[s0] = t == AM_LWW ? R.value.v1[r] : 0;
+        C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
+        C.poff[s0] = off;
+        C.plen[s0] = off ? w : 0;
       }
-      for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
-      C.pres[s0] = np;
-      C.last_op[s0] = nlo;
-      C.v0[s0] = (t == AM_PN || t == AM_LWW) ? R.value.v0[r] : 0;
-      C.v1[s0] = t == AM_LWW ? R.value.v1[r] : 0;
-      C.vflag[s0] = t == AM_LWW ? R.value.vflag[r] : 0;
-      // the value words into the pool: copied by k_sc_copy, a wave per read (one thread
-      // copying a read's pairs serially cost C3's read/6 3.4 ms of 16)
-      if (w && off) S.cp_dst[r] = off, S.cp_len[r] = w;
-      C.poff[s0] = off;
-      C.plen[s0] = off ? w : 0;
+      C.cnt[key] = (uint8_t)keep;
+      if (gc && G.mask) {  // the prune threshold over the kept entries
+        G.thr_pres[key] = gc_threshold(C, s0, keep, G.thr_vc + key, C.n_keys);
+        G.mask[key] = 1;
+      }
     }
-    C.cnt[key] = (uint8_t)keep;
-    if (gc && G.mask) {  // the prune threshold over the kept entries
-      G.thr_pres[key] = gc_threshold(C, s0, keep, G.thr_vc + key, C.n_keys);
-      G.mask[key] = 1;
+    // the stored snapshots' value words into the pool (a thread copying a read's pairs
+    // serially cost C3's read/6 3.4 ms of 16)
+    const uint64_t src = off ? R.value.set_off[r] : 0;
+    for (uint64_t cm = __ballot(off != 0); cm; cm &= cm - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(cm);
+      const uint64_t sj = shfl_u64(src, j), dj = shfl_u64(off, j);
+      const uint32_t wj = shfl_u32(w, j);
+      for (uint32_t i = lane; i < wj; i += 64) {
+        C.pool_a[dj + i] = R.value.set_a[sj + i], C.pool_b[dj + i] = R.value.set_b[sj + i];
+        C.pool_g[dj + i] = hint ? hint[sj + i] : ~0u;
+      }
     }
-  }
-}
-
-// one wave per read: a stored snapshot's value words (set pairs, bounded-counter entries)
-// from the read's result CSR into the pool, coalesced
-__global__ void k_sc_copy(ScView C, am_read_result R, ScSel S, uint64_t n) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < n; r += waves) {
-    const uint32_t w = S.cp_len[r];
-    if (!w) continue;
-    const uint64_t src = R.value.set_off[r], dst = S.cp_dst[r];
-    for (uint32_t i = lane; i < w; i += 64) C.pool_a[dst + i] = R.value.set_a[src + i], C.pool_b[dst + i] = R.value.set_b[src + i];
   }
 }
 
 ScView view(const am_snapcache *c) {
   return ScView{c->n_dc, c->n_keys, c->cnt, c->owner, c->vc, c->pres, c->last_op, c->v0, c->v1, c->vflag,
-                c->poff, c->plen, c->pool_a, c->pool_b, c->pool_p, c->pool_cap, c->ctr};
+                c->poff, c->plen, c->pool_a, c->pool_b, c->pool_p, c->pool_g, c->pool_cap, c->ctr};
 }
 unsigned grid(uint64_t n) { return (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096); }
 
@@ -350,14 +364,17 @@ __global__ void k_pool_len(ScView C, uint64_t *len) {
     len[i] = (cnt != ABSENT && e < cnt && C.poff[i]) ? C.plen[i] : 0;
   }
 }
-__global__ void k_pool_move(ScView C, const uint64_t *off, uint64_t base, uint64_t *na, uint64_t *nb, uint8_t *np) {
+__global__ void k_pool_move(ScView C, const uint64_t *off, uint64_t base, uint64_t *na, uint64_t *nb, uint8_t *np,
+                            uint32_t *ng) {
   const uint64_t ne = C.n_keys * CAP;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = i / CAP, e = i % CAP;
     const uint32_t cnt = C.cnt[k];
     if (cnt == ABSENT || e >= cnt || !C.poff[i]) continue;
     const uint64_t src = C.poff[i], dst = base + off[i];
-    for (uint32_t j = 0; j < C.plen[i]; ++j) na[dst + j] = C.pool_a[src + j], nb[dst + j] = C.pool_b[src + j], np[dst + j] = C.pool_p[src + j];
+    for (uint32_t j = 0; j < C.plen[i]; ++j)
+      na[dst + j] = C.pool_a[src + j], nb[dst + j] = C.pool_b[src + j], np[dst + j] = C.pool_p[src + j],
+               ng[dst + j] = C.pool_g[src + j];
     C.poff[i] = dst;
   }
 }
@@ -365,13 +382,21 @@ __global__ void k_pool_move(ScView C, const uint64_t *off, uint64_t base, uint64
 // words at the pool start kept zero: a new() bounded counter's base (every slot absent)
 uint64_t reserved_words(uint32_t nd) { return (uint64_t)nd * nd + nd + 1; }
 
-// at least `need` free pool words after the used ones: compact, and grow when compaction
-// does not free enough (synchronizes the stream)
-int pool_reserve(am_snapcache *c, uint64_t need) {
+// a batch's sizes in one readback: the result CSR's first and last offsets and the pool
+// counters (words used, room-missing flag)
+__global__ void k_sc_sizes(const uint64_t *set_off, uint64_t n, const uint64_t *ctr, uint64_t *out) {
+  if (threadIdx.x == 0) {
+    out[0] = set_off ? set_off[0] : 0;
+    out[1] = set_off ? set_off[n] : 0;
+    out[2] = ctr[0];
+    out[3] = ctr[1];
+  }
+}
+
+// at least `need` free pool words after the used ones (w = the pool counters as read by
+// k_sc_sizes): compact, and grow when compaction does not free enough (synchronizes the stream)
+int pool_reserve(am_snapcache *c, uint64_t need, const uint64_t w[2]) {
   am_ctx *ctx = c->ctx;
-  uint64_t w[2] = {0, 0};
-  int rc = am_ctx_fetch(ctx, c->ctr, 2, w);
-  if (rc) return rc;
   if (w[1]) {  // an earlier batch found its room missing (k_sc_store did not cache that snapshot)
     am_set_error("am_snapcache: a snapshot was not cached for lack of value-pool room (pool sizing)");
     return AM_ERR_NOMEM;
@@ -402,12 +427,14 @@ int pool_reserve(am_snapcache *c, uint64_t need) {
   if (cap < 2 * (res + live + need)) cap = 2 * (res + live + need);  // grow: room for this batch twice
   uint64_t *na = nullptr, *nb = nullptr;
   uint8_t *np = nullptr;
+  uint32_t *ng = nullptr;
   ok = ok && hipMalloc((void **)&na, cap * 8) == hipSuccess && hipMalloc((void **)&nb, cap * 8) == hipSuccess &&
-       hipMalloc((void **)&np, cap) == hipSuccess;
+       hipMalloc((void **)&np, cap) == hipSuccess && hipMalloc((void **)&ng, cap * 4) == hipSuccess;
   ok = ok && hipMemsetAsync(na, 0, res * 8, ctx->stream) == hipSuccess &&
-       hipMemsetAsync(nb, 0, res * 8, ctx->stream) == hipSuccess && hipMemsetAsync(np, 0, res, ctx->stream) == hipSuccess;
+       hipMemsetAsync(nb, 0, res * 8, ctx->stream) == hipSuccess && hipMemsetAsync(np, 0, res, ctx->stream) == hipSuccess &&
+       hipMemsetAsync(ng, 0xFF, res * 4, ctx->stream) == hipSuccess;
   if (ok && ne) {
-    hipLaunchKernelGGL(k_pool_move, dim3(grid(ne)), dim3(256), 0, ctx->stream, V, len, res, na, nb, np);
+    hipLaunchKernelGGL(k_pool_move, dim3(grid(ne)), dim3(256), 0, ctx->stream, V, len, res, na, nb, np, ng);
     ok = hipGetLastError() == hipSuccess;
   }
   const uint64_t nused = res + live;
@@ -419,13 +446,15 @@ int pool_reserve(am_snapcache *c, uint64_t need) {
     if (na) (void)hipFree(na);
     if (nb) (void)hipFree(nb);
     if (np) (void)hipFree(np);
+    if (ng) (void)hipFree(ng);
     am_set_error("snapshot cache: value pool compaction failed");
     return AM_ERR_HIP;
   }
   (void)hipFree(c->pool_a);
   (void)hipFree(c->pool_b);
   (void)hipFree(c->pool_p);
-  c->pool_a = na, c->pool_b = nb, c->pool_p = np, c->pool_cap = cap;
+  (void)hipFree(c->pool_g);
+  c->pool_a = na, c->pool_b = nb, c->pool_p = np, c->pool_g = ng, c->pool_cap = cap;
   return AM_OK;
 }
 
@@ -499,7 +528,8 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
   c->pool_cap = 4 * res + 4096;
   if (!rc && (hipMalloc((void **)&c->pool_a, c->pool_cap * 8) != hipSuccess ||
               hipMalloc((void **)&c->pool_b, c->pool_cap * 8) != hipSuccess ||
-              hipMalloc((void **)&c->pool_p, c->pool_cap) != hipSuccess))
+              hipMalloc((void **)&c->pool_p, c->pool_cap) != hipSuccess ||
+              hipMalloc((void **)&c->pool_g, c->pool_cap * 4) != hipSuccess))
     rc = AM_ERR_NOMEM;
   if (!rc && (hipMemsetAsync(c->cnt, ABSENT, n_keys + 16, ctx->stream) != hipSuccess ||
               hipMemsetAsync(c->owner, 0xFF, (n_keys + 1) * 4, ctx->stream) != hipSuccess ||
@@ -508,6 +538,7 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
               hipMemsetAsync(c->pool_a, 0, res * 8, ctx->stream) != hipSuccess ||
               hipMemsetAsync(c->pool_b, 0, res * 8, ctx->stream) != hipSuccess ||
               hipMemsetAsync(c->pool_p, 0, res, ctx->stream) != hipSuccess ||
+              hipMemsetAsync(c->pool_g, 0xFF, res * 4, ctx->stream) != hipSuccess ||
               hipMemcpyAsync(c->ctr, &res, 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
               hipMemsetAsync(c->ctr + 1, 0, 8, ctx->stream) != hipSuccess ||
               hipStreamSynchronize(ctx->stream) != hipSuccess))
@@ -607,6 +638,7 @@ int am_snapcache_destroy(am_snapcache *c) {
   if (c->pool_a) (void)hipFree(c->pool_a);
   if (c->pool_b) (void)hipFree(c->pool_b);
   if (c->pool_p) (void)hipFree(c->pool_p);
+  if (c->pool_g) (void)hipFree(c->pool_g);
   delete c;
   return AM_OK;
 }
@@ -635,19 +667,25 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   if (n == 0) return AM_OK;
   const uint32_t nd = c->n_dc;
   // value pool room for every value this batch could store
-  uint64_t need = 0;
-  if (th == 0 || th == AM_AWSET || th == AM_MVREG || th == AM_BCOUNTER) {
-    if (R->value.set_off) {
-      uint64_t so[2] = {0, 0};
-      int rc = am_ctx_fetch(ctx, R->value.set_off, 1, &so[0]);
-      if (!rc) rc = am_ctx_fetch(ctx, R->value.set_off + n, 1, &so[1]);
-      if (rc) return rc;
-      need += so[1] - so[0];
-    }
+  uint64_t need = 0, words_end = 0;
+  if ((th == 0 || th == AM_AWSET || th == AM_MVREG || th == AM_BCOUNTER) && R->value.set_off) {
+    void *sz = nullptr;
+    if (int rc = am_ctx_scratch(ctx, AM_SCR_SIZES, 64, &sz)) return rc;
+    hipLaunchKernelGGL(k_sc_sizes, dim3(1), dim3(64), 0, ctx->stream, R->value.set_off, n, c->ctr, (uint64_t *)sz);
+    AM_HIP(hipGetLastError());
+    uint64_t w[4] = {0, 0, 0, 0};
+    if (int rc = am_ctx_fetch(ctx, sz, 4, w)) return rc;
+    need = w[1] - w[0];
+    words_end = w[1];
+    if (need)
+      if (int rc = pool_reserve(c, need, w + 2)) return rc;
   }
-  if (need) {
-    int rc = pool_reserve(c, need);
-    if (rc) return rc;
+  // the result words' group hints (am_ctx::grp_hint_out), copied into the pool with the words
+  uint32_t *hint = nullptr;
+  if (need && (th == 0 || th == AM_AWSET || th == AM_MVREG)) {
+    void *h = nullptr;
+    if (int rc = am_ctx_scratch(ctx, AM_SCR_HINT, (words_end + 1) * 4, &h)) return rc;
+    hint = (uint32_t *)h;
   }
   // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres, set_len [n] u32 |
   // base_last_op, v0, v1, set_off [n] u64 | base_vc [nd][n]
@@ -666,8 +704,6 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   S.v0 = (int64_t *)take(n * 8);
   S.v1 = (uint64_t *)take(n * 8);
   S.set_off = (uint64_t *)take(n * 8);
-  S.cp_dst = (uint64_t *)take(n * 8);
-  S.cp_len = (uint32_t *)take(n * 4);
   S.base_vc = (uint64_t *)take(n * nd * 8);
   S.base_pres = (uint32_t *)take(n * 4);
   S.set_len = (uint32_t *)take(n * 4);
@@ -693,16 +729,14 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
     db.base.set_len = S.set_len;
     db.base.set_a = c->pool_a;
     db.base.set_b = c->pool_b;
+    ctx->grp_hint_in = c->pool_g;
+    ctx->grp_hint_out = hint;
     rc = am_launch_materialize(ctx, L, &db, R);
+    ctx->grp_hint_in = nullptr;
+    ctx->grp_hint_out = nullptr;
     if (rc == AM_OK) {
       const ScGc G{gc_mask, thr_vc, thr_pres};
-      if (hipMemsetAsync(S.cp_len, 0, n * 4, ctx->stream) != hipSuccess) {
-        rc = AM_ERR_HIP;
-      } else {
-        hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G);
-        const uint64_t wg = (n + 3) / 4 < 65536 ? (n + 3) / 4 : 65536;
-        hipLaunchKernelGGL(k_sc_copy, dim3((unsigned)wg), dim3(256), 0, ctx->stream, V, *R, S, n);
-      }
+      hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G, hint);
       if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
     }
   }

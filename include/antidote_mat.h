@@ -212,6 +212,23 @@ typedef struct am_op_log {
 #define AM_REC_GRP(m) ((m) >> 17)
 #define AM_NGRP_NONE 0xFFFFFFFFu
 #define AM_GRP_MAX_REC 2048u
+/* Chunked token-group view of a hot MV-register key (more than AM_GRP_MAX_REC ops): its groups
+ * are built with device-wide sorts instead of one workgroup's LDS, key_ngrp[k] = G |
+ * AM_NGRP_BIG (G < AM_BIG_MAX_GRP), and its record range is laid out per AM_BIG_CHUNK ops:
+ *   rec_g[rec_key_off[k] + c], c = 0..nch   the chunk table: record offset (relative to
+ *                                           rec_key_off[k]) of the first record of key op
+ *                                           c * AM_BIG_CHUNK; entry nch ends the last chunk
+ *                                           (nch = ceil(ops / AM_BIG_CHUNK))
+ *   then one record per birth / effective kill, in op order:
+ *     op within its chunk (bits 0-9) | kill << 10 | group << 11, or 0xFFFFFFFF
+ * Groups and their pairs (grp) are as above; an effective kill always follows its group's
+ * birth, so a group survives a read iff its birth is included and no kill of it is. */
+#define AM_NGRP_BIG 0x80000000u
+#define AM_BIG_CHUNK 1024u
+#define AM_BIG_MAX_GRP (1u << 21)
+#define AM_BREC_OP(m) ((m) & 0x3FFu)
+#define AM_BREC_KILL (1u << 10)
+#define AM_BREC_GRP(m) ((m) >> 11)
 #define AM_PK_ESC 0xFFFFFFFFu
 
 /*

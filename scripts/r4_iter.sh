@@ -9,7 +9,7 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/steps.log
 if [ $rc -ge 2 ]; then exit $rc; fi
 cp antidote_amd/libantidote_mat.so /tmp/intree.so
 VARS="${C4_VARS:-old cur gm2}" CFG=c4 ROUNDS=2 bash scripts/ab_libs.sh || exit $?
-VARS="${C5_VARS:-c5old cur}" CFG=c5 ROUNDS=1 bash scripts/ab_libs.sh || exit $?
+VARS="${C5_VARS:-cur big}" CFG=c5 ROUNDS=1 bash scripts/ab_libs.sh || exit $?
 if [ -n "${PMC_VARS:-}" ]; then VARS="$PMC_VARS" CFG=c4 bash scripts/pmc_sq.sh || exit $?; fi
 cp /tmp/intree.so antidote_amd/libantidote_mat.so
 echo done >> gpurun_out/steps.log
