@@ -568,10 +568,19 @@ __device__ __forceinline__ uint32_t base_group(const am_op_log &L, uint64_t rk0,
   return ~0u;
 }
 
-// group-index hints of a snapshot-cache read (am_ctx::grp_hint_in / grp_hint_out)
+// a snapshot-cache read's group hints and pool tee (am_ctx::grp_hint_in, tee_*)
 struct GrpHint {
   const uint32_t *in;  // [base word] the pair's group when it was cached, or null
-  uint32_t *out;       // [result word] the output pair's group, or null
+  uint64_t *pa, *pb;   // the pool's words (null: no tee)
+  uint32_t *pg;
+  int64_t shift;       // pool word of result word o
+  uint8_t *done;       // [read] its words are in the pool
+  __device__ __forceinline__ void put(uint64_t o, uint64_t a, uint64_t b, uint32_t g) const {
+    if (pa) {
+      const uint64_t q = (uint64_t)((int64_t)o + shift);
+      pa[q] = a, pb[q] = b, pg[q] = g;
+    }
+  }
 };
 
 // base pair (a, b)'s group through its hint: one load of the hinted group's pair; a hint
@@ -672,7 +681,7 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
       }
       const uint64_t o = ooff + i + alive_below(lo);
       R.value.set_a[o] = np[h].x, R.value.set_b[o] = np[h].y;
-      if (H.out) H.out[o] = list[i];
+      H.put(o, np[h].x, np[h].y, list[i]);
     }
     const uint32_t jb = lane + 64u * h;
     if (jb < nb && ((am[h] >> lane) & 1ull)) {  // + new survivors with a key not above it
@@ -684,7 +693,7 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
       }
       const uint64_t o = ooff + alive_below(jb) + lo;
       R.value.set_a[o] = bp[h].x, R.value.set_b[o] = bp[h].y;
-      if (H.out) H.out[o] = bg[h];
+      H.put(o, bp[h].x, bp[h].y, bg[h]);
     }
   }
   wave_sync();
@@ -879,8 +888,8 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           if (j2 < nput) p2 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j2]));
           if (j1 < nput) R.value.set_a[ooff + j1] = p1.x, R.value.set_b[ooff + j1] = p1.y;
           if (j2 < nput) R.value.set_a[ooff + j2] = p2.x, R.value.set_b[ooff + j2] = p2.y;
-          if (H.out && j1 < nput) H.out[ooff + j1] = s.list[j1];
-          if (H.out && j2 < nput) H.out[ooff + j2] = s.list[j2];
+          if (j1 < nput) H.put(ooff + j1, p1.x, p1.y, s.list[j1]);
+          if (j2 < nput) H.put(ooff + j2, p2.x, p2.y, s.list[j2]);
         }
         if (ns > ocap) status = AM_ERR_CAPACITY;
       }
@@ -897,6 +906,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           R.count[r] = count;
           R.value.set_len[r] = ns;
         }
+        if (H.done) H.done[r] = status == AM_OK ? 1 : 0;
       }
       PH(5);
       wave_sync();
@@ -1087,7 +1097,8 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     if (blocks > cap) blocks = cap;
     if (blocks == 0) return AM_OK;
     hipLaunchKernelGGL((k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), smem,
-                       ctx->stream, *L, *B, *R, S, next, short_opl, GrpHint{ctx->grp_hint_in, ctx->grp_hint_out});
+                       ctx->stream, *L, *B, *R, S, next, short_opl, GrpHint{ctx->grp_hint_in, ctx->tee_a, ctx->tee_b, ctx->tee_g, ctx->tee_shift,
+                                                                  ctx->tee_done});
   } else if (tier == AM_GRP_ROW) {
     static int occ = 0;
     if (!occ) {

@@ -210,7 +210,7 @@ int am_launch_group_build_big(am_ctx *ctx, const am_op_log *L, const uint64_t *r
   uint32_t *pos_s = nullptr, *flag = nullptr, *gid = nullptr;
   if (!alloc(n * 8, (void **)&C.tok) || !alloc(n * 8, (void **)&C.val) || !alloc(n * 4, (void **)&C.info) ||
       !alloc(n * 4, (void **)&C.kid) || !alloc(n * 4, (void **)&C.pos) || !alloc(n * 8, (void **)&tok_s) ||
-      !alloc(n * 4, (void **)&pos_s) || !alloc(n * 4, (void **)&flag) || !alloc(n * 4, (void **)&gid))
+      !alloc(n * 4, (void **)&pos_s) || !alloc(n * 4, (void **)&flag) || !alloc(n * 4 + 8, (void **)&gid))
     return done(AM_ERR_NOMEM);
   const unsigned eb = nb < 65536u ? nb : 65536u;
   hipLaunchKernelGGL(k_bg_emit, dim3(eb), dim3(256), 0, st, *L, rcnt, nb, list, bo, C);

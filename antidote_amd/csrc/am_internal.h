@@ -13,7 +13,7 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_HINT = 8, AM_SCR_SIZES = 9, AM_N_SCR = 10 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_N_SCR = 9 };
 
 struct am_ctx {
   int device = 0;
@@ -35,13 +35,20 @@ struct am_ctx {
   // servers, include/antidote.hrl:28) serialize instead of sharing scratch; recursive
   // because composite calls (am_vnode_*, the *_host wrappers) re-enter.
   std::recursive_mutex mu;
-  // Group-index hints of a snapshot-cache read (am_snapcache.hip sets them around its
-  // am_launch_materialize call, null otherwise): grp_hint_in[w] = the token group of cached
-  // base word w in the log it was cached from (used only after its pair matches the group's
-  // pair in the current log, so a stale hint costs a search, never a wrong answer);
-  // grp_hint_out[o] = the group of result word o, written by the wave kernel.
+  // A snapshot-cache read (am_snapcache.hip sets these around its am_launch_materialize
+  // call, null otherwise):
+  //   grp_hint_in[w]  the token group of cached base word w in the log it was cached from
+  //                   (used only after its pair matches the group's pair in the current log,
+  //                   so a stale hint costs a search, never a wrong answer)
+  //   tee_*           the wave kernel also writes every value word it outputs (result word o)
+  //                   into the cache's pool at word o + tee_shift, with its group, and sets
+  //                   tee_done[r]; k_sc_store then links a stored snapshot to those words
+  //                   instead of copying them
   const uint32_t *grp_hint_in = nullptr;
-  uint32_t *grp_hint_out = nullptr;
+  uint64_t *tee_a = nullptr, *tee_b = nullptr;
+  uint32_t *tee_g = nullptr;
+  int64_t tee_shift = 0;
+  uint8_t *tee_done = nullptr;
 };
 #define AM_LOCK(ctxp) std::lock_guard<std::recursive_mutex> am_lock_((ctxp)->mu)
 

@@ -383,12 +383,10 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_g(am_op_log L, am_read_batch B,
 //   * a read the quad does not take (longer logs up to 64 ops / 64 groups, an escaped op) is
 //     finished by its own lane; results come back through LDS; survivors leave through one
 //     gather per wave; each lane writes its read's outputs (coalesced stores).
-#ifndef AMK_QPH
-#define AMK_QPH 4
-#endif
+// phases whose loads are in flight together (2 at D <= 4 measured within noise of 4)
 template <int DMAX>
 constexpr int qph() {
-  return DMAX <= 4 ? AMK_QPH : DMAX <= 8 ? (AMK_QPH < 2 ? AMK_QPH : 2) : 1;
+  return DMAX <= 4 ? 4 : DMAX <= 8 ? 2 : 1;
 }
 template <int DMAX>
 struct QSlot {  // the read at a scan position, for the quad that scans it
@@ -624,10 +622,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
     //      read does not need is loaded from its column's first line (one line for the whole
     //      chip, cached) and ignored, so the loads issue back to back with no branch between
     //      them and the wave's later waits count them exactly ----
-#ifndef AMK_QPG_UNROLL
-#define AMK_QPG_UNROLL 4
-#endif
-#pragma unroll AMK_QPG_UNROLL
+#pragma unroll
     for (int pg = 0; pg < 4; pg += NPH) {
       u32x4 xv[NPH][DMAX], wv[NPH][4];
 #pragma unroll

@@ -86,6 +86,8 @@ struct ScSel {
   uint64_t *base_vc, *v1, *set_off;
   uint32_t *base_pres, *set_len;
   int64_t *base_last_op, *v0;
+  uint64_t *cp_dst;  // k_sc_store -> k_sc_copy: the stored snapshot's value words go to pool
+  uint32_t *cp_len;  //   words [cp_dst, cp_dst + cp_len) from the read's result CSR (0: none)
 };
 // prune thresholds emitted by snapshot_insert_gc (optional)
 struct ScGc {
@@ -206,12 +208,14 @@ __device__ __forceinline__ uint32_t value_words(const am_read_result &R, uint64_
   return 0;
 }
 
-// One wave per 64 reads.  The pool room of the wave's stored snapshots is claimed with one
-// atomic per wave (a scan of the word counts), and the wave then copies every stored
-// snapshot's value words (set pairs, bounded-counter entries, group hints) from the read's
-// result CSR into the pool, a read at a time, coalesced.
+// Pool room: the batch reserved one pool word per result word (pool_reserve), so read r's
+// snapshot goes to words [used + set_off[r] - set_off[0], + w) -- no atomics (one per read on
+// one counter cost most of this kernel).  The group wave kernel already wrote the words there
+// (tee_done[r]); k_sc_copy moves the others' from the result CSR.
 __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_result R, ScSel S,
-                                                  const uint8_t *should_gc, ScGc G, const uint32_t *hint) {
+                                                  const uint8_t *should_gc, ScGc G, uint64_t used, uint64_t so0,
+                                                  uint64_t new_used, const uint8_t *teed) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && new_used != ~0ull) C.ctr[0] = new_used;
   const uint32_t nd = C.n_dc;
   const uint64_t n = B.n_reads;
   const uint32_t lane = threadIdx.x & 63u;
@@ -270,20 +274,13 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
     // handed out): if it is ever missing the snapshot is not cached at all -- the read's own
     // result stands -- rather than cached with an empty value (ctr[1] records the event)
     const uint32_t w = ins ? value_words(R, r, t, nd) : 0u;
-    const uint32_t inc = wave_incl_scan_u32(w, lane);
-    const uint32_t tot = (uint32_t)__shfl((int)inc, 63, WAVE);
     uint64_t off = 0;
-    if (tot) {
-      uint64_t base = 0;
-      if (lane == 63) base = atomicAdd((unsigned long long *)C.ctr, (unsigned long long)tot);
-      base = shfl_u64(base, 63);
-      if (w) {
-        off = base + inc - w;
-        if (off == 0 || off + w > C.pool_cap) {
-          atomicOr((unsigned long long *)(C.ctr + 1), 1ull);
-          ins = false;
-          off = 0;
-        }
+    if (w) {
+      off = used + (R.value.set_off[r] - so0);
+      if (off == 0 || off + w > C.pool_cap) {
+        atomicOr((unsigned long long *)(C.ctr + 1), 1ull);
+        ins = false;
+        off = 0;
       }
     }
     if (act) {
@@ -319,17 +316,24 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
         G.mask[key] = 1;
       }
     }
-    // the stored snapshots' value words into the pool (a thread copying a read's pairs
-    // serially cost C3's read/6 3.4 ms of 16)
-    const uint64_t src = off ? R.value.set_off[r] : 0;
-    for (uint64_t cm = __ballot(off != 0); cm; cm &= cm - 1) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(cm);
-      const uint64_t sj = shfl_u64(src, j), dj = shfl_u64(off, j);
-      const uint32_t wj = shfl_u32(w, j);
-      for (uint32_t i = lane; i < wj; i += 64) {
-        C.pool_a[dj + i] = R.value.set_a[sj + i], C.pool_b[dj + i] = R.value.set_b[sj + i];
-        C.pool_g[dj + i] = hint ? hint[sj + i] : ~0u;
-      }
+    if (r < n) S.cp_dst[r] = off, S.cp_len[r] = (off && !(teed && teed[r])) ? w : 0u;
+  }
+}
+
+// the value words (set pairs, bounded-counter entries) of stored snapshots the group wave
+// kernel did not tee from the read's result CSR into the pool: 16 lanes per read, four reads
+// per wave, coalesced (a thread copying a read's pairs serially cost C3's read/6 3.4 ms of 16;
+// copying them inside k_sc_store, a read at a time per wave, 1.45 ms)
+__global__ void k_sc_copy(ScView C, am_read_result R, ScSel S, uint64_t n) {
+  const uint32_t sl = threadIdx.x & 15u;
+  const uint64_t rows = (uint64_t)gridDim.x * (blockDim.x / 16);
+  for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x / 16) + threadIdx.x / 16; r < n; r += rows) {
+    const uint32_t w = S.cp_len[r];
+    if (!w) continue;
+    const uint64_t src = R.value.set_off[r], dst = S.cp_dst[r];
+    for (uint32_t i = sl; i < w; i += 16) {
+      C.pool_a[dst + i] = R.value.set_a[src + i], C.pool_b[dst + i] = R.value.set_b[src + i];
+      C.pool_g[dst + i] = ~0u;  // no group hint
     }
   }
 }
@@ -395,13 +399,14 @@ __global__ void k_sc_sizes(const uint64_t *set_off, uint64_t n, const uint64_t *
 
 // at least `need` free pool words after the used ones (w = the pool counters as read by
 // k_sc_sizes): compact, and grow when compaction does not free enough (synchronizes the stream)
-int pool_reserve(am_snapcache *c, uint64_t need, const uint64_t w[2]) {
+int pool_reserve(am_snapcache *c, uint64_t need, const uint64_t w[2], uint64_t *used_out) {
   am_ctx *ctx = c->ctx;
   if (w[1]) {  // an earlier batch found its room missing (k_sc_store did not cache that snapshot)
     am_set_error("am_snapcache: a snapshot was not cached for lack of value-pool room (pool sizing)");
     return AM_ERR_NOMEM;
   }
   const uint64_t used = w[0];
+  *used_out = used;
   if (used + need <= c->pool_cap) return AM_OK;
   const uint64_t ne = c->n_keys * CAP;
   uint64_t *len = nullptr;
@@ -438,6 +443,7 @@ int pool_reserve(am_snapcache *c, uint64_t need, const uint64_t w[2]) {
     ok = hipGetLastError() == hipSuccess;
   }
   const uint64_t nused = res + live;
+  *used_out = nused;
   ok = ok && hipMemcpyAsync(c->ctr, &nused, 8, hipMemcpyHostToDevice, ctx->stream) == hipSuccess &&
        hipStreamSynchronize(ctx->stream) == hipSuccess;
   (void)hipFree(len);
@@ -667,7 +673,7 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   if (n == 0) return AM_OK;
   const uint32_t nd = c->n_dc;
   // value pool room for every value this batch could store
-  uint64_t need = 0, words_end = 0;
+  uint64_t need = 0, so0 = 0, used = 0, new_used = ~0ull;  // ~0: the pool counter stays
   if ((th == 0 || th == AM_AWSET || th == AM_MVREG || th == AM_BCOUNTER) && R->value.set_off) {
     void *sz = nullptr;
     if (int rc = am_ctx_scratch(ctx, AM_SCR_SIZES, 64, &sz)) return rc;
@@ -676,20 +682,15 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
     uint64_t w[4] = {0, 0, 0, 0};
     if (int rc = am_ctx_fetch(ctx, sz, 4, w)) return rc;
     need = w[1] - w[0];
-    words_end = w[1];
-    if (need)
-      if (int rc = pool_reserve(c, need, w + 2)) return rc;
-  }
-  // the result words' group hints (am_ctx::grp_hint_out), copied into the pool with the words
-  uint32_t *hint = nullptr;
-  if (need && (th == 0 || th == AM_AWSET || th == AM_MVREG)) {
-    void *h = nullptr;
-    if (int rc = am_ctx_scratch(ctx, AM_SCR_HINT, (words_end + 1) * 4, &h)) return rc;
-    hint = (uint32_t *)h;
+    so0 = w[0];
+    if (need) {
+      if (int rc = pool_reserve(c, need, w + 2, &used)) return rc;
+      new_used = used + need;  // this batch's words: one pool word per result word
+    }
   }
   // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres, set_len [n] u32 |
   // base_last_op, v0, v1, set_off [n] u64 | base_vc [nd][n]
-  const size_t bytes = n * (4 + 8 + 4 * 8 + (size_t)nd * 8 + 12) + 4096;
+  const size_t bytes = n * (4 + 8 + 4 * 8 + (size_t)nd * 8 + 13) + 4096;
   void *scr = nullptr;
   int rc = am_ctx_scratch(ctx, AM_SCR_SNAP, bytes, &scr);
   if (rc) return rc;
@@ -704,6 +705,8 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   S.v0 = (int64_t *)take(n * 8);
   S.v1 = (uint64_t *)take(n * 8);
   S.set_off = (uint64_t *)take(n * 8);
+  S.cp_dst = (uint64_t *)take(n * 8);
+  S.cp_len = (uint32_t *)take(n * 4);
   S.base_vc = (uint64_t *)take(n * nd * 8);
   S.base_pres = (uint32_t *)take(n * 4);
   S.set_len = (uint32_t *)take(n * 4);
@@ -711,6 +714,7 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   S.newest = (uint8_t *)take(n);
   S.base_ignore = (uint8_t *)take(n);
   S.vflag = (uint8_t *)take(n);
+  uint8_t *teed = (uint8_t *)take(n);
   const ScView V = view(c);
   hipLaunchKernelGGL(k_sc_claim, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B);
   hipLaunchKernelGGL(k_sc_select, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *B, S);
@@ -729,14 +733,24 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
     db.base.set_len = S.set_len;
     db.base.set_a = c->pool_a;
     db.base.set_b = c->pool_b;
+    // the group wave kernel tees set pairs into the pool (am_ctx::tee_*)
+    const bool tee = need && (th == 0 || th == AM_AWSET || th == AM_MVREG) &&
+                     hipMemsetAsync(teed, 0, n, ctx->stream) == hipSuccess;
     ctx->grp_hint_in = c->pool_g;
-    ctx->grp_hint_out = hint;
+    if (tee) {
+      ctx->tee_a = c->pool_a, ctx->tee_b = c->pool_b, ctx->tee_g = c->pool_g, ctx->tee_done = teed;
+      ctx->tee_shift = (int64_t)used - (int64_t)so0;
+    }
     rc = am_launch_materialize(ctx, L, &db, R);
     ctx->grp_hint_in = nullptr;
-    ctx->grp_hint_out = nullptr;
+    ctx->tee_a = ctx->tee_b = nullptr, ctx->tee_g = nullptr, ctx->tee_done = nullptr, ctx->tee_shift = 0;
     if (rc == AM_OK) {
       const ScGc G{gc_mask, thr_vc, thr_pres};
-      hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G, hint);
+      hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G, used,
+                         so0, new_used, tee ? (const uint8_t *)teed : nullptr);
+      const uint64_t rows = (n + 15) / 16;
+      hipLaunchKernelGGL(k_sc_copy, dim3((unsigned)(rows < 65536 ? rows : 65536)), dim3(256), 0, ctx->stream, V, *R, S,
+                         n);
       if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
     }
   }

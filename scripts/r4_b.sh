@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-4 iteration on one box: GPU tests (in-tree library), then A/B of library variants.
+# round-4 iteration B: GPU tests, cached C3 A/B (hints only vs hints + split copy), kernel
+# stats of c5 / c4 / c3 with the in-tree library, SQ counters of c4.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -8,8 +9,9 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --maxfail=8 --timeout 120 
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/steps.log
 if [ $rc -ge 2 ]; then exit $rc; fi
 cp antidote_amd/libantidote_mat.so /tmp/intree.so
-VARS="${C4_VARS:-cur gm2}" CFG=c4 ROUNDS=2 bash scripts/ab_libs.sh || exit $?
-VARS="${C5_VARS:-cur big}" CFG=c5 ROUNDS=1 bash scripts/ab_libs.sh || exit $?
-if [ -n "${PMC_VARS:-}" ]; then VARS="$PMC_VARS" CFG=c4 bash scripts/pmc_sq.sh || exit $?; fi
+VARS="sep tee" CFG=c3 ROUNDS=2 BENCH_EXTRA="--base cached" bash scripts/ab_libs.sh || exit $?
+cp /tmp/intree.so antidote_amd/libantidote_mat.so
+CFGS="c5 c4" bash scripts/prof_configs.sh || exit $?
+VARS="tee" CFG=c4 bash scripts/pmc_sq.sh || exit $?
 cp /tmp/intree.so antidote_amd/libantidote_mat.so
 echo done >> gpurun_out/steps.log

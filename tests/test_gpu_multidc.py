@@ -49,6 +49,21 @@ class _Tee:
         self.n += 1
         return a
 
+    def restart(self, dc):
+        self.g.restart(dc)
+        self.o.restart(dc)
+
+    def read_many(self, dc, keys, clock):
+        a, b = self.g.read_many(dc, keys, clock), self.o.read_many(dc, keys, clock)
+        assert a == b, ("read_many", dc, keys, clock, a, b)
+        self.n += 1
+        return a
+
+    def gst(self, dc, parts, gr):
+        a, b = self.g.gst(dc, parts, gr), self.o.gst(dc, parts, gr)
+        assert a == b, ("gst", dc, parts, gr, a, b)
+        return a
+
     def close(self):
         self.g.close()
 
