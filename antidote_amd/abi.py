@@ -58,6 +58,7 @@ class am_op_log(ctypes.Structure):
         ("key_tbase", c_void_p), ("pk_vc", c_void_p),
         ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp", c_void_p),
         ("key_ngrp", c_void_p), ("key_end", c_void_p), ("rec_key_end", c_void_p), ("gmask", c_void_p),
+        ("zone_vc", c_void_p),
     ]
 
 
@@ -95,6 +96,8 @@ class am_synth_params(ctypes.Structure):
 
 
 AM_SYNTH_MV_BC = 6
+AM_STAT_OPS_SKIPPED = 0
+AM_ZONE_OPS = 256
 AM_ERR_COLD_PATH = 5
 AM_SNAPSHOT_THRESHOLD = 10
 AM_SNAPCACHE_ABSENT = 0xFFFFFFFF
@@ -112,6 +115,7 @@ SIGNATURES = [
     ("am_ctx_sync", c_int, [c_void_p]),
     ("am_last_error", c_char_p, []),
     ("am_timer_start", c_int, [c_void_p]),
+    ("am_ctx_stat", c_int, [c_void_p, c_int, c_void_p, c_int]),
     ("am_timer_stop", c_int, [c_void_p, POINTER(c_float)]),
     ("am_dev_alloc", c_int, [c_void_p, ctypes.c_size_t, POINTER(c_void_p)]),
     ("am_dev_free", c_int, [c_void_p, c_void_p]),
@@ -211,7 +215,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 6:
+        if L.am_abi_version() != 7:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

@@ -100,6 +100,15 @@ __global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter,
           const_cast<uint32_t *>(L.pk_vc)[(uint64_t)d * ls + q] = S.pk_vc[(uint64_t)d * ss + p];
       if (L.var_off) const_cast<uint64_t *>(L.var_off)[q] = vb + (S.var_off ? S.var_off[p] - sv0 : 0);
       if (L.gmask) const_cast<uint64_t *>(L.gmask)[q] = S.gmask ? S.gmask[p] : 0;
+      if (L.zone_vc) {  // the zone map stays an upper bound of the ops written into it
+        const uint64_t nz = (ls + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
+        const uint32_t dc = AM_META_DC(S.op_meta[p]), sp = S.snap_pres ? S.snap_pres[p] : 0xFFFFFFFFu;
+        for (uint32_t d = 0; d < L.n_dc; ++d) {
+          const uint64_t x = d == dc ? S.commit_time[p] : (((sp >> d) & 1u) ? S.snap_vc[(uint64_t)d * ss + p] : 0);
+          atomicMax((unsigned long long *)const_cast<uint64_t *>(L.zone_vc) + (uint64_t)d * nz + q / AM_ZONE_OPS,
+                    (unsigned long long)x);
+        }
+      }
     }
     for (uint64_t q = d0 + n + lane; L.gmask && q < cap_end; q += WAVE_SZ) const_cast<uint64_t *>(L.gmask)[q] = 0;
     if (L.var_off) {
@@ -220,7 +229,7 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   view.n_keys = m;
   view.key_off = V.off, view.key_end = V.end, view.key_id_base = V.idb, view.key_type = V.type, view.key_flags = V.flags;
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
-  view.gmask = nullptr;
+  view.gmask = nullptr, view.zone_vc = nullptr;
   am_store *sub = nullptr;
   int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
                               false, nullptr, &sub);
@@ -347,7 +356,7 @@ int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint
   view.key_off = (uint64_t *)b, view.key_end = (uint64_t *)(b + o_end), view.key_id_base = (uint64_t *)(b + o_idb);
   view.key_type = (uint8_t *)(b + o_type), view.key_flags = (uint8_t *)(b + o_flags);
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
-  view.gmask = nullptr;
+  view.gmask = nullptr, view.zone_vc = nullptr;
   hipLaunchKernelGGL(k_grow_view, dim3(grid_threads(n_new + 1)), dim3(256), 0, c->stream, L,
                      (const uint64_t *)st->counter, n_new, (uint64_t *)view.key_off, (uint64_t *)view.key_end,
                      (uint64_t *)view.key_id_base, (uint64_t *)(b + o_ctr), (uint8_t *)view.key_type,

@@ -47,6 +47,7 @@ struct BigRead {
   uint64_t h0;      // first hash slot
   uint64_t hmask;   // hash slots - 1
   uint64_t bm0;     // grouped mode: first word of the born | killed group bitmaps
+  uint64_t gchunk0; // k_big_run's reads: first chunk in its chunk space
   uint32_t G;       // grouped mode: the key's groups (chunked token-group view)
   uint32_t grouped;
 };
@@ -137,9 +138,11 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
     x.r = r, x.off0 = off0, x.off1 = off1, x.chunk0 = 0, x.rec0 = 0, x.cap = cap, x.h0 = 0, x.hmask = 2 * cap - 1;
     x.bm0 = 0, x.G = G, x.grouped = grouped ? 1u : 0u;
     br[b] = x;
-    sz[b] = nch;
+    const bool run = grouped || TYPE == AM_BCOUNTER;  // k_big_run's reads (its own chunk space)
+    sz[b] = run ? 0 : nch;
     sz[(uint64_t)nbig + b] = cap;
     sz[2 * (uint64_t)nbig + b] = grouped ? 2 * (uint64_t)((G + 31) / 32) : 0;
+    sz[3 * (uint64_t)nbig + b] = run ? nch : 0;
     BigAcc a;
     a.count = a.flags = a.pres = a.nbirth = a.nkill = a.pad0 = 0;
     a.min_excl = NONE;
@@ -148,14 +151,15 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
   }
 }
 
-// one workgroup of 1024: exclusive scans of chunks, caps and bitmap words; totals[0..2]
+// one workgroup of 1024: exclusive scans of chunks, caps, bitmap words and grouped-mode
+// chunks; totals[0..3]
 __global__ void __launch_bounds__(1024) k_big_offsets(const uint32_t *nbig_p, BigRead *br, const uint64_t *sz,
                                                       uint64_t *totals) {
   __shared__ uint64_t part[1024];
   const uint32_t nbig = *nbig_p, tid = threadIdx.x;
   const uint32_t per = (nbig + 1023) / 1024;
   const uint32_t b0 = tid * per < nbig ? tid * per : nbig, b1 = b0 + per < nbig ? b0 + per : nbig;
-  for (int f = 0; f < 3; ++f) {
+  for (int f = 0; f < 4; ++f) {
     const uint64_t *v = sz + (uint64_t)f * nbig;
     uint64_t s = 0;
     for (uint32_t b = b0; b < b1; ++b) s += v[b];
@@ -171,7 +175,8 @@ __global__ void __launch_bounds__(1024) k_big_offsets(const uint32_t *nbig_p, Bi
     for (uint32_t b = b0; b < b1; ++b) {
       if (f == 0) br[b].chunk0 = run;
       else if (f == 1) br[b].rec0 = run, br[b].h0 = 2 * run;
-      else br[b].bm0 = run;
+      else if (f == 2) br[b].bm0 = run;
+      else br[b].gchunk0 = run;
       run += v[b];
     }
     if (tid == 1023) totals[f] = part[1023];
@@ -344,9 +349,6 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
 
     if (tid < 8) s.ctr[tid] = 0;
     constexpr bool MVH = TYPE == AM_MVREG;
-    const bool grouped = TYPE == AM_MVREG && R0.grouped;  // the chunk's inclusion bits, then records
-    uint32_t *sincl = reinterpret_cast<uint32_t *>(s.lb_p);
-    if (grouped && tid < CHUNK / 32) sincl[tid] = 0;
     if (MVH)
       for (uint32_t i = tid; i < LK; i += BLOCK) s.lk_a[i] = HKEY_EMPTY, s.lk_p[i] = (int32_t)0x80000000;
     ChunkSink sink{&s, G, acc, R0.rec0, MVH};
@@ -401,10 +403,6 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
           if (eval_op<DMAX, true>(u, (meta4 >> (8 * k)) & 0xFFu, ct[k], sv[k], sp[k], txm, p, a)) ib |= 1u << k;
         }
       }
-      if (grouped) {
-        if (ib) atomicOr(&sincl[(uint32_t)(g - lo) >> 5], ib << ((uint32_t)(g - lo) & 31u));
-        ib = 0;
-      }
 #pragma unroll
       for (int k = 0; k < OPL; ++k) {
         if (!((ib >> k) & 1u)) continue;
@@ -445,11 +443,6 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
         if (d < (int)nd && mx[d]) atomicMax(&acc->mx[d], (unsigned long long)mx[d]);
     }
 
-    if (TYPE == AM_MVREG && grouped) {  // grouped mode: the chunk's records -> group bitmaps
-      grouped_records(L, B.key[r], R0, lo, hi, sincl, reinterpret_cast<uint32_t *>(s.lk_a), G.bm + R0.bm0, tid);
-      __syncthreads();
-      continue;
-    }
     if (TYPE == AM_BCOUNTER) {  // flush the chunk's slot sums into the read's global slots
       for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
         const uint64_t q = (uint64_t)b * SL.ns + i;
@@ -506,6 +499,141 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
     }
     __syncthreads();
   }
+}
+
+// ---- runs of chunks: grouped-mode MV reads and bounded-counter reads.  A workgroup takes a
+//      contiguous run of 1024-op chunks, so a read's partials stay on the workgroup across its
+//      chunks -- the scalar partials in registers, the bounded counter's slot sums in LDS --
+//      and reach the read's accumulators once per read and workgroup (k_big_chunk reduces and
+//      flushes every chunk).  LDS holds only what the type needs: MV the two hash sets, the
+//      bounded counter its slot sums (k_big_chunk's 64 KB allow two workgroups per CU). ----
+template <int DMAX, int TYPE, bool PACKED>
+__global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
+                                                   const BigRead *br, BigAcc *accs, uint32_t *bm, BigSlots SL,
+                                                   uint64_t n_gch) {
+  constexpr uint32_t NS = (uint32_t)(DMAX * DMAX + DMAX);
+  constexpr size_t HB = TYPE == AM_MVREG ? 2 * GH * 4 : (size_t)NS * 20;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[HB];
+  uint32_t *hs = reinterpret_cast<uint32_t *>(lds);  // MV: hash sets
+  uint64_t *slo = reinterpret_cast<uint64_t *>(lds);  // bounded counter: 128-bit slot sums + presence
+  int64_t *shi = reinterpret_cast<int64_t *>(lds + (size_t)NS * 8);
+  uint32_t *spres = reinterpret_cast<uint32_t *>(lds + (size_t)NS * 16);
+  __shared__ uint32_t incl[CHUNK / 32];
+  __shared__ uint64_t red[BLOCK / WAVE][DMAX + 4];
+  const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+  const uint32_t nbig = uniform_u32(*nbig_p);
+  const uint64_t n = B.n_reads;
+  const uint32_t nd = L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint64_t per = (n_gch + gridDim.x - 1) / gridDim.x;
+  const uint64_t x0 = (uint64_t)blockIdx.x * per < n_gch ? (uint64_t)blockIdx.x * per : n_gch;
+  const uint64_t x1 = x0 + per < n_gch ? x0 + per : n_gch;
+  uint32_t cur = 0xFFFFFFFFu;
+  BigRead R0{};
+  ReadU<DMAX> u;
+  PkRead<DMAX> pk;
+  AccP<DMAX> ap;
+  Acc<DMAX> a;
+  // the read's partials -> its accumulators (one LDS round over the waves)
+  auto flush = [&]() {
+    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
+    const uint32_t cnt = wave_sum_u32(a.count), fl = wave_or_u32(a.flags), pr = wave_or_u32(a.pres);
+    const uint64_t mn = wave_min_u64(a.min_excl);
+    uint64_t mx[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? wave_max_u64(a.mx[d]) : 0;
+    if (lane == 0) {
+      red[wv][0] = cnt, red[wv][1] = fl, red[wv][2] = pr, red[wv][3] = mn;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) red[wv][4 + d] = mx[d];
+    }
+    __syncthreads();
+    if (tid < 4 + (uint32_t)DMAX) {
+      uint64_t v = red[0][tid];
+      for (uint32_t w = 1; w < BLOCK / WAVE; ++w) {
+        const uint64_t y = red[w][tid];
+        v = tid == 0 ? v + y : (tid <= 2 ? (v | y) : tid == 3 ? (v < y ? v : y) : (v > y ? v : y));
+      }
+      BigAcc *acc = accs + cur;
+      if (tid == 0 && v) atomicAdd(&acc->count, (uint32_t)v);
+      if (tid == 1 && v) atomicOr(&acc->flags, (uint32_t)v);
+      if (tid == 2 && v) atomicOr(&acc->pres, (uint32_t)v);
+      if (tid == 3 && v != NONE) atomicMin(&acc->min_excl, (unsigned long long)v);
+      if (tid >= 4 && tid - 4 < nd && v) atomicMax(&acc->mx[tid - 4], (unsigned long long)v);
+    }
+    if (TYPE == AM_BCOUNTER) {  // the slot sums -> the read's global slots, then cleared
+      for (uint32_t i = tid; i < SL.ns; i += BLOCK) {
+        const uint64_t q = (uint64_t)cur * SL.ns + i;
+        if (slo[i] || shi[i]) acc128_atomic(&SL.lo[q], &SL.hi[q], shi[i], slo[i]);
+        if (spres[i]) atomicOr(&SL.pres[q], 1u);
+        slo[i] = 0, shi[i] = 0, spres[i] = 0;
+      }
+    }
+    __syncthreads();
+  };
+  if (TYPE == AM_BCOUNTER) {
+    for (uint32_t i = tid; i < SL.ns; i += BLOCK) slo[i] = 0, shi[i] = 0, spres[i] = 0;
+    __syncthreads();
+  }
+  for (uint64_t x = x0; x < x1; ++x) {
+    const uint32_t b = find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
+    if (b != cur) {
+      if (cur != 0xFFFFFFFFu) flush();
+      cur = b;
+      R0 = br[b];
+      const uint64_t r = R0.r;
+      u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+      const uint64_t rstride = B.per_read_clock ? n : 1, ridx = B.per_read_clock ? r : 0;
+      u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
+      u.base_ignore = !B.base_ignore || B.base_ignore[r];
+      u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+        u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+      }
+      u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+      u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+      if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[r])]), pk);
+      ap.reset();
+      a.reset();
+    }
+    const uint64_t t0 = R0.off0 & ~(uint64_t)(OPL - 1), c = x - R0.gchunk0;
+    const uint64_t lo = t0 + c * CHUNK, hi = lo + CHUNK < R0.off1 ? lo + CHUNK : R0.off1;
+    const uint64_t g = lo + (uint64_t)tid * OPL;
+    if (TYPE == AM_BCOUNTER) {  // included ops -> LDS slot sums (orddict:update_counter)
+      if (g < hi) {
+        const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
+        const uint32_t ib = incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
+#pragma unroll
+        for (int k = 0; k < OPL; ++k) {
+          if (!((ib >> k) & 1u)) continue;
+          const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
+          if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
+          uint32_t slot;
+          int64_t v;
+          if (!bc_slot(L, g + k, meta, nd, slot, v)) {
+            a.flags |= FLAG_BAD;
+            continue;
+          }
+          acc128_atomic(&slo[slot], &shi[slot], v < 0 ? -1 : 0, (uint64_t)v);
+          atomicOr(&spres[slot], 1u);
+        }
+      }
+      continue;  // the slot sums stay in LDS until the read's flush
+    }
+    for (uint32_t i = tid; i < 2 * GH; i += BLOCK) hs[i] = GH_EMPTY;
+    if (tid < CHUNK / 32) incl[tid] = 0;
+    __syncthreads();
+    if (g < hi) {
+      const uint32_t ib = incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
+      if (ib) atomicOr(&incl[(uint32_t)(g - lo) >> 5], ib << ((uint32_t)(g - lo) & 31u));
+    }
+    __syncthreads();
+    grouped_records(L, B.key[R0.r], R0, lo, hi, incl, hs, bm + R0.bm0, tid);
+    __syncthreads();
+  }
+  if (cur != 0xFFFFFFFFu) flush();
 }
 
 // ---- births -> hash on the kill key ----
@@ -708,7 +836,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch
 template <int DMAX, int TYPE>
 int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, const uint32_t *list,
             const uint32_t *nbig_d, uint32_t nbig, BigRead *br, BigAcc *acc, BigRec G, BigSlots SL,
-            uint64_t n_chunks, uint64_t n_rec) {
+            uint64_t n_chunks, uint64_t n_rec, uint64_t n_gch) {
   const uint32_t cap = (uint32_t)ctx->n_cu * 2;
   static bool attr = false;
   if (!attr) {
@@ -719,13 +847,26 @@ int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_res
     attr = true;
   }
   const unsigned g1 = (unsigned)(n_chunks < cap ? n_chunks : cap);
-  if (am_log_packed(L))  // the packed view: u32 commit vectors (4 * n_dc bytes per op, not 8 + 8 * n_dc)
-    hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE, true>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L, *B,
-                       nbig_d, br, acc, G, SL, n_chunks);
-  else
-    hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE, false>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L, *B,
-                       nbig_d, br, acc, G, SL, n_chunks);
-  AM_HIP(hipGetLastError());
+  if (g1) {
+    if (am_log_packed(L))  // the packed view: u32 commit vectors (4 * n_dc bytes per op, not 8 + 8 * n_dc)
+      hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE, true>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L,
+                         *B, nbig_d, br, acc, G, SL, n_chunks);
+    else
+      hipLaunchKernelGGL((k_big_chunk<DMAX, TYPE, false>), dim3(g1), dim3(BLOCK), sizeof(ChunkSmem), ctx->stream, *L,
+                         *B, nbig_d, br, acc, G, SL, n_chunks);
+    AM_HIP(hipGetLastError());
+  }
+  if constexpr (TYPE != AM_AWSET) if (n_gch) {  // runs of chunks: grouped MV reads, bounded-counter reads
+    const uint64_t gcap = (uint64_t)ctx->n_cu * 8;
+    const unsigned g4 = (unsigned)(n_gch < gcap ? n_gch : gcap);
+    if (am_log_packed(L))
+      hipLaunchKernelGGL((k_big_run<DMAX, TYPE, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br, acc,
+                         G.bm, SL, n_gch);
+    else
+      hipLaunchKernelGGL((k_big_run<DMAX, TYPE, false>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br,
+                         acc, G.bm, SL, n_gch);
+    AM_HIP(hipGetLastError());
+  }
   if (TYPE != AM_BCOUNTER) {
     const uint64_t eg = (n_rec + 255) / 256;
     const unsigned g2 = (unsigned)(eg < (uint64_t)ctx->n_cu * 16 ? eg : (uint64_t)ctx->n_cu * 16);
@@ -753,7 +894,7 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   SL.ns = TYPE == AM_BCOUNTER ? L->n_dc * L->n_dc + L->n_dc : 0;
   const size_t o_acc = am_round_up((size_t)nbig * sizeof(BigRead), 256);
   const size_t o_sz = o_acc + am_round_up((size_t)nbig * sizeof(BigAcc), 256);
-  const size_t o_tot = o_sz + am_round_up((size_t)nbig * 24, 256);
+  const size_t o_tot = o_sz + am_round_up((size_t)nbig * 32, 256);
   const size_t o_slo = o_tot + 256, nsl = (size_t)nbig * SL.ns;
   const size_t o_shi = o_slo + am_round_up(nsl * 8, 256), o_spr = o_shi + am_round_up(nsl * 8, 256);
   void *meta = nullptr;
@@ -772,10 +913,10 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   AM_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_big_offsets, dim3(1), dim3(1024), 0, ctx->stream, retry.count, br, sz, tot);
   AM_HIP(hipGetLastError());
-  uint64_t t3[3];
-  rc = am_ctx_fetch(ctx, tot, 3, t3);
+  uint64_t t4[4];
+  rc = am_ctx_fetch(ctx, tot, 4, t4);
   if (rc) return rc;
-  const uint64_t n_chunks = t3[0], n_rec = t3[1], n_bm = t3[2];
+  const uint64_t n_chunks = t4[0], n_rec = t4[1], n_bm = t4[2], n_gch = t4[3];
   // records: births (a, b, p, sub, dead), kills (a, b, p) -- n_rec each; hash 2*n_rec
   // slots; the finish pass's AW token / index scratch -- n_rec each
   const size_t rb = am_round_up(n_rec * 8, 256), r4 = am_round_up(n_rec * 4, 256), r1 = am_round_up(n_rec, 256);
@@ -801,7 +942,8 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   AM_HIP(hipMemsetAsync(G.dead, 0, n_rec, ctx->stream));
   AM_HIP(hipMemsetAsync(G.H, 0xFF, 2 * n_rec * 4, ctx->stream));
   const uint32_t nd = L->n_dc;
-#define AM_B(D) return run_big<D, TYPE>(ctx, L, B, R, retry.list, retry.count, nbig, br, acc, G, SL, n_chunks, n_rec);
+#define AM_B(D) \
+  return run_big<D, TYPE>(ctx, L, B, R, retry.list, retry.count, nbig, br, acc, G, SL, n_chunks, n_rec, n_gch);
   if (nd <= 1) AM_B(1)
   if (nd <= 2) AM_B(2)
   if (nd <= 3) AM_B(3)

@@ -575,6 +575,7 @@ struct GrpHint {
   uint32_t *pg;
   int64_t shift;       // pool word of result word o
   uint8_t *done;       // [read] its words are in the pool
+  unsigned long long *skipped;  // AM_STAT_OPS_SKIPPED (am_ctx_stat)
   __device__ __forceinline__ void put(uint64_t o, uint64_t a, uint64_t b, uint32_t g) const {
     if (pa) {
       const uint64_t q = (uint64_t)((int64_t)o + shift);
@@ -719,6 +720,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
   const uint64_t gw = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6);
   ReadU<DMAX> u;
   if (!GENERAL) read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
+  uint64_t n_skipped = 0;  // ops of zones inside a base snapshot (uniform)
   PH_DECL();
   PH_BEGIN();
 
@@ -791,8 +793,25 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       ap.reset();
       a.reset();
       bool esc = false;  // some op of this lane did not fit the packed view
+      // zone map: with a base snapshot (and no TxId), a tile whose zones are vectorclock:le the
+      // base clock holds no candidate (belongs_to_snapshot_op/3) -- not streamed
+      const bool zskip = GENERAL && L.zone_vc && !u.base_ignore && !u.has_txid;
+      const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
       for (uint64_t t = t0; t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
+        if (zskip) {
+          const uint64_t te = t + TILE < off1 ? t + TILE : off1;
+          bool in_base = true;
+          for (uint64_t z = t / AM_ZONE_OPS; z <= (te - 1) / AM_ZONE_OPS; ++z)
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d)
+              if (d < (int)nd) in_base &= L.zone_vc[(uint64_t)d * nz + z] <= u.C0[d];
+          if (in_base) {
+            if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = 0u;
+            n_skipped += te - (t > off0 ? t : off0);
+            continue;
+          }
+        }
         const uint32_t ib =
             g < off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, off0, off1, stride, ap, a, esc) : 0u;
         uint32_t word = ib << (OPL * (lane % LPW));
@@ -913,6 +932,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
     }
     wave_sync();  // the slots are rewritten by the next batch
   }
+  if (GENERAL && n_skipped && lane == 0) atomicAdd(H.skipped, (unsigned long long)n_skipped);
   PH_END();
 }
 
@@ -1098,7 +1118,8 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     if (blocks == 0) return AM_OK;
     hipLaunchKernelGGL((k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), smem,
                        ctx->stream, *L, *B, *R, S, next, short_opl, GrpHint{ctx->grp_hint_in, ctx->tee_a, ctx->tee_b, ctx->tee_g, ctx->tee_shift,
-                                                                  ctx->tee_done});
+                                                                  ctx->tee_done,
+                                                                  (unsigned long long *)(ctx->stats + AM_STAT_OPS_SKIPPED)});
   } else if (tier == AM_GRP_ROW) {
     static int occ = 0;
     if (!occ) {

@@ -23,6 +23,7 @@ struct am_ctx {
   void *scratch[AM_N_SCR] = {};  // grow-only device scratch slots (planner, row/group hand-offs, big-read path)
   size_t scratch_bytes[AM_N_SCR] = {};
   uint64_t *pinned = nullptr;    // small pinned host buffer for device -> host counters
+  uint64_t *stats = nullptr;     // device counters (am_ctx_stat: AM_STAT_*)
   // Device blocks of destroyed stores / caches kept for reuse by am_dev_alloc (a rebuilt
   // store -- am_store_update every GC round -- asks for the same column sizes again), by
   // size; block sizes of every am_dev_alloc block.  Reuse is stream-ordered: every kernel
@@ -147,7 +148,7 @@ bool am_bcrows_applies(const am_op_log *L, const am_read_batch *B, const am_read
 int am_launch_bcrows(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                      am_retry next);
 // Bounded-counter wave tier (am_bcwave.hip): one wave per read with LDS slot sums, reads
-// up to 32768 ops over the packed view (n_dc <= 16); the rest go to `next`.
+// up to 4096 ops over the packed view (n_dc <= 16); the rest go to `next`.
 bool am_bcwave_applies(const am_op_log *L, const am_read_result *R);
 int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                      am_retry next);

@@ -126,6 +126,31 @@ __global__ void k_rec_key_off(const uint64_t *key_off, const uint64_t *key_end, 
   }
 }
 
+// the zone map (include/antidote_mat.h zone_vc): one wave per block of AM_ZONE_OPS op slots,
+// the max of every op's commit vector X per DC (X[commit dc] = commit_time; a snapshot entry
+// the op does not carry reads as 0, as in is_op_in_snapshot/7)
+__global__ void k_zone(am_op_log L, uint64_t *zone, uint64_t nz) {
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  for (uint64_t z = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; z < nz; z += waves) {
+    uint64_t mx[AM_MAX_DC];
+    for (uint32_t d = 0; d < L.n_dc; ++d) mx[d] = 0;
+    for (uint64_t p = z * AM_ZONE_OPS + lane; p < (z + 1) * AM_ZONE_OPS && p < L.n_ops; p += WAVE) {
+      const uint32_t dc = AM_META_DC(L.op_meta[p]);
+      const uint32_t sp = L.snap_pres ? L.snap_pres[p] : 0xFFFFFFFFu;
+      for (uint32_t d = 0; d < L.n_dc; ++d) {
+        const uint64_t x = d == dc ? L.commit_time[p] : (((sp >> d) & 1u) ? L.snap_vc[(uint64_t)d * stride + p] : 0);
+        mx[d] = x > mx[d] ? x : mx[d];
+      }
+    }
+    for (uint32_t d = 0; d < L.n_dc; ++d) {
+      const uint64_t m = wave_max_u64(mx[d]);
+      if (lane == 0) zone[(uint64_t)d * nz + z] = m;
+    }
+  }
+}
+
 struct MaxOp {
   __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
 };
@@ -233,10 +258,31 @@ int build_records(am_store *st) {
   return AM_OK;
 }
 
+// the zone map of a device store (every op column written)
+int build_zones(am_store *st) {
+  am_ctx *c = st->ctx;
+  am_op_log &d = st->dev;
+  if (!d.commit_time || !d.op_meta || !d.n_ops || (d.n_dc && !d.snap_vc)) return AM_OK;
+  const uint64_t stride = d.snap_stride ? d.snap_stride : d.n_ops;
+  const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
+  void *zb = nullptr;
+  if (int rc = am_dev_alloc(c, (size_t)d.n_dc * nz * 8 + 8, &zb)) return rc;
+  st->allocs.push_back(zb);
+  const uint64_t blocks = (nz + 3) / 4 < 65536 ? (nz + 3) / 4 : 65536;
+  hipLaunchKernelGGL(k_zone, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz);
+  AM_HIP(hipGetLastError());
+  d.zone_vc = (const uint64_t *)zb;
+  return AM_OK;
+}
+
 }  // namespace
 
-// the record view only, for a store whose packed view was written by its builder (am_gc.hip)
-int am_store_pack_records(am_store *st) { return build_records(st); }
+// the record view and zone map, for a store whose packed view was written by its builder
+// (am_gc.hip)
+int am_store_pack_records(am_store *st) {
+  if (int rc = build_records(st)) return rc;
+  return build_zones(st);
+}
 
 int am_store_pack(am_store *st) {
   am_ctx *c = st->ctx;
@@ -245,7 +291,10 @@ int am_store_pack(am_store *st) {
   // the packed view assumes full clocks (snap_pres NULL) and padded columns (16-byte loads);
   // the token-group view is built either way
   if (!d.commit_time || !d.op_meta || (d.n_ops && !d.snap_vc)) return AM_OK;
-  if (stride % 4 || d.snap_pres) return build_records(st);
+  if (stride % 4 || d.snap_pres) {
+    if (int rc = build_records(st)) return rc;
+    return build_zones(st);
+  }
   void *tb = nullptr, *pk = nullptr;
   int rc = am_dev_alloc(c, d.n_keys * 8 + 8, &tb);
   if (rc) return rc;
@@ -263,5 +312,6 @@ int am_store_pack(am_store *st) {
   AM_HIP(hipStreamSynchronize(c->stream));
   d.key_tbase = (const uint64_t *)tb;
   d.pk_vc = (const uint32_t *)pk;
-  return build_records(st);
+  if (int rc = build_records(st)) return rc;
+  return build_zones(st);
 }

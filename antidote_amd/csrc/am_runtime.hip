@@ -37,6 +37,8 @@ int am_ctx_open(int device, am_ctx **out) {
   AM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   AM_HIP(hipEventCreate(&c->ev0));
   AM_HIP(hipEventCreate(&c->ev1));
+  AM_HIP(hipMalloc((void **)&c->stats, 8 * sizeof(uint64_t)));
+  AM_HIP(hipMemsetAsync(c->stats, 0, 8 * sizeof(uint64_t), c->stream));
   *out = c;
   return AM_OK;
 }
@@ -50,6 +52,7 @@ int am_ctx_close(am_ctx *c) {
   for (auto &kv : c->free_blocks) (void)hipFree(kv.second);
   c->free_blocks.clear();
   if (c->pinned) (void)hipHostFree(c->pinned), c->pinned = nullptr;
+  if (c->stats) (void)hipFree(c->stats), c->stats = nullptr;
   (void)hipEventDestroy(c->ev0);
   (void)hipEventDestroy(c->ev1);
   (void)hipStreamDestroy(c->stream);
@@ -63,6 +66,15 @@ int am_ctx_sync(am_ctx *c) {
   if (!c) return AM_ERR_INVALID;
   AM_LOCK(c);
   AM_HIP(hipStreamSynchronize(c->stream));
+  return AM_OK;
+}
+
+int am_ctx_stat(am_ctx *c, int which, uint64_t *value, int reset) {
+  if (!c || !value || which != AM_STAT_OPS_SKIPPED) return AM_ERR_INVALID;
+  AM_LOCK(c);
+  AM_HIP(hipSetDevice(c->device));
+  if (int rc = am_ctx_fetch(c, c->stats + which, 1, value)) return rc;
+  if (reset) AM_HIP(hipMemsetAsync(c->stats + which, 0, sizeof(uint64_t), c->stream));
   return AM_OK;
 }
 

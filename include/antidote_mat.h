@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 6
+#define AM_ABI_VERSION 7
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -205,7 +205,17 @@ typedef struct am_op_log {
    * kills (bits 32-63) -- the key's records folded per op, so a short read ORs one word per
    * included op instead of testing records; 0 for every other op.  NULL in host logs. */
   const uint64_t *gmask;       /* [n_ops] or NULL                                    */
+  /* Zone map (device stores, NULL in host logs): per block z of AM_ZONE_OPS consecutive op
+   * slots [z * AM_ZONE_OPS, (z + 1) * AM_ZONE_OPS) of the columns, zone_vc[d * n_zones + z] >=
+   * X[d] of every op in the block (X = the commit vector is_op_in_snapshot/7 compares;
+   * n_zones = ceil(snap_stride or n_ops / AM_ZONE_OPS)).  An upper bound, kept by every writer
+   * (a GC may leave it above the surviving ops).  A read with a base snapshot skips a block
+   * whose bound is vectorclock:le the base clock: none of its ops is a candidate
+   * (belongs_to_snapshot_op/3), so none counts, none is applied and none bounds NewLastOp --
+   * the ops already folded into the cached snapshot are not streamed again. */
+  const uint64_t *zone_vc;
 } am_op_log;
+#define AM_ZONE_OPS 256u
 #define AM_GMASK_MAX_GRP 32u
 #define AM_REC_KILL (1u << 16)
 #define AM_REC_OP(m) ((m) & 0xFFFFu)
@@ -303,6 +313,11 @@ int am_ctx_sync(am_ctx *ctx);
 const char *am_last_error(void);            /* thread-local message of the last failure */
 int am_timer_start(am_ctx *ctx);             /* hipEventRecord on the ctx stream         */
 int am_timer_stop(am_ctx *ctx, float *ms);   /* records, syncs, returns elapsed ms       */
+/* Counters of the context's kernels (synchronizes the stream): AM_STAT_OPS_SKIPPED = ops whose
+ * commit vectors a read did not stream because their zone is inside its base snapshot
+ * (am_op_log.zone_vc).  reset != 0 zeroes the counter after reading it. */
+#define AM_STAT_OPS_SKIPPED 0
+int am_ctx_stat(am_ctx *ctx, int which, uint64_t *value, int reset);
 
 /* ---- device memory helpers (the NIF owns no framework allocator) ---- */
 int am_dev_alloc(am_ctx *ctx, size_t bytes, void **out);

@@ -1,0 +1,84 @@
+"""The zone map (am_op_log.zone_vc: per 256-op block an upper bound of the ops' commit
+vectors) lets a read with a cached base skip the blocks inside its base snapshot
+(belongs_to_snapshot_op/3: none of their ops is a candidate).  Reads through the device
+snapshot cache at rising snapshot times, against the oracle's internal_read/7; the context
+counter shows blocks were skipped.  Bar: bit-exact read values and statuses."""
+import ctypes
+import random
+
+import pytest
+
+from antidote_amd import abi
+from antidote_amd.oplog import HostLog, Read
+from oracle import ref_materializer as R
+from tests import randlog
+from tests.test_gpu_snapcache import _oracle_state
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mat():
+    from antidote_amd.materializer import Materializer
+    m = Materializer(0)
+    yield m
+    m.close()
+
+
+def _skipped(mat, reset=True):
+    v = ctypes.c_uint64()
+    abi.check(mat.L.am_ctx_stat(mat.ctx, abi.AM_STAT_OPS_SKIPPED, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
+    return v.value
+
+
+@pytest.mark.parametrize("t", [abi.AM_AWSET, abi.AM_MVREG])
+@pytest.mark.parametrize("n_dc", [2, 8])
+def test_gpu_zone_skip_cached_reads(mat, t, n_dc):
+    rng = random.Random(4400 + 31 * t + n_dc)
+    n_keys = 24
+    keys = [randlog.rand_key_ops(rng, t, n_dc, rng.choice([0, 40, 300, 700, 1000])) for _ in range(n_keys)]
+    types = [t] * n_keys
+    log = HostLog(n_dc, keys, key_types=types)
+    store = mat.store(log)
+    cache = mat.snapshot_cache(store, n_keys)
+    st = _oracle_state(keys, types)
+    hi = [ops[-1].commit_time if ops else 20 for ops in keys]
+    _skipped(mat)
+    try:
+        for q in (0.3, 0.55, 0.8, 1.0, 1.2):
+            reads = []
+            for k in range(n_keys):
+                c = int(10 + (hi[k] - 10) * q)
+                reads.append(Read(k, t, {d: c + rng.randint(0, 3) for d in range(n_dc)}))
+            got = cache.read(reads, set_capacity=[4096] * n_keys)
+            for i, rd in enumerate(reads):
+                try:
+                    ref = R.internal_read(rd.key, rd.type, dict(rd.clock), R.IGNORE, False, st)
+                except R.LogColdPath:
+                    ref = ("cold",)
+                g = got.result(i)
+                if ref[0] == "cold":
+                    assert g == ("error", abi.AM_ERR_COLD_PATH), (q, rd.key, g)
+                elif ref[0] == "error":
+                    assert g[0] == "error", (q, rd.key, g, ref)
+                else:
+                    assert g[0] == "ok" and g[1] == randlog.canon_state(t, ref[1]), (q, rd.key, g, ref)
+        assert _skipped(mat) > 0  # the later rounds' bases cover whole blocks
+    finally:
+        cache.close()
+        store.close()
+
+
+def test_gpu_zone_no_skip_without_base(mat):
+    """Fresh reads (base ignore) stream every op: the counter stays at zero."""
+    rng = random.Random(4500)
+    keys = [randlog.rand_key_ops(rng, abi.AM_AWSET, 3, 800) for _ in range(4)]
+    log = HostLog(3, keys, key_types=[abi.AM_AWSET] * 4)
+    st = mat.store(log)
+    _skipped(mat)
+    try:
+        hi = max(ops[-1].commit_time for ops in keys)
+        mat.read_batch(st, [Read(k, abi.AM_AWSET, {d: hi for d in range(3)}) for k in range(4)], [4096] * 4)
+        assert _skipped(mat) == 0
+    finally:
+        st.close()
