@@ -797,15 +797,39 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       // base clock holds no candidate (belongs_to_snapshot_op/3) -- not streamed
       const bool zskip = GENERAL && L.zone_vc && !u.base_ignore && !u.has_txid;
       const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
+      // the read's zones in one round of loads: lane (d, z) tests zone z of DC d against the
+      // base clock; a zone is inside the base when every DC's lane passes (reads spanning more
+      // zones than a wave holds test per tile)
+      uint64_t zin = 0;  // bit z - zb: zone z inside the base
+      const uint64_t zb = t0 / AM_ZONE_OPS, nzr = (zskip && off1 > t0) ? (off1 - 1) / AM_ZONE_OPS - zb + 1 : 0;
+      const bool zbatch = zskip && nzr * nd <= (uint64_t)WAVE;
+      if (zbatch) {
+        const uint32_t dl = lane / (uint32_t)nzr, zl = lane % (uint32_t)nzr;
+        bool ok = true;
+        if (dl < nd) {
+          uint64_t c0 = 0;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) c0 = (uint32_t)d == dl ? u.C0[d] : c0;
+          ok = L.zone_vc[(uint64_t)dl * nz + zb + zl] <= c0;
+        }
+        const uint64_t okm = __ballot(ok);
+        zin = nzr >= 64 ? ~0ull : ((1ull << nzr) - 1ull);
+        for (uint32_t d = 0; d < nd; ++d) zin &= okm >> (d * nzr);
+      }
       for (uint64_t t = t0; t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
         if (zskip) {
           const uint64_t te = t + TILE < off1 ? t + TILE : off1;
+          const uint64_t z0 = t / AM_ZONE_OPS, z1 = (te - 1) / AM_ZONE_OPS;
           bool in_base = true;
-          for (uint64_t z = t / AM_ZONE_OPS; z <= (te - 1) / AM_ZONE_OPS; ++z)
+          if (zbatch) {
+            for (uint64_t z = z0; z <= z1; ++z) in_base &= (zin >> (z - zb)) & 1ull;
+          } else {
+            for (uint64_t z = z0; z <= z1; ++z)
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d)
-              if (d < (int)nd) in_base &= L.zone_vc[(uint64_t)d * nz + z] <= u.C0[d];
+              for (int d = 0; d < DMAX; ++d)
+                if (d < (int)nd) in_base &= L.zone_vc[(uint64_t)d * nz + z] <= u.C0[d];
+          }
           if (in_base) {
             if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = 0u;
             n_skipped += te - (t > off0 ? t : off0);

@@ -18,7 +18,8 @@
 //                  (vectorclock:min over them) is emitted for prune_ops (am_store_update)
 //   k_sc_release   frees the key claims
 // Layout: per key a fixed array of CAP entries, newest first (clock [n_dc] + presence,
-// last_op_id, value).  Scalar values (PN counter, LWW register) live in the entry; set
+// last_op_id, value), entry-major: field[e][key] (clocks [e][d][key]), so a batch's reads of
+// consecutive keys touch consecutive words of every field.  Scalar values (PN counter, LWW register) live in the entry; set
 // values (add-wins set / MV register pairs) and bounded-counter (slot, value) entries live in
 // a value pool (pool_a / pool_b words, bump-allocated, compacted on the host side when a batch
 // could overflow it) that the next read's base points into (base.set_off/set_len), so a
@@ -37,14 +38,14 @@ struct am_snapcache {
   uint64_t n_keys = 0;
   uint8_t *cnt = nullptr;      // [n_keys] entries; ABSENT: no snapshot dict yet
   uint32_t *owner = nullptr;   // [n_keys] batch claim (~0: free)
-  uint64_t *vc = nullptr;      // [n_keys][CAP][n_dc]
-  uint32_t *pres = nullptr;    // [n_keys][CAP]
-  int64_t *last_op = nullptr;  // [n_keys][CAP]
-  int64_t *v0 = nullptr;       // [n_keys][CAP]
-  uint64_t *v1 = nullptr;      // [n_keys][CAP]
-  uint8_t *vflag = nullptr;    // [n_keys][CAP]
-  uint64_t *poff = nullptr;    // [n_keys][CAP] value words in the pool
-  uint32_t *plen = nullptr;    // [n_keys][CAP]
+  uint64_t *vc = nullptr;      // [CAP][n_dc][n_keys]
+  uint32_t *pres = nullptr;    // [CAP][n_keys]
+  int64_t *last_op = nullptr;  // [CAP][n_keys]
+  int64_t *v0 = nullptr;       // [CAP][n_keys]
+  uint64_t *v1 = nullptr;      // [CAP][n_keys]
+  uint8_t *vflag = nullptr;    // [CAP][n_keys]
+  uint64_t *poff = nullptr;    // [CAP][n_keys] value words in the pool
+  uint32_t *plen = nullptr;    // [CAP][n_keys]
   uint64_t *pool_a = nullptr, *pool_b = nullptr;  // set pairs (a, b); bcounter slot values in a
   uint8_t *pool_p = nullptr;                      // bcounter slot presence
   uint32_t *pool_g = nullptr;                     // set pairs: token-group hint (am_ctx::grp_hint_in)
@@ -96,26 +97,31 @@ struct ScGc {
   uint32_t *thr_pres;
 };
 
-__device__ __forceinline__ uint64_t clk(const uint64_t *vc, uint32_t pres, uint32_t d) {
-  return ((pres >> d) & 1u) ? vc[d] : 0;
+// entry e of key k: its field index, its clock entry d (entry-major layout)
+__device__ __forceinline__ uint64_t ent(const ScView &C, uint32_t e, uint64_t k) { return (uint64_t)e * C.n_keys + k; }
+__device__ __forceinline__ uint64_t vci(const ScView &C, uint32_t e, uint64_t k, uint32_t d) {
+  return ((uint64_t)e * C.n_dc + d) * C.n_keys + k;
+}
+__device__ __forceinline__ uint64_t clk(const ScView &C, uint32_t e, uint64_t k, uint32_t pres, uint32_t d) {
+  return ((pres >> d) & 1u) ? C.vc[vci(C, e, k, d)] : 0;
 }
 
-// snapshot_insert_gc/4's prune threshold (src/materializer_vnode.erl:523-527) over the kept
-// entries [s0, s0 + keep) (newest first): Acc = the oldest kept clock, then for every entry
+// snapshot_insert_gc/4's prune threshold (src/materializer_vnode.erl:523-527) over key k's
+// kept entries [0, keep) (newest first): Acc = the oldest kept clock, then for every entry
 // newest -> oldest Acc = vectorclock:min([CT1, Acc]), i.e. each DC of CT1 lowered to
 // min(CT1[dc], Acc[dc]) with a DC missing from Acc read as 0 (a DC only in Acc keeps its entry;
 // oracle/ref_materializer.py vc_min2 gives the evidence for this rule).  Writes thr[d * stride]
 // (0 for absent DCs) and returns the presence mask.
-__device__ uint32_t gc_threshold(const ScView &C, uint64_t s0, uint32_t keep, uint64_t *thr, uint64_t stride) {
+__device__ uint32_t gc_threshold(const ScView &C, uint64_t k, uint32_t keep, uint64_t *thr, uint64_t stride) {
   const uint32_t nd = C.n_dc;
-  const uint64_t last = s0 + keep - 1;
+  const uint32_t last = keep - 1;
   uint32_t pres = 0;
   for (uint32_t d = 0; d < nd; ++d) {
-    bool have = (C.pres[last] >> d) & 1u;
-    uint64_t acc = have ? C.vc[last * nd + d] : 0;
+    bool have = (C.pres[ent(C, last, k)] >> d) & 1u;
+    uint64_t acc = have ? C.vc[vci(C, last, k, d)] : 0;
     for (uint32_t e = 0; e < keep; ++e) {
-      if (!((C.pres[s0 + e] >> d) & 1u)) continue;
-      const uint64_t a = C.vc[(s0 + e) * nd + d], b = have ? acc : 0;
+      if (!((C.pres[ent(C, e, k)] >> d) & 1u)) continue;
+      const uint64_t a = C.vc[vci(C, e, k, d)], b = have ? acc : 0;
       acc = a < b ? a : b;
       have = true;
     }
@@ -157,11 +163,10 @@ __global__ void k_sc_select(ScView C, am_read_batch B, ScSel S) {
       const uint32_t spres = B.read_pres[ridx] & all;
       const uint32_t ne = C.cnt[key];
       for (uint32_t e = 0; e < ne && sel == CAP; ++e) {  // vector_orddict:get_smaller: newest first
-        const uint64_t slot = key * CAP + e;
-        const uint32_t ep = C.pres[slot] & all;
+        const uint32_t ep = C.pres[ent(C, e, key)] & all;
         bool le = true;  // vectorclock:le(Entry, ReadClock): every DC of either, missing = 0
         for (uint32_t d = 0; d < nd && le; ++d) {
-          const uint64_t x = clk(C.vc + slot * nd, ep, d);
+          const uint64_t x = clk(C, e, key, ep, d);
           const uint64_t y = ((spres >> d) & 1u) ? B.read_vc[(uint64_t)d * rstride + ridx] : 0;
           le = x <= y;
         }
@@ -170,12 +175,12 @@ __global__ void k_sc_select(ScView C, am_read_batch B, ScSel S) {
       if (sel == CAP) {
         code = SEL_COLD;  // get_from_snapshot_log: the log path, not the cache
       } else {
-        const uint64_t slot = key * CAP + sel;
+        const uint64_t slot = ent(C, sel, key);
         code = SEL_CACHED;
         newest = sel == 0;
         bign = 0;
         bpres = C.pres[slot] & all;
-        for (uint32_t d = 0; d < nd; ++d) S.base_vc[(uint64_t)d * n + r] = clk(C.vc + slot * nd, bpres, d);
+        for (uint32_t d = 0; d < nd; ++d) S.base_vc[(uint64_t)d * n + r] = clk(C, sel, key, bpres, d);
         blast = C.last_op[slot];
         bv0 = C.v0[slot];
         bv1 = C.v1[slot];
@@ -236,11 +241,11 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
     }
     const uint64_t key = act ? B.key[r] : 0;
     const uint32_t t = act ? B.type[r] : 0u;
-    const uint64_t s0 = key * CAP;
+    const uint64_t s0 = key;  // entry 0 of the key (entry e: ent(C, e, key))
     uint32_t ne = act ? C.cnt[key] : 0u;
     if (act && code == SEL_NEW_DICT) {  // store_snapshot(TxId, Key, Empty, vectorclock:new(), false)
       C.pres[s0] = 0;
-      for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = 0;
+      for (uint32_t d = 0; d < nd; ++d) C.vc[vci(C, 0, key, d)] = 0;
       C.last_op[s0] = 0;
       C.v0[s0] = 0;
       C.v1[s0] = 0;
@@ -266,7 +271,7 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
       bool le = true;
       for (uint32_t d = 0; d < nd && le; ++d) {
         const uint64_t x = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
-        le = x <= clk(C.vc + s0 * nd, fp, d);
+        le = x <= clk(C, 0, key, fp, d);
       }
       ins = !le;
     }
@@ -291,8 +296,8 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
       const uint32_t keep = gc ? (grown < SMIN ? grown : SMIN) : grown;
       if (ins) {
         for (uint32_t e = keep - 1; e >= 1; --e) {  // shift right by one (newest first)
-          const uint64_t dst = s0 + e, src = s0 + e - 1;
-          for (uint32_t d = 0; d < nd; ++d) C.vc[dst * nd + d] = C.vc[src * nd + d];
+          const uint64_t dst = ent(C, e, key), src = ent(C, e - 1, key);
+          for (uint32_t d = 0; d < nd; ++d) C.vc[vci(C, e, key, d)] = C.vc[vci(C, e - 1, key, d)];
           C.pres[dst] = C.pres[src];
           C.last_op[dst] = C.last_op[src];
           C.v0[dst] = C.v0[src];
@@ -301,7 +306,7 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
           C.poff[dst] = C.poff[src];
           C.plen[dst] = C.plen[src];
         }
-        for (uint32_t d = 0; d < nd; ++d) C.vc[s0 * nd + d] = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
+        for (uint32_t d = 0; d < nd; ++d) C.vc[vci(C, 0, key, d)] = ((np >> d) & 1u) ? R.last_ct[(uint64_t)d * n + r] : 0;
         C.pres[s0] = np;
         C.last_op[s0] = nlo;
         C.v0[s0] = (t == AM_PN || t == AM_LWW) ? R.value.v0[r] : 0;
@@ -312,7 +317,7 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
       }
       C.cnt[key] = (uint8_t)keep;
       if (gc && G.mask) {  // the prune threshold over the kept entries
-        G.thr_pres[key] = gc_threshold(C, s0, keep, G.thr_vc + key, C.n_keys);
+        G.thr_pres[key] = gc_threshold(C, key, keep, G.thr_vc + key, C.n_keys);
         G.mask[key] = 1;
       }
     }
@@ -352,7 +357,7 @@ __global__ void k_sc_threshold(ScView C, uint8_t *mask, uint64_t *thr_vc, uint32
     const uint32_t cnt = C.cnt[k];
     const uint32_t m = (cnt == ABSENT) ? 0 : (cnt < SMIN ? cnt : SMIN);
     if (cnt != ABSENT) C.cnt[k] = (uint8_t)m;
-    thr_pres[k] = m ? gc_threshold(C, k * CAP, m, thr_vc + k, C.n_keys) : 0u;
+    thr_pres[k] = m ? gc_threshold(C, k, m, thr_vc + k, C.n_keys) : 0u;
     if (!m)
       for (uint32_t d = 0; d < C.n_dc; ++d) thr_vc[(uint64_t)d * C.n_keys + k] = 0;
     mask[k] = m ? 1 : 0;
@@ -363,7 +368,7 @@ __global__ void k_sc_threshold(ScView C, uint8_t *mask, uint64_t *thr_vc, uint32
 __global__ void k_pool_len(ScView C, uint64_t *len) {
   const uint64_t ne = C.n_keys * CAP;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = i / CAP, e = i % CAP;
+    const uint64_t k = i % C.n_keys, e = i / C.n_keys;
     const uint32_t cnt = C.cnt[k];
     len[i] = (cnt != ABSENT && e < cnt && C.poff[i]) ? C.plen[i] : 0;
   }
@@ -372,7 +377,7 @@ __global__ void k_pool_move(ScView C, const uint64_t *off, uint64_t base, uint64
                             uint32_t *ng) {
   const uint64_t ne = C.n_keys * CAP;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = i / CAP, e = i % CAP;
+    const uint64_t k = i % C.n_keys, e = i / C.n_keys;
     const uint32_t cnt = C.cnt[k];
     if (cnt == ABSENT || e >= cnt || !C.poff[i]) continue;
     const uint64_t src = C.poff[i], dst = base + off[i];
@@ -483,8 +488,8 @@ __global__ void k_sc_relabel_entries(const uint8_t *cnt, uint64_t n_keys, const 
                                      uint64_t *v1, const uint64_t *poff, const uint32_t *plen, uint32_t *mark,
                                      const uint64_t *old, const uint64_t *nw, uint64_t n) {
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_keys * CAP; s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = s / CAP;
-    if (cnt[k] == ABSENT || s % CAP >= cnt[k]) continue;
+    const uint64_t k = s % n_keys;  // entry-major: entry s / n_keys of key k
+    if (cnt[k] == ABSENT || s / n_keys >= cnt[k]) continue;
     const uint32_t t = ktype[k];
     if (t == AM_LWW && !vflag[s]) sc_relabel_word(v1 + s, old, nw, n);
     if (t == AM_AWSET || t == AM_MVREG)
@@ -563,29 +568,32 @@ int am_snapcache_grow(am_snapcache *c, uint64_t new_n) {
   am_ctx *ctx = c->ctx;
   AM_LOCK(ctx);
   if (new_n <= c->n_keys) return AM_OK;
-  const uint64_t nd = c->n_dc, ne0 = c->n_keys * CAP, ne = new_n * CAP + 1;
+  const uint64_t nd = c->n_dc, n0 = c->n_keys, ne = new_n * CAP + 1;
   std::vector<void *> fresh;
   int rc = AM_OK;
-  auto grow = [&](void **field, size_t old_b, size_t new_b, int fill) {
+  // rows = 1: a per-key column; rows = CAP (or CAP * n_dc): an entry-major field, whose rows of
+  // n0 keys move to rows of new_n
+  auto grow = [&](void **field, size_t w, size_t rows, size_t new_b, int fill) {
     void *p = nullptr;
     if (rc || (rc = am_dev_alloc(ctx, new_b, &p))) return;
     fresh.push_back(p);
     if (hipMemsetAsync(p, fill, new_b, ctx->stream) != hipSuccess ||
-        (old_b && hipMemcpyAsync(p, *field, old_b, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess))
+        (n0 && hipMemcpy2DAsync(p, new_n * w, *field, n0 * w, n0 * w, rows, hipMemcpyDeviceToDevice, ctx->stream) !=
+                   hipSuccess))
       rc = AM_ERR_HIP;
     *field = p;
   };
   void *old[10] = {c->cnt, c->owner, c->vc, c->pres, c->last_op, c->v0, c->v1, c->vflag, c->poff, c->plen};
-  grow((void **)&c->cnt, c->n_keys, new_n + 16, ABSENT);
-  grow((void **)&c->owner, c->n_keys * 4, (new_n + 1) * 4, 0xFF);
-  grow((void **)&c->vc, ne0 * nd * 8, ne * nd * 8, 0);
-  grow((void **)&c->pres, ne0 * 4, ne * 4, 0);
-  grow((void **)&c->last_op, ne0 * 8, ne * 8, 0);
-  grow((void **)&c->v0, ne0 * 8, ne * 8, 0);
-  grow((void **)&c->v1, ne0 * 8, ne * 8, 0);
-  grow((void **)&c->vflag, ne0, ne, 0);
-  grow((void **)&c->poff, ne0 * 8, ne * 8, 0);
-  grow((void **)&c->plen, ne0 * 4, ne * 4, 0);
+  grow((void **)&c->cnt, 1, 1, new_n + 16, ABSENT);
+  grow((void **)&c->owner, 4, 1, (new_n + 1) * 4, 0xFF);
+  grow((void **)&c->vc, 8, CAP * nd, ne * nd * 8, 0);
+  grow((void **)&c->pres, 4, CAP, ne * 4, 0);
+  grow((void **)&c->last_op, 8, CAP, ne * 8, 0);
+  grow((void **)&c->v0, 8, CAP, ne * 8, 0);
+  grow((void **)&c->v1, 8, CAP, ne * 8, 0);
+  grow((void **)&c->vflag, 1, CAP, ne, 0);
+  grow((void **)&c->poff, 8, CAP, ne * 8, 0);
+  grow((void **)&c->plen, 4, CAP, ne * 4, 0);
   if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
   if (rc) {
     for (void *p : fresh) c->allocs.push_back(p);  // freed with the cache
@@ -779,14 +787,16 @@ int am_snapcache_get(am_ctx *ctx, const am_snapcache *c, uint64_t key, uint32_t 
   AM_LOCK(ctx);
   AM_HIP(hipSetDevice(ctx->device));
   uint8_t cnt = 0;
-  const uint64_t s0 = key * CAP, nd = c->n_dc;
+  const uint64_t nk = c->n_keys, nd = c->n_dc;
   AM_HIP(hipMemcpyAsync(&cnt, c->cnt + key, 1, hipMemcpyDeviceToHost, ctx->stream));
-  if (vc) AM_HIP(hipMemcpyAsync(vc, c->vc + s0 * nd, CAP * nd * 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (pres) AM_HIP(hipMemcpyAsync(pres, c->pres + s0, CAP * 4, hipMemcpyDeviceToHost, ctx->stream));
-  if (last_op) AM_HIP(hipMemcpyAsync(last_op, c->last_op + s0, CAP * 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (v0) AM_HIP(hipMemcpyAsync(v0, c->v0 + s0, CAP * 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (v1) AM_HIP(hipMemcpyAsync(v1, c->v1 + s0, CAP * 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (vflag) AM_HIP(hipMemcpyAsync(vflag, c->vflag + s0, CAP, hipMemcpyDeviceToHost, ctx->stream));
+  // the key's column of each entry-major field (host arrays entry-first: vc [CAP][n_dc])
+  if (vc) AM_HIP(hipMemcpy2DAsync(vc, 8, c->vc + key, nk * 8, 8, CAP * nd, hipMemcpyDeviceToHost, ctx->stream));
+  if (pres) AM_HIP(hipMemcpy2DAsync(pres, 4, c->pres + key, nk * 4, 4, CAP, hipMemcpyDeviceToHost, ctx->stream));
+  if (last_op)
+    AM_HIP(hipMemcpy2DAsync(last_op, 8, c->last_op + key, nk * 8, 8, CAP, hipMemcpyDeviceToHost, ctx->stream));
+  if (v0) AM_HIP(hipMemcpy2DAsync(v0, 8, c->v0 + key, nk * 8, 8, CAP, hipMemcpyDeviceToHost, ctx->stream));
+  if (v1) AM_HIP(hipMemcpy2DAsync(v1, 8, c->v1 + key, nk * 8, 8, CAP, hipMemcpyDeviceToHost, ctx->stream));
+  if (vflag) AM_HIP(hipMemcpy2DAsync(vflag, 1, c->vflag + key, nk, 1, CAP, hipMemcpyDeviceToHost, ctx->stream));
   AM_HIP(hipStreamSynchronize(ctx->stream));
   *n_entries = cnt == ABSENT ? AM_SNAPCACHE_ABSENT : cnt;
   return AM_OK;
@@ -797,7 +807,7 @@ int am_snapcache_get_value(am_ctx *ctx, const am_snapcache *c, uint64_t key, uin
   if (!ctx || !c || !n_words || key >= c->n_keys || e >= CAP) return AM_ERR_INVALID;
   AM_LOCK(ctx);
   AM_HIP(hipSetDevice(ctx->device));
-  const uint64_t s = key * CAP + e;
+  const uint64_t s = (uint64_t)e * c->n_keys + key;  // entry-major
   uint64_t off = 0;
   uint32_t len = 0;
   AM_HIP(hipMemcpyAsync(&off, c->poff + s, 8, hipMemcpyDeviceToHost, ctx->stream));
