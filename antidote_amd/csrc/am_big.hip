@@ -576,7 +576,10 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     __syncthreads();
   }
   for (uint64_t x = x0; x < x1; ++x) {
-    const uint32_t b = find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
+    // a workgroup's run mostly stays in one read: search the read list (a chain of dependent
+    // loads) only when x leaves the current read's chunks
+    const bool same = cur != 0xFFFFFFFFu && x < R0.gchunk0 + ((R0.off1 - (R0.off0 & ~(uint64_t)(OPL - 1)) + CHUNK - 1) / CHUNK);
+    const uint32_t b = same ? cur : find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
     if (b != cur) {
       if (cur != 0xFFFFFFFFu) flush();
       cur = b;
