@@ -10,7 +10,8 @@ import glob
 import json
 import sys
 
-MAT = ("k_lane", "k_plan", "k_rows", "k_stream", "k_grp_wave", "k_grp_wg", "k_grp_row", "k_sets", "k_big_", "k_bc_wave",
+MAT = ("k_lane", "k_plan", "k_rows", "k_bc_rows", "k_stream", "k_grp_wave", "k_grp_wg", "k_grp_row", "k_sets", "k_big_",
+       "k_bc_wave",
        "k_sc_")
 
 
