@@ -111,6 +111,11 @@ __global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter,
       }
     }
     for (uint64_t q = d0 + n + lane; L.gmask && q < cap_end; q += WAVE_SZ) const_cast<uint64_t *>(L.gmask)[q] = 0;
+    if (L.zone_vc && cap_end > d0) {  // the key's blocks are no longer exact (ops replaced in place)
+      const uint64_t nz = (ls + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
+      uint64_t *ex = const_cast<uint64_t *>(L.zone_vc) + (uint64_t)L.n_dc * nz;
+      for (uint64_t z = d0 / AM_ZONE_OPS + lane; z <= (cap_end - 1) / AM_ZONE_OPS; z += WAVE_SZ) ex[z] = 0;
+    }
     if (L.var_off) {
       uint64_t *vo = const_cast<uint64_t *>(L.var_off);
       for (uint64_t q = d0 + n + lane; q < cap_end; q += WAVE_SZ) vo[q] = vb + nv;  // the free slots

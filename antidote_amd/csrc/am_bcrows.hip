@@ -137,10 +137,29 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
     const uint64_t tm = __ballot(take);
     wave_sync();
 
-    // ---- row q reads the batch's reads q, q + 4, ... (every row in lockstep, full EXEC) ----
+    // ---- row q reads the batch's reads q, q + 4, ... (every row in lockstep, full EXEC).  The
+    //      first 16 ops of the row's next read are loaded while this one is evaluated (most
+    //      reads have at most 16) ----
+    uint32_t nx[DMAX], nmeta = 0;
+    int64_t namt = 0;
+    uint64_t nft = 0;
+    auto load_op = [&](const BcrIn &w, uint32_t q, uint32_t(&x)[DMAX], uint32_t &meta, int64_t &amt, uint64_t &ft) {
+      const uint64_t p = (w.tk && q < w.nops) ? w.off0 + q : 0;  // (a row without a read loads op 0, unused)
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) x[d] = d < (int)nd ? L.pk_vc[(uint64_t)d * stride + p] : 0u;
+      meta = L.op_meta[p], amt = (int64_t)L.p0[p], ft = L.p1[p];
+    };
+    if (tm) load_op(sm.in[row], sl, nx, nmeta, namt, nft);
     for (uint32_t it = 0; it < WAVE / 4 && (tm >> (4 * it)); ++it) {
       const uint32_t j = 4 * it + row;
       const BcrIn in = sm.in[j];
+      uint32_t cx[DMAX];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) cx[d] = nx[d];
+      const uint32_t cmeta = nmeta;
+      const int64_t camt = namt;
+      const uint64_t cft = nft;
+      if (it + 1 < WAVE / 4 && (tm >> (4 * (it + 1)))) load_op(sm.in[j + 4], sl, nx, nmeta, namt, nft);
       const bool act = in.tk != 0;
       PkRead<DMAX> pk;
       pk_setup(u, nd, in.K, pk);
@@ -159,13 +178,16 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
         if (!__ballot(act && RG * t < in.nops)) continue;
         const uint32_t q = RG * t + sl;
         const bool v = act && q < in.nops;
-        const uint64_t p = v ? in.off0 + q : 0;  // (a row without a read loads op 0, unused)
-        uint32_t x[DMAX];
+        uint32_t x[DMAX], meta;
+        int64_t amt;
+        uint64_t ft;
+        if (t == 0) {  // prefetched
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d) x[d] = d < (int)nd ? L.pk_vc[(uint64_t)d * stride + p] : 0u;
-        const uint32_t meta = L.op_meta[p];
-        const int64_t amt = (int64_t)L.p0[p];
-        const uint64_t ft = L.p1[p];
+          for (int d = 0; d < DMAX; ++d) x[d] = cx[d];
+          meta = cmeta, amt = camt, ft = cft;
+        } else {
+          load_op(in, q, x, meta, amt, ft);
+        }
         if (!v) continue;
         if (x[0] == AM_PK_ESC) {  // outside the packed view: the row evaluates it below
           esc |= 1u << t;

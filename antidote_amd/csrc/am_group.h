@@ -816,8 +816,50 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         zin = nzr >= 64 ? ~0ull : ((1ull << nzr) - 1ull);
         for (uint32_t d = 0; d < nd; ++d) zin &= okm >> (d * nzr);
       }
+      // fresh reads (the batch clock): an aligned tile that is one EXACT zone whose bound the
+      // clock covers includes every op -- its bits, count and LastOpCt maxima come from the zone,
+      // not from the ops' commit vectors.  One round of loads per read: lane (d, z) tests zone z's
+      // bound of DC d (row nd: the exactness mark)
+      uint64_t zfull = 0;  // bit z - t0 / AM_ZONE_OPS: tile z is such a zone
+      uint64_t zval = 0;   // this lane's bound (row d < nd)
+      uint32_t zrows = 0;
+      if (!GENERAL && PACKED && L.zone_vc && !pk.never && TILE == AM_ZONE_OPS && t0 % AM_ZONE_OPS == 0 &&
+          off1 >= t0 + AM_ZONE_OPS) {
+        zrows = (uint32_t)((off1 - t0) / AM_ZONE_OPS);  // the read's whole tiles
+        if (zrows * (nd + 1) <= WAVE) {
+          const uint32_t dl = lane / zrows, zl = lane % zrows;
+          bool ok = true;
+          if (dl <= nd) {
+            zval = L.zone_vc[(uint64_t)dl * nz + t0 / AM_ZONE_OPS + zl];
+            uint64_t s0 = 0;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) s0 = (uint32_t)d == dl ? u.S[d] : s0;
+            ok = dl == nd ? zval == 1 : zval <= s0;
+          }
+          const uint64_t okm = __ballot(ok);
+          zfull = zrows >= 64 ? ~0ull : ((1ull << zrows) - 1ull);
+          for (uint32_t d = 0; d <= nd; ++d) zfull &= okm >> (d * zrows);
+        } else {
+          zrows = 0;
+        }
+      }
       for (uint64_t t = t0; t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
+        if (!GENERAL && zfull) {
+          const uint32_t zi = (uint32_t)((t - t0) / AM_ZONE_OPS);
+          if ((zfull >> zi) & 1ull) {  // every op of the tile included
+            if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = 0xFFFFFFFFu;
+            if (lane == 0) ap.count += AM_ZONE_OPS;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d)
+              if (d < (int)nd) {
+                const uint64_t zm = shfl_u64(zval, (uint32_t)d * zrows + zi);
+                ap.mx[d] = max(ap.mx[d], (uint32_t)(zm - pk.K));
+              }
+            n_skipped += AM_ZONE_OPS;
+            continue;
+          }
+        }
         if (zskip) {
           const uint64_t te = t + TILE < off1 ? t + TILE : off1;
           const uint64_t z0 = t / AM_ZONE_OPS, z1 = (te - 1) / AM_ZONE_OPS;
@@ -956,7 +998,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
     }
     wave_sync();  // the slots are rewritten by the next batch
   }
-  if (GENERAL && n_skipped && lane == 0) atomicAdd(H.skipped, (unsigned long long)n_skipped);
+  if (n_skipped && lane == 0) atomicAdd(H.skipped, (unsigned long long)n_skipped);
   PH_END();
 }
 

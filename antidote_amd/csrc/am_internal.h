@@ -205,9 +205,11 @@ __host__ __device__ __forceinline__ bool am_ngrp_big(uint32_t ng) {
   return ng != AM_NGRP_NONE && (ng & AM_NGRP_BIG) != 0;
 }
 // a key that gets the chunked token-group view when its log allows (include/antidote_mat.h):
-// an MV register with more than AM_GRP_MAX_REC ops, all of one type
+// an MV register with more than AM_BIG_MIN_OPS ops (an assign births one token and kills the
+// ones it overrides, so such a key's records outgrow the LDS builder's AM_GRP_MAX_REC), all of
+// one type
 __host__ __device__ __forceinline__ bool am_big_grp_key(const am_op_log &L, uint64_t k) {
-  return L.key_type[k] == AM_MVREG && am_kend(L, k) - L.key_off[k] > AM_GRP_MAX_REC &&
+  return L.key_type[k] == AM_MVREG && am_kend(L, k) - L.key_off[k] > AM_BIG_MIN_OPS &&
          !(L.key_flags && (L.key_flags[k] & AM_KEY_MIXED_TYPES));
 }
 // the chunk table's words

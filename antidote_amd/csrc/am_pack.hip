@@ -148,6 +148,22 @@ __global__ void k_zone(am_op_log L, uint64_t *zone, uint64_t nz) {
       const uint64_t m = wave_max_u64(mx[d]);
       if (lane == 0) zone[(uint64_t)d * nz + z] = m;
     }
+    // exact: every slot a used op of the block's first key, in the packed view, valid
+    const uint64_t z0 = z * AM_ZONE_OPS, z1 = z0 + AM_ZONE_OPS;
+    bool exact = z1 <= L.n_ops && L.pk_vc && L.key_tbase;
+    if (exact) {
+      uint64_t lo = 0, hi = L.n_keys;  // the key holding slot z0: last k with key_off[k] <= z0
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (L.key_off[mid] <= z0) lo = mid;
+        else hi = mid;
+      }
+      exact = L.key_off[lo] <= z0 && z1 <= am_kend(L, lo);
+    }
+    for (uint64_t p = z0 + lane; exact && p < z1; p += WAVE)
+      if (L.pk_vc[p] == AM_PK_ESC || (L.op_meta[p] & AM_META_BAD)) exact = false;
+    exact = __ballot(!exact) == 0;
+    if (lane == 0) zone[(uint64_t)L.n_dc * nz + z] = exact ? 1u : 0u;
   }
 }
 
@@ -266,7 +282,7 @@ int build_zones(am_store *st) {
   const uint64_t stride = d.snap_stride ? d.snap_stride : d.n_ops;
   const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
   void *zb = nullptr;
-  if (int rc = am_dev_alloc(c, (size_t)d.n_dc * nz * 8 + 8, &zb)) return rc;
+  if (int rc = am_dev_alloc(c, (size_t)(d.n_dc + 1) * nz * 8 + 8, &zb)) return rc;  // + the exactness row
   st->allocs.push_back(zb);
   const uint64_t blocks = (nz + 3) / 4 < 65536 ? (nz + 3) / 4 : 65536;
   hipLaunchKernelGGL(k_zone, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz);

@@ -494,14 +494,18 @@ def main():
             skipped += stat(False) / kern_iters  # ops of zones inside the reads' base snapshots
     else:
         step_ev = [event_ms(step) for _ in range(args.steps)]
+        stat(True)
         kern_ev = [event_ms(lambda: materialize(mat, dlog, reads)) for _ in range(kern_iters)]
+        skipped = stat(False) / kern_iters  # ops of exact zones inside the read clock
     kern_ms = float(np.mean(kern_ev))
     packed = bool(dlog.pk_vc)
     alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed, mat)
     if args.base == "cached":
-        # the commit vectors of ops in zones inside the base snapshot are not streamed (zone map,
-        # DESIGN 2): counted out of the layout bytes, reported as ops_skipped_per_launch
-        alg_bytes += cached_bytes(cfg, pre, reads) - skipped * bytes_per_vc(cfg["n_dc"], packed)
+        alg_bytes += cached_bytes(cfg, pre, reads)
+    # the commit vectors of ops whose zone decided them (cached: inside the base snapshot; fresh:
+    # an exact zone inside the read clock) are not streamed (zone map): counted out of
+    # the layout bytes, reported as ops_skipped_per_launch
+    alg_bytes -= skipped * bytes_per_vc(cfg["n_dc"], packed)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     logical = logical_bytes(cfg, dlog, ko, kt, reads, cached=args.base == "cached")
 

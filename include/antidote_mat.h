@@ -212,7 +212,12 @@ typedef struct am_op_log {
    * (a GC may leave it above the surviving ops).  A read with a base snapshot skips a block
    * whose bound is vectorclock:le the base clock: none of its ops is a candidate
    * (belongs_to_snapshot_op/3), so none counts, none is applied and none bounds NewLastOp --
-   * the ops already folded into the cached snapshot are not streamed again. */
+   * the ops already folded into the cached snapshot are not streamed again.
+   * Row n_dc, zone_vc[n_dc * n_zones + z] = 1 marks an EXACT block: all its slots are used ops
+   * of one key, none escaped from the packed view or invalid, and the bound is their maximum
+   * (built so; an in-place apply clears the mark of the blocks it touches).  A read whose clock
+   * covers an exact block's bound includes every op of it: its inclusion bits, count and
+   * LastOpCt maxima come from the mark and the bound, without the ops' commit vectors. */
   const uint64_t *zone_vc;
 } am_op_log;
 #define AM_ZONE_OPS 256u
@@ -222,7 +227,7 @@ typedef struct am_op_log {
 #define AM_REC_GRP(m) ((m) >> 17)
 #define AM_NGRP_NONE 0xFFFFFFFFu
 #define AM_GRP_MAX_REC 2048u
-/* Chunked token-group view of a hot MV-register key (more than AM_GRP_MAX_REC ops): its groups
+/* Chunked token-group view of a hot MV-register key (more than AM_BIG_MIN_OPS ops): its groups
  * are built with device-wide sorts instead of one workgroup's LDS, key_ngrp[k] = G |
  * AM_NGRP_BIG (G < AM_BIG_MAX_GRP), and its record range is laid out per AM_BIG_CHUNK ops:
  *   rec_g[rec_key_off[k] + c], c = 0..nch   the chunk table: record offset (relative to
@@ -234,6 +239,7 @@ typedef struct am_op_log {
  * Groups and their pairs (grp) are as above; an effective kill always follows its group's
  * birth, so a group survives a read iff its birth is included and no kill of it is. */
 #define AM_NGRP_BIG 0x80000000u
+#define AM_BIG_MIN_OPS (AM_GRP_MAX_REC / 2)
 #define AM_BIG_CHUNK 1024u
 #define AM_BIG_MAX_GRP (1u << 21)
 #define AM_BREC_OP(m) ((m) & 0x3FFu)

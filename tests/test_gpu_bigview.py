@@ -62,9 +62,9 @@ def _chain(n_dc, n_ops, t0=10, vals=1000):
 
 @pytest.mark.parametrize("n_dc", [3, 16])
 def test_gpu_chunked_view_chains(mat, n_dc):
-    """Override chains of 2049 .. 70000 ops (beyond the LDS builder, one above the old 2^16-op
+    """Override chains of 1025 .. 70000 ops (beyond the LDS builder, one above the old 2^16-op
     limit) read at several snapshot quantiles; short keys in the same batch."""
-    lens = [0, 40, 2048, 2049, 5000, 70000, 9001]
+    lens = [0, 40, 1024, 1025, 2049, 5000, 70000, 9001]
     keys = [_chain(n_dc, n) for n in lens]
     log = HostLog(n_dc, keys, key_types=[abi.AM_MVREG] * len(keys))
     reads = []
@@ -74,9 +74,9 @@ def test_gpu_chunked_view_chains(mat, n_dc):
             reads.append(Read(k, abi.AM_MVREG, {d: int(hi * q) + d for d in range(n_dc)}))
     got, ng = _compare(mat, log, reads, cap=64)
     for k, n in enumerate(lens):
-        if n > 2048:  # one group per token
+        if n > 1024:  # one group per token
             assert int(ng[k]) == (NGRP_BIG | n), (k, hex(int(ng[k])))
-        else:         # the LDS builder's (2048 ops hold 4095 records: ungrouped)
+        else:         # the LDS builder's (1024 ops hold 2047 records)
             assert int(ng[k]) == NGRP_NONE or not int(ng[k]) & NGRP_BIG, (k, hex(int(ng[k])))
 
 

@@ -69,16 +69,33 @@ def test_gpu_zone_skip_cached_reads(mat, t, n_dc):
         store.close()
 
 
-def test_gpu_zone_no_skip_without_base(mat):
-    """Fresh reads (base ignore) stream every op: the counter stays at zero."""
-    rng = random.Random(4500)
-    keys = [randlog.rand_key_ops(rng, abi.AM_AWSET, 3, 800) for _ in range(4)]
-    log = HostLog(3, keys, key_types=[abi.AM_AWSET] * 4)
+@pytest.mark.parametrize("t", [abi.AM_AWSET, abi.AM_MVREG])
+def test_gpu_zone_fresh_exact_blocks(mat, t):
+    """Fresh reads (the batch clock): an aligned 256-op block that is EXACT (one key's ops, all in
+    the packed view) and inside the read clock is included whole from its zone -- bits, count
+    and LastOpCt maxima -- without streaming its commit vectors.  Key lengths that are multiples
+    of 256 keep the blocks aligned; a ragged key last."""
+    from antidote_amd.oplog import HostBatch
+    from oracle import amo
+    rng = random.Random(4600 + t)
+    n_dc = 4
+    lens = [1024, 512, 768, 256, 1024, 300]
+    keys = [randlog.rand_key_ops(rng, t, n_dc, n) for n in lens]
+    log = HostLog(n_dc, keys, key_types=[t] * len(keys))
     st = mat.store(log)
-    _skipped(mat)
     try:
-        hi = max(ops[-1].commit_time for ops in keys)
-        mat.read_batch(st, [Read(k, abi.AM_AWSET, {d: hi for d in range(3)}) for k in range(4)], [4096] * 4)
-        assert _skipped(mat) == 0
+        for q in (0.3, 0.8, 1.2):
+            hi = max(ops[-1].commit_time for ops in keys)
+            clock = {d: int(hi * q) + d for d in range(n_dc)}
+            reads = [Read(k, t, clock) for k in range(len(keys))]
+            caps = [4096] * len(reads)
+            _skipped(mat)
+            got = mat.read_batch(st, reads, caps)
+            skipped = _skipped(mat)
+            ref = amo.materialize(log, HostBatch(n_dc, reads, caps))
+            for i in range(len(reads)):
+                assert got.result(i) == ref.result(i), (q, i)
+            if q > 1.0:
+                assert skipped > 0  # the clock covers whole blocks
     finally:
         st.close()
