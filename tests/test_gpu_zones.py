@@ -71,31 +71,46 @@ def test_gpu_zone_skip_cached_reads(mat, t, n_dc):
 
 @pytest.mark.parametrize("t", [abi.AM_AWSET, abi.AM_MVREG])
 def test_gpu_zone_fresh_exact_blocks(mat, t):
-    """Fresh reads (the batch clock): an aligned 256-op block that is EXACT (one key's ops, all in
-    the packed view) and inside the read clock is included whole from its zone -- bits, count
-    and LastOpCt maxima -- without streaming its commit vectors.  Key lengths that are multiples
-    of 256 keep the blocks aligned; a ragged key last."""
+    """Fresh reads at one batch clock (the bench's step): an aligned 256-op block that is EXACT
+    (one key's ops, all in the packed view) and inside the clock is included whole from its
+    zone -- bits, count and LastOpCt maxima -- without streaming its commit vectors.  Device
+    generated 1024-op keys (aligned blocks), sampled keys against the oracle on the host
+    regeneration; the context counter shows blocks were taken from their zones."""
+    import numpy as np
+    import torch
+    from antidote_amd import synth
+    from antidote_amd.devbatch import DeviceReads, materialize
     from antidote_amd.oplog import HostBatch
     from oracle import amo
-    rng = random.Random(4600 + t)
-    n_dc = 4
-    lens = [1024, 512, 768, 256, 1024, 300]
-    keys = [randlog.rand_key_ops(rng, t, n_dc, n) for n in lens]
-    log = HostLog(n_dc, keys, key_types=[t] * len(keys))
-    st = mat.store(log)
+    kw = dict(n_keys=400, n_dc=8, type_=t, ops_per_key=1024)
+    if t == abi.AM_AWSET:
+        kw["universe"] = 64
+    p = synth.params(**kw)
+    st = mat.synth_store(p)
+    dlog = st.device_log()
+    hlog = synth.host_log(p, 0, p.n_keys)
+    rng = np.random.default_rng(5)
     try:
-        for q in (0.3, 0.8, 1.2):
-            hi = max(ops[-1].commit_time for ops in keys)
-            clock = {d: int(hi * q) + d for d in range(n_dc)}
-            reads = [Read(k, t, clock) for k in range(len(keys))]
-            caps = [4096] * len(reads)
+        for q in (0.3, 0.75, 1.0):
+            clock = synth.read_clock(p, q)
+            dr = DeviceReads(p.n_keys, p.n_dc, t, clock, set_cap=1100)
+            torch.cuda.synchronize()
             _skipped(mat)
-            got = mat.read_batch(st, reads, caps)
+            materialize(mat, dlog, dr)
+            mat.sync()
             skipped = _skipped(mat)
-            ref = amo.materialize(log, HostBatch(n_dc, reads, caps))
-            for i in range(len(reads)):
-                assert got.result(i) == ref.result(i), (q, i)
-            if q > 1.0:
+            h = dr.host()
+            sample = np.sort(rng.choice(p.n_keys, 60, replace=False))
+            reads = [Read(int(k), t, {d: clock[d] for d in range(p.n_dc)}) for k in sample]
+            ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, [1100] * len(reads)))
+            vals = dr.values(sample)
+            for j, k in enumerate(sample):
+                ct = None if h["last_ct_ignore"][k] else {d: int(h["last_ct"][d, k]) for d in range(p.n_dc)
+                                                          if (int(h["last_ct_pres"][k]) >> d) & 1}
+                got = ("ok", vals[j], int(h["new_last_op"][k]), ct, bool(h["is_new_ss"][k]), int(h["count"][k]),
+                       int(h["flags"][k]))
+                assert got == ref.result(j), (q, int(k))
+            if q >= 0.75:
                 assert skipped > 0  # the clock covers whole blocks
     finally:
         st.close()
