@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
 template <int DMAX, int TYPE, bool PACKED>
 __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
                                                    const BigRead *br, BigAcc *accs, uint32_t *bm, BigSlots SL,
-                                                   uint64_t n_gch, unsigned long long *skipped) {
+                                                   uint64_t n_gch) {
   constexpr uint32_t NS = (uint32_t)(DMAX * DMAX + DMAX);
   constexpr size_t HB = TYPE == AM_MVREG ? 2 * GH * 4 : (size_t)NS * 20;
   __shared__ __attribute__((aligned(16))) unsigned char lds[HB];
@@ -520,12 +520,6 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
   uint32_t *spres = reinterpret_cast<uint32_t *>(lds + (size_t)NS * 16);
   __shared__ uint32_t incl[CHUNK / 32];
   __shared__ uint64_t red[BLOCK / WAVE][DMAX + 4];
-  // exact zones (include/antidote_mat.h zone_vc) of the chunk that a fresh read's clock covers:
-  // their ops are included whole, without their commit vectors
-  constexpr uint32_t ZC = CHUNK / AM_ZONE_OPS + 1;  // zones a chunk touches
-  __shared__ uint32_t zin[ZC];
-  __shared__ uint32_t zmx[ZC][DMAX];
-  uint64_t n_zone = 0;
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
   const uint32_t nbig = uniform_u32(*nbig_p);
   const uint64_t n = B.n_reads;
@@ -610,45 +604,10 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     const uint64_t t0 = R0.off0 & ~(uint64_t)(OPL - 1), c = x - R0.gchunk0;
     const uint64_t lo = t0 + c * CHUNK, hi = lo + CHUNK < R0.off1 ? lo + CHUNK : R0.off1;
     const uint64_t g = lo + (uint64_t)tid * OPL;
-    const bool zok = PACKED && L.zone_vc && u.base_ignore && !pk.never;
-    const uint64_t zlo = lo / AM_ZONE_OPS;
-    if (zok) {  // the chunk's zones: exact and inside the clock?
-      const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
-      const uint32_t nzc = (uint32_t)((hi - 1) / AM_ZONE_OPS - zlo + 1);
-      if (tid < nzc) {
-        const uint64_t z = zlo + tid;
-        bool in = L.zone_vc[(uint64_t)nd * nz + z] == 1;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d)
-          if (d < (int)nd) {
-            const uint64_t b = L.zone_vc[(uint64_t)d * nz + z];
-            in = in && b <= u.S[d];
-            zmx[tid][d] = (uint32_t)(b - pk.K);
-          }
-        zin[tid] = in ? 1u : 0u;
-        if (in) {  // its ops inside this chunk
-          const uint64_t a = z * AM_ZONE_OPS > lo ? z * AM_ZONE_OPS : lo;
-          const uint64_t e = (z + 1) * AM_ZONE_OPS < hi ? (z + 1) * AM_ZONE_OPS : hi;
-          n_zone += e - a;
-        }
-      }
-      __syncthreads();
-    }
-    // a lane's 4 ops lie in one zone (g is 4-aligned)
-    auto incl_z = [&]() -> uint32_t {
-      if (zok && zin[g / AM_ZONE_OPS - zlo]) {
-        const uint32_t zi = (uint32_t)(g / AM_ZONE_OPS - zlo);
-        ap.count += OPL;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) ap.mx[d] = max(ap.mx[d], zmx[zi][d]);
-        return (1u << OPL) - 1u;
-      }
-      return incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
-    };
     if (TYPE == AM_BCOUNTER) {  // included ops -> LDS slot sums (orddict:update_counter)
       if (g < hi) {
         const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
-        const uint32_t ib = incl_z();
+        const uint32_t ib = incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
 #pragma unroll
         for (int k = 0; k < OPL; ++k) {
           if (!((ib >> k) & 1u)) continue;
@@ -664,14 +623,13 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
           atomicOr(&spres[slot], 1u);
         }
       }
-      if (zok) __syncthreads();  // zin / zmx are rewritten by the next chunk
-      continue;                  // the slot sums stay in LDS until the read's flush
+      continue;  // the slot sums stay in LDS until the read's flush
     }
     for (uint32_t i = tid; i < 2 * GH; i += BLOCK) hs[i] = GH_EMPTY;
     if (tid < CHUNK / 32) incl[tid] = 0;
     __syncthreads();
     if (g < hi) {
-      const uint32_t ib = incl_z();
+      const uint32_t ib = incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
       if (ib) atomicOr(&incl[(uint32_t)(g - lo) >> 5], ib << ((uint32_t)(g - lo) & 31u));
     }
     __syncthreads();
@@ -679,7 +637,6 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     __syncthreads();
   }
   if (cur != 0xFFFFFFFFu) flush();
-  if (n_zone) atomicAdd(skipped, (unsigned long long)n_zone);
 }
 
 // ---- births -> hash on the kill key ----
@@ -907,10 +864,10 @@ int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_res
     const unsigned g4 = (unsigned)(n_gch < gcap ? n_gch : gcap);
     if (am_log_packed(L))
       hipLaunchKernelGGL((k_big_run<DMAX, TYPE, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br, acc,
-                         G.bm, SL, n_gch, (unsigned long long *)(ctx->stats + AM_STAT_OPS_SKIPPED));
+                         G.bm, SL, n_gch);
     else
       hipLaunchKernelGGL((k_big_run<DMAX, TYPE, false>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br,
-                         acc, G.bm, SL, n_gch, (unsigned long long *)(ctx->stats + AM_STAT_OPS_SKIPPED));
+                         acc, G.bm, SL, n_gch);
     AM_HIP(hipGetLastError());
   }
   if (TYPE != AM_BCOUNTER) {
