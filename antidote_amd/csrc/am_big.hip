@@ -72,6 +72,7 @@ struct BigRec {
   uint64_t *ot;       // finish: AW survivor tokens (global-scratch sort)
   int32_t *oi;        // finish: AW survivor index (global-scratch sort payload)
   uint32_t *bm;       // grouped mode: per read born [gw] | killed [gw] bitmaps
+  uint32_t *ibm;      // grouped mode: per chunk inclusion bits (32 words)
   uint8_t *dead;
   uint64_t *ka, *kb;  // exported kills: kill key
   int32_t *kp;
@@ -639,6 +640,121 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
   if (cur != 0xFFFFFFFFu) flush();
 }
 
+// ---- grouped MV reads in two passes (no barrier-bound per-chunk pipeline):
+//      k_big_gincl  runs of chunks: the ops' inclusion bits into a global bitmap (32 words per
+//                   1024-op chunk, every word written) + the scalar partials, one reduction per
+//                   read and workgroup -- a streaming kernel with no LDS state
+//      k_big_grec   per chunk: the records against those bits, the chunk's births and kills
+//                   settled in the LDS hash sets (grouped_records), the rest exported ----
+template <int DMAX, bool PACKED>
+__global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
+                                                     const BigRead *br, BigAcc *accs, uint32_t *ibm, uint64_t n_gch) {
+  __shared__ uint64_t red[BLOCK / WAVE][DMAX + 4];
+  const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+  const uint32_t nbig = uniform_u32(*nbig_p);
+  const uint32_t nd = L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint64_t per = (n_gch + gridDim.x - 1) / gridDim.x;
+  const uint64_t x0 = (uint64_t)blockIdx.x * per < n_gch ? (uint64_t)blockIdx.x * per : n_gch;
+  const uint64_t x1 = x0 + per < n_gch ? x0 + per : n_gch;
+  uint32_t cur = 0xFFFFFFFFu;
+  BigRead R0{};
+  ReadU<DMAX> u;
+  PkRead<DMAX> pk;
+  AccP<DMAX> ap;
+  Acc<DMAX> a;
+  auto flush = [&]() {
+    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
+    const uint32_t cnt = wave_sum_u32(a.count), fl = wave_or_u32(a.flags), pr = wave_or_u32(a.pres);
+    const uint64_t mn = wave_min_u64(a.min_excl);
+    uint64_t mx[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? wave_max_u64(a.mx[d]) : 0;
+    if (lane == 0) {
+      red[wv][0] = cnt, red[wv][1] = fl, red[wv][2] = pr, red[wv][3] = mn;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) red[wv][4 + d] = mx[d];
+    }
+    __syncthreads();
+    if (tid < 4 + (uint32_t)DMAX) {
+      uint64_t v = red[0][tid];
+      for (uint32_t w = 1; w < BLOCK / WAVE; ++w) {
+        const uint64_t y = red[w][tid];
+        v = tid == 0 ? v + y : (tid <= 2 ? (v | y) : tid == 3 ? (v < y ? v : y) : (v > y ? v : y));
+      }
+      BigAcc *acc = accs + cur;
+      if (tid == 0 && v) atomicAdd(&acc->count, (uint32_t)v);
+      if (tid == 1 && v) atomicOr(&acc->flags, (uint32_t)v);
+      if (tid == 2 && v) atomicOr(&acc->pres, (uint32_t)v);
+      if (tid == 3 && v != NONE) atomicMin(&acc->min_excl, (unsigned long long)v);
+      if (tid >= 4 && tid - 4 < nd && v) atomicMax(&acc->mx[tid - 4], (unsigned long long)v);
+    }
+    __syncthreads();
+  };
+  for (uint64_t x = x0; x < x1; ++x) {
+    const bool same = cur != 0xFFFFFFFFu && x < R0.gchunk0 + ((R0.off1 - (R0.off0 & ~(uint64_t)(OPL - 1)) + CHUNK - 1) / CHUNK);
+    const uint32_t b = same ? cur : find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
+    if (b != cur) {
+      if (cur != 0xFFFFFFFFu) flush();
+      cur = b;
+      R0 = br[b];
+      const uint64_t r = R0.r;
+      const uint64_t n = B.n_reads;
+      u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+      const uint64_t rstride = B.per_read_clock ? n : 1, ridx = B.per_read_clock ? r : 0;
+      u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
+      u.base_ignore = !B.base_ignore || B.base_ignore[r];
+      u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+        u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+      }
+      u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+      u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+      if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[r])]), pk);
+      ap.reset();
+      a.reset();
+    }
+    const uint64_t t0 = R0.off0 & ~(uint64_t)(OPL - 1), c = x - R0.gchunk0;
+    const uint64_t lo = t0 + c * CHUNK, hi = lo + CHUNK < R0.off1 ? lo + CHUNK : R0.off1;
+    const uint64_t g = lo + (uint64_t)tid * OPL;
+    const uint32_t ib = g < hi ? incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a) : 0u;
+    uint32_t word = ib << (OPL * (tid % 8));  // 8 lanes of 4 ops per 32-bit word
+    word |= (uint32_t)__shfl_xor((int)word, 1);
+    word |= (uint32_t)__shfl_xor((int)word, 2);
+    word |= (uint32_t)__shfl_xor((int)word, 4);
+    if (tid % 8 == 0) ibm[x * (CHUNK / 32) + tid / 8] = word;
+  }
+  if (cur != 0xFFFFFFFFu) flush();
+}
+
+__global__ void __launch_bounds__(BLOCK) k_big_grec(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
+                                                    const BigRead *br, const uint32_t *ibm, uint32_t *bm,
+                                                    uint64_t n_gch) {
+  __shared__ uint32_t hs[2 * GH];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nbig = uniform_u32(*nbig_p);
+  const uint64_t per = (n_gch + gridDim.x - 1) / gridDim.x;
+  const uint64_t x0 = (uint64_t)blockIdx.x * per < n_gch ? (uint64_t)blockIdx.x * per : n_gch;
+  const uint64_t x1 = x0 + per < n_gch ? x0 + per : n_gch;
+  uint32_t cur = 0xFFFFFFFFu;
+  BigRead R0{};
+  for (uint64_t x = x0; x < x1; ++x) {
+    const bool same = cur != 0xFFFFFFFFu && x < R0.gchunk0 + ((R0.off1 - (R0.off0 & ~(uint64_t)(OPL - 1)) + CHUNK - 1) / CHUNK);
+    if (!same) {
+      cur = find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
+      R0 = br[cur];
+    }
+    const uint64_t t0 = R0.off0 & ~(uint64_t)(OPL - 1), c = x - R0.gchunk0;
+    const uint64_t lo = t0 + c * CHUNK, hi = lo + CHUNK < R0.off1 ? lo + CHUNK : R0.off1;
+    for (uint32_t i = tid; i < 2 * GH; i += BLOCK) hs[i] = GH_EMPTY;
+    __syncthreads();
+    grouped_records(L, B.key[R0.r], R0, lo, hi, ibm + x * (CHUNK / 32), hs, bm + R0.bm0, tid);
+    __syncthreads();
+  }
+}
+
 // ---- births -> hash on the kill key ----
 template <int TYPE>
 __global__ void k_big_hash(const uint32_t *nbig_p, const BigRead *br, const BigAcc *accs, BigRec G, uint64_t total) {
@@ -859,7 +975,21 @@ int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_res
                          *B, nbig_d, br, acc, G, SL, n_chunks);
     AM_HIP(hipGetLastError());
   }
-  if constexpr (TYPE != AM_AWSET) if (n_gch) {  // runs of chunks: grouped MV reads, bounded-counter reads
+  if constexpr (TYPE == AM_MVREG) if (n_gch) {  // grouped MV reads: inclusion pass, record pass
+    const uint64_t gcap = (uint64_t)ctx->n_cu * 8;
+    const unsigned g4 = (unsigned)(n_gch < gcap ? n_gch : gcap);
+    if (am_log_packed(L))
+      hipLaunchKernelGGL((k_big_gincl<DMAX, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br, acc,
+                         G.ibm, n_gch);
+    else
+      hipLaunchKernelGGL((k_big_gincl<DMAX, false>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br, acc,
+                         G.ibm, n_gch);
+    const uint64_t rcap = (uint64_t)ctx->n_cu * 16;
+    hipLaunchKernelGGL(k_big_grec, dim3((unsigned)(n_gch < rcap ? n_gch : rcap)), dim3(BLOCK), 0, ctx->stream, *L, *B,
+                       nbig_d, br, G.ibm, G.bm, n_gch);
+    AM_HIP(hipGetLastError());
+  }
+  if constexpr (TYPE == AM_BCOUNTER) if (n_gch) {  // runs of chunks: bounded-counter reads
     const uint64_t gcap = (uint64_t)ctx->n_cu * 8;
     const unsigned g4 = (unsigned)(n_gch < gcap ? n_gch : gcap);
     if (am_log_packed(L))
@@ -924,8 +1054,9 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   // slots; the finish pass's AW token / index scratch -- n_rec each
   const size_t rb = am_round_up(n_rec * 8, 256), r4 = am_round_up(n_rec * 4, 256), r1 = am_round_up(n_rec, 256);
   const size_t hb = am_round_up(2 * n_rec * 4, 256), bmb = am_round_up(n_bm * 4 + 4, 256);
+  const size_t ib = TYPE == AM_MVREG ? am_round_up(n_gch * (CHUNK / 32) * 4 + 4, 256) : 0;
   void *recs = nullptr;
-  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 5 * rb + 4 * r4 + r1 + hb + bmb, &recs);
+  rc = am_ctx_scratch(ctx, AM_SCR_BIGREC, 5 * rb + 4 * r4 + r1 + hb + bmb + ib, &recs);
   if (rc) return rc;
   char *q = (char *)recs;
   BigRec G;
@@ -940,7 +1071,8 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   G.oi = (int32_t *)q, q += r4;
   G.dead = (uint8_t *)q, q += r1;
   G.H = (uint32_t *)q, q += hb;
-  G.bm = (uint32_t *)q;
+  G.bm = (uint32_t *)q, q += bmb;
+  G.ibm = (uint32_t *)q;
   if (n_bm) AM_HIP(hipMemsetAsync(G.bm, 0, n_bm * 4, ctx->stream));
   AM_HIP(hipMemsetAsync(G.dead, 0, n_rec, ctx->stream));
   AM_HIP(hipMemsetAsync(G.H, 0xFF, 2 * n_rec * 4, ctx->stream));
