@@ -50,7 +50,16 @@ struct am_ctx {
   uint32_t *tee_g = nullptr;
   int64_t tee_shift = 0;
   uint8_t *tee_done = nullptr;
+  // The mixed-batch planner's per-type streams (am_plan.hip): sub-contexts of the set types
+  // on the same device, sharing the counters, each with its own stream, scratch slots and
+  // pinned buffer, so one type's tiers overlap another's.  ev_fork orders them after the
+  // planner; their ev0 joins them back.
+  am_ctx *sub[3] = {};
+  bool is_sub = false;
+  hipEvent_t ev_fork = nullptr;
 };
+// sub-context i of c (created on first use; null on failure, error set)
+am_ctx *am_ctx_sub(am_ctx *c, int i);
 #define AM_LOCK(ctxp) std::lock_guard<std::recursive_mutex> am_lock_((ctxp)->mu)
 
 // A selection of a batch's reads: the planner's per-kernel sub-batches.  idx == nullptr

@@ -18,7 +18,9 @@
 // count at start, so the planner adds no host round trip.
 //
 // Single-type batches (type_hint != 0) skip the planner.  Set types may need the
-// big-read path, which sizes its scratch on the host (one synchronization).
+// big-read path, which sizes its scratch on the host (one synchronization).  In a mixed
+// batch every set type's chain runs on a stream of its own (am_ctx::sub), joined back
+// before the call returns: a type's latency-bound tiers overlap the other types' tiers.
 #include "am_wave.h"
 
 using namespace amk;
@@ -127,8 +129,10 @@ int run_scalar(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
 //   bounded counter: row tier -> (hand-off lists) wave tier (am_bcwave.hip) -> k_sets ->
 //     (retry list) big-read tier
 // rows_buf / grp_buf (two lists): [0] = 0, [1] = hand-off count, list at +64.
-int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
-             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf, bool lanes_done) {
+// run_sets_front: every tier up to k_sets, the big-read tier's retry list in *retry_out.
+int run_sets_front(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                   uint32_t type, uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf, bool lanes_done,
+                   am_retry *retry_out) {
   am_retry retry;
   retry.count = retry_buf;
   retry.list = retry_buf + 1;
@@ -184,9 +188,15 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
       cur.range = bufs[k];
     }
   }
-  rc = am_launch_sets(ctx, L, B, R, cur, type, retry);
-  if (rc) return rc;
-  return am_launch_big(ctx, L, B, R, type, retry);
+  *retry_out = retry;
+  return am_launch_sets(ctx, L, B, R, cur, type, retry);
+}
+
+int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, uint32_t type,
+             uint32_t *retry_buf, uint32_t *rows_buf, uint32_t *grp_buf, bool lanes_done) {
+  am_retry retry;
+  const int rc = run_sets_front(ctx, L, B, R, S, type, retry_buf, rows_buf, grp_buf, lanes_done, &retry);
+  return rc ? rc : am_launch_big(ctx, L, B, R, type, retry);
 }
 
 }  // namespace
@@ -214,7 +224,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   void *rows_scr = nullptr, *grp_scr = nullptr;
   {
     int rc = am_ctx_scratch(ctx, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &rows_scr);
-    if (!rc && B->type_hint != AM_PN && B->type_hint != AM_LWW)
+    if (!rc && B->type_hint >= AM_AWSET)
       rc = am_ctx_scratch(ctx, AM_SCR_GRP, 2 * (n + 64) * sizeof(uint32_t), &grp_scr);
     if (rc) return rc;
   }
@@ -259,13 +269,12 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     in.range = lbuf;
   }
   const uint64_t n_blk = (n_in + PCHUNK - 1) / PCHUNK;
-  // scratch: [retry count + list: n+1][range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
-  const size_t words = (n + 64) + 3 * NCLS + n_blk * NCLS + n + 64;
+  // scratch: [range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
+  const size_t words = 3 * NCLS + n_blk * NCLS + n + 64;
   void *scr = nullptr;
   int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, words * sizeof(uint32_t), &scr);
   if (rc) return rc;
-  uint32_t *retry_buf = (uint32_t *)scr;
-  uint32_t *range = retry_buf + n + 64;
+  uint32_t *range = (uint32_t *)scr;
   uint32_t *tot = range + 2 * NCLS;
   uint32_t *cnt = tot + NCLS;
   uint32_t *idx = cnt + n_blk * NCLS;
@@ -275,16 +284,45 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, tot, range,
                      idx);
   AM_HIP(hipGetLastError());
-  for (uint32_t t = AM_PN; t <= AM_BCOUNTER; ++t) {
+  // The set types' chains run on the sub-contexts' streams (one per type, own scratch), the
+  // scalar types' on this one: the chains share only the planner's selection, so one type's
+  // tiers fill the machine while another's drain.  The big-read tier synchronizes its own
+  // stream once, so every chain's front is queued before the first of those waits.
+  am_ctx *sub[3] = {};
+  am_retry retry[3];
+  AM_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+  auto join = [&]() {
+    for (am_ctx *s : sub)
+      if (s && hipEventRecord(s->ev0, s->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, s->ev0, 0);
+  };
+  for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t) {
+    am_ctx *s = am_ctx_sub(ctx, (int)(t - AM_AWSET));
+    if (!s) rc = AM_ERR_HIP;
+    if (!rc && hipStreamWaitEvent(s->stream, ctx->ev_fork, 0) != hipSuccess) rc = AM_ERR_HIP;
+    if (rc) break;
+    sub[t - AM_AWSET] = s;
+    s->grp_hint_in = ctx->grp_hint_in;
+    s->tee_a = ctx->tee_a, s->tee_b = ctx->tee_b, s->tee_g = ctx->tee_g, s->tee_shift = ctx->tee_shift;
+    s->tee_done = ctx->tee_done;
+    void *sr = nullptr, *sg = nullptr, *sp = nullptr;
+    rc = am_ctx_scratch(s, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &sr);
+    if (!rc) rc = am_ctx_scratch(s, AM_SCR_GRP, 2 * (n + 64) * sizeof(uint32_t), &sg);
+    if (!rc) rc = am_ctx_scratch(s, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &sp);
     am_sel S;
     S.idx = idx;
     S.range = range + 2 * (t - 1);
-    if (t == AM_PN || t == AM_LWW)
-      rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
-    else
-      rc = run_sets(ctx, L, B, R, S, t, retry_buf, (uint32_t *)rows_scr, (uint32_t *)grp_scr,
-                    ((lanes >> t) & 1u) != 0);
-    if (rc) return rc;
+    if (!rc)
+      rc = run_sets_front(s, L, B, R, S, t, (uint32_t *)sp, (uint32_t *)sr, (uint32_t *)sg, ((lanes >> t) & 1u) != 0,
+                          &retry[t - AM_AWSET]);
   }
-  return AM_OK;
+  for (uint32_t t = AM_PN; t <= AM_LWW && !rc; ++t) {
+    am_sel S;
+    S.idx = idx;
+    S.range = range + 2 * (t - 1);
+    rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
+  }
+  for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t)
+    rc = am_launch_big(sub[t - AM_AWSET], L, B, R, t, retry[t - AM_AWSET]);
+  join();
+  return rc;
 }

@@ -37,6 +37,7 @@ int am_ctx_open(int device, am_ctx **out) {
   AM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   AM_HIP(hipEventCreate(&c->ev0));
   AM_HIP(hipEventCreate(&c->ev1));
+  AM_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
   AM_HIP(hipMalloc((void **)&c->stats, 8 * sizeof(uint64_t)));
   AM_HIP(hipMemsetAsync(c->stats, 0, 8 * sizeof(uint64_t), c->stream));
   *out = c;
@@ -46,15 +47,19 @@ int am_ctx_open(int device, am_ctx **out) {
 int am_ctx_close(am_ctx *c) {
   if (!c) return AM_OK;
   AM_HIP(hipSetDevice(c->device));
+  for (am_ctx *&s : c->sub)
+    if (s) (void)am_ctx_close(s), s = nullptr;
   AM_HIP(hipStreamSynchronize(c->stream));
   for (void *&p : c->scratch)
     if (p) (void)hipFree(p), p = nullptr;
   for (auto &kv : c->free_blocks) (void)hipFree(kv.second);
   c->free_blocks.clear();
   if (c->pinned) (void)hipHostFree(c->pinned), c->pinned = nullptr;
-  if (c->stats) (void)hipFree(c->stats), c->stats = nullptr;
+  if (c->stats && !c->is_sub) (void)hipFree(c->stats);
+  c->stats = nullptr;
   (void)hipEventDestroy(c->ev0);
   (void)hipEventDestroy(c->ev1);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return AM_OK;
@@ -95,6 +100,25 @@ int am_timer_stop(am_ctx *c, float *ms) {
 }
 
 }  // extern "C"
+
+am_ctx *am_ctx_sub(am_ctx *c, int i) {
+  if (c->sub[i]) return c->sub[i];
+  am_ctx *s = new am_ctx();
+  s->device = c->device;
+  s->n_cu = c->n_cu;
+  s->is_sub = true;
+  s->stats = c->stats;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev0, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev1, hipEventDisableTiming) != hipSuccess) {
+    am_set_error("sub-context stream / events: %s", hipGetErrorString(hipGetLastError()));
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    delete s;
+    return nullptr;
+  }
+  return c->sub[i] = s;
+}
 
 int am_ctx_scratch(am_ctx *c, int slot, size_t bytes, void **out) {
   if (!c || slot < 0 || slot >= AM_N_SCR || !out) return AM_ERR_INVALID;
