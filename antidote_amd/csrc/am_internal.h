@@ -13,7 +13,7 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_N_SCR = 9 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_SCR_MISC = 9, AM_N_SCR = 10 };
 
 struct am_ctx {
   int device = 0;
@@ -57,6 +57,8 @@ struct am_ctx {
   am_ctx *sub[3] = {};
   bool is_sub = false;
   hipEvent_t ev_fork = nullptr;
+  // the CRDT types present in a log's keys, by key_type array: {n_keys, 1 << type mask}
+  std::unordered_map<const void *, std::pair<uint64_t, uint32_t>> type_masks;
 };
 // sub-context i of c (created on first use; null on failure, error set)
 am_ctx *am_ctx_sub(am_ctx *c, int i);

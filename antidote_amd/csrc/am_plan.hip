@@ -53,14 +53,14 @@ __device__ __forceinline__ uint64_t in_read(am_sel in, uint64_t i) {
 }
 
 __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
-                                                   uint32_t *cnt, uint32_t *tot) {
+                                                   uint32_t *cnt, uint32_t *tot, bool write_status) {
   __shared__ uint32_t c[NCLS];
   if (threadIdx.x < NCLS) c[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
-    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), true)], 1u);
+    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), write_status)], 1u);
   }
   __syncthreads();
   if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = atomicAdd(&tot[threadIdx.x], c[threadIdx.x]);
@@ -103,6 +103,40 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
     }
     __syncthreads();
   }
+}
+
+__global__ void __launch_bounds__(PB) k_type_mask(const uint8_t *key_type, uint64_t n, uint32_t *out) {
+  uint32_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * PB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * PB) {
+    const uint32_t t = key_type[i];
+    m |= t < 32 ? 1u << t : 0u;
+  }
+  m = wave_or_u32(m);
+  if ((threadIdx.x & (WAVE - 1)) == 0 && m) atomicOr(out, m);
+}
+
+// The types present in the log's keys (one pass + readback per key_type array, cached on the
+// context).  It only picks the order of the mixed batch's chains: a stale entry (a store
+// rebuilt over a reused block) costs time, never a result.
+int log_types(am_ctx *ctx, const am_op_log *L, uint32_t *mask) {
+  auto it = ctx->type_masks.find(L->key_type);
+  if (it != ctx->type_masks.end() && it->second.first == L->n_keys) {
+    *mask = it->second.second;
+    return AM_OK;
+  }
+  void *w = nullptr;
+  if (int rc = am_ctx_scratch(ctx, AM_SCR_MISC, 256, &w)) return rc;
+  AM_HIP(hipMemsetAsync(w, 0, sizeof(uint64_t), ctx->stream));
+  const uint64_t cap = (uint64_t)ctx->n_cu * 4, nb = (L->n_keys + PB - 1) / PB;
+  if (nb) hipLaunchKernelGGL(k_type_mask, dim3((unsigned)(nb < cap ? nb : cap)), dim3(PB), 0, ctx->stream, L->key_type,
+                             L->n_keys, (uint32_t *)w);
+  AM_HIP(hipGetLastError());
+  uint64_t h = 0;
+  if (int rc = am_ctx_fetch(ctx, w, 1, &h)) return rc;
+  if (ctx->type_masks.size() >= 64) ctx->type_masks.clear();
+  ctx->type_masks[L->key_type] = {L->n_keys, (uint32_t)h};
+  *mask = (uint32_t)h;
+  return AM_OK;
 }
 
 // Short-read limit of the row tier (am_rows.hip): at most 64 ops (one 16-lane row, 4 steps)
@@ -243,78 +277,103 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   }
 
   // ---- mixed batch: the lane tier takes the short reads of every type it can in one
-  //      launch; the planner partitions the rest by class on the device ----
+  //      launch; the planner partitions the rest by class on the device.  The set types'
+  //      chains run on the sub-contexts' streams (one per type, own scratch), the scalar
+  //      types' on this one: the chains share only the planner's selection, so one type's
+  //      tiers fill the machine while another's drain.  Bounded-counter reads never go to
+  //      the lane tier, so their chain is planned from the whole batch on its own stream
+  //      and starts beside the lane tier when the log holds bounded-counter keys (on C5
+  //      -4.5 %; run over a log without them it cost C4 13 %). ----
   const uint32_t lanes = am_lane_accept(L, R, (1u << AM_PN) | (1u << AM_LWW) | (1u << AM_AWSET) | (1u << AM_MVREG));
-  am_sel in{};
-  uint64_t n_in = n;  // reads the planner partitions
-  if (lanes) {
-    void *lscr = nullptr;
-    int rc = am_ctx_scratch(ctx, AM_SCR_SPARE, (n + 64) * sizeof(uint32_t), &lscr);
-    if (rc) return rc;
-    uint32_t *lbuf = (uint32_t *)lscr;  // [0] = 0, [1] = hand-off count, list at +64
-    AM_HIP(hipMemsetAsync(lbuf, 0, 2 * sizeof(uint32_t), ctx->stream));
-    am_retry nx;
-    nx.count = lbuf + 1;
-    nx.list = lbuf + 64;
-    rc = am_launch_lanes(ctx, L, B, R, all, nx, lanes);
-    if (rc) return rc;
-    // one counter readback: a batch of short reads (the common case) ends here instead of
-    // launching the planner and every class's kernels over empty selections
-    uint64_t hc = 0;
-    rc = am_ctx_fetch(ctx, nx.count, 1, &hc);
-    if (rc) return rc;
-    n_in = (uint32_t)hc;
-    if (n_in == 0) return AM_OK;
-    in.idx = nx.list;
-    in.range = lbuf;
-  }
-  const uint64_t n_blk = (n_in + PCHUNK - 1) / PCHUNK;
-  // scratch: [range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
-  const size_t words = 3 * NCLS + n_blk * NCLS + n + 64;
-  void *scr = nullptr;
-  int rc = am_ctx_scratch(ctx, AM_SCR_PLAN, words * sizeof(uint32_t), &scr);
-  if (rc) return rc;
-  uint32_t *range = (uint32_t *)scr;
-  uint32_t *tot = range + 2 * NCLS;
-  uint32_t *cnt = tot + NCLS;
-  uint32_t *idx = cnt + n_blk * NCLS;
-  AM_HIP(hipMemsetAsync(tot, 0, NCLS * sizeof(uint32_t), ctx->stream));
-  hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, tot);
-  AM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, ctx->stream, *L, *B, *R, in, cnt, tot, range,
-                     idx);
-  AM_HIP(hipGetLastError());
-  // The set types' chains run on the sub-contexts' streams (one per type, own scratch), the
-  // scalar types' on this one: the chains share only the planner's selection, so one type's
-  // tiers fill the machine while another's drain.  The big-read tier synchronizes its own
-  // stream once, so every chain's front is queued before the first of those waits.
   am_ctx *sub[3] = {};
   am_retry retry[3];
-  AM_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+  int rc = AM_OK;
   auto join = [&]() {
     for (am_ctx *s : sub)
       if (s && hipEventRecord(s->ev0, s->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, s->ev0, 0);
   };
-  for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t) {
+  // type t's set chain over class range `range` of selection idx, on its sub-context
+  auto start_chain = [&](uint32_t t, const uint32_t *idx, const uint32_t *range, bool forked) -> int {
     am_ctx *s = am_ctx_sub(ctx, (int)(t - AM_AWSET));
-    if (!s) rc = AM_ERR_HIP;
-    if (!rc && hipStreamWaitEvent(s->stream, ctx->ev_fork, 0) != hipSuccess) rc = AM_ERR_HIP;
-    if (rc) break;
+    if (!s) return AM_ERR_HIP;
+    if (!forked) AM_HIP(hipStreamWaitEvent(s->stream, ctx->ev_fork, 0));
     sub[t - AM_AWSET] = s;
     s->grp_hint_in = ctx->grp_hint_in;
     s->tee_a = ctx->tee_a, s->tee_b = ctx->tee_b, s->tee_g = ctx->tee_g, s->tee_shift = ctx->tee_shift;
     s->tee_done = ctx->tee_done;
     void *sr = nullptr, *sg = nullptr, *sp = nullptr;
-    rc = am_ctx_scratch(s, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &sr);
-    if (!rc) rc = am_ctx_scratch(s, AM_SCR_GRP, 2 * (n + 64) * sizeof(uint32_t), &sg);
-    if (!rc) rc = am_ctx_scratch(s, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &sp);
+    int e = am_ctx_scratch(s, AM_SCR_ROWS, (n + 64) * sizeof(uint32_t), &sr);
+    if (!e) e = am_ctx_scratch(s, AM_SCR_GRP, 2 * (n + 64) * sizeof(uint32_t), &sg);
+    if (!e) e = am_ctx_scratch(s, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &sp);
     am_sel S;
     S.idx = idx;
     S.range = range + 2 * (t - 1);
-    if (!rc)
-      rc = run_sets_front(s, L, B, R, S, t, (uint32_t *)sp, (uint32_t *)sr, (uint32_t *)sg, ((lanes >> t) & 1u) != 0,
-                          &retry[t - AM_AWSET]);
+    if (!e)
+      e = run_sets_front(s, L, B, R, S, t, (uint32_t *)sp, (uint32_t *)sr, (uint32_t *)sg, ((lanes >> t) & 1u) != 0,
+                         &retry[t - AM_AWSET]);
+    return e;
+  };
+  // the planner over selection `in` (n_in reads) on c's stream, scratch slot `slot`:
+  // [range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
+  auto plan = [&](am_ctx *c, int slot, am_sel in, uint64_t n_in, bool write_status, uint32_t **range,
+                  uint32_t **idx) -> int {
+    const uint64_t n_blk = (n_in + PCHUNK - 1) / PCHUNK;
+    void *scr = nullptr;
+    if (int e = am_ctx_scratch(c, slot, (3 * NCLS + n_blk * NCLS + n + 64) * sizeof(uint32_t), &scr)) return e;
+    *range = (uint32_t *)scr;
+    uint32_t *tot = *range + 2 * NCLS, *cnt = tot + NCLS;
+    *idx = cnt + n_blk * NCLS;
+    AM_HIP(hipMemsetAsync(tot, 0, NCLS * sizeof(uint32_t), c->stream));
+    hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, c->stream, *L, *B, *R, in, cnt, tot,
+                       write_status);
+    AM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, c->stream, *L, *B, *R, in, cnt, tot,
+                       *range, *idx);
+    AM_HIP(hipGetLastError());
+    return AM_OK;
+  };
+  am_sel in{};
+  uint64_t n_in = n;  // reads the planner partitions
+  uint32_t types = 0;
+  if (lanes && (rc = log_types(ctx, L, &types))) return rc;
+  const bool bc_early = lanes && ((types >> AM_BCOUNTER) & 1u);
+  if (lanes) {
+    void *lscr = nullptr;
+    rc = am_ctx_scratch(ctx, AM_SCR_SPARE, (n + 64) * sizeof(uint32_t), &lscr);
+    if (rc) return rc;
+    AM_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    if (bc_early) {
+      am_ctx *bs = am_ctx_sub(ctx, (int)(AM_BCOUNTER - AM_AWSET));
+      if (!bs) return AM_ERR_HIP;
+      AM_HIP(hipStreamWaitEvent(bs->stream, ctx->ev_fork, 0));
+      uint32_t *brange = nullptr, *bidx = nullptr;
+      rc = plan(bs, AM_SCR_SPARE, all, n, false, &brange, &bidx);
+      if (!rc) rc = start_chain(AM_BCOUNTER, bidx, brange, true);
+    }
+    uint32_t *lbuf = (uint32_t *)lscr;  // [0] = 0, [1] = hand-off count, list at +64
+    am_retry nx;
+    nx.count = lbuf + 1;
+    nx.list = lbuf + 64;
+    if (!rc && hipMemsetAsync(lbuf, 0, 2 * sizeof(uint32_t), ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
+    if (!rc) rc = am_launch_lanes(ctx, L, B, R, all, nx, lanes);
+    // one counter readback: a batch of short reads (the common case) ends here instead of
+    // launching the planner and every class's kernels over empty selections
+    uint64_t hc = 0;
+    if (!rc) rc = am_ctx_fetch(ctx, nx.count, 1, &hc);
+    n_in = (uint32_t)hc;
+    if (rc || n_in == 0) {
+      if (!rc && bc_early) rc = am_launch_big(sub[AM_BCOUNTER - AM_AWSET], L, B, R, AM_BCOUNTER, retry[AM_BCOUNTER - AM_AWSET]);
+      join();
+      return rc;
+    }
+    in.idx = nx.list;
+    in.range = lbuf;
   }
+  uint32_t *range = nullptr, *idx = nullptr;
+  rc = plan(ctx, AM_SCR_PLAN, in, n_in, true, &range, &idx);
+  if (!rc && hipEventRecord(ctx->ev_fork, ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
+  for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t)
+    if (t != AM_BCOUNTER || !bc_early) rc = start_chain(t, idx, range, false);
   for (uint32_t t = AM_PN; t <= AM_LWW && !rc; ++t) {
     am_sel S;
     S.idx = idx;
