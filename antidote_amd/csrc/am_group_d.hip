@@ -16,8 +16,8 @@ int AM_CAT(am_grp_launch_d, GRP_D)(am_ctx *ctx, const am_op_log *L, const am_rea
   return AM_ERR_UNSUPPORTED;
 }
 
-#ifdef AMK_PHASE_PROF
-// experiments only: read and clear the wave kernel's phase cycle sums
+#if defined(AMK_PHASE_PROF) && GRP_D == 8
+// experiments only: read and clear the wave kernel's phase cycle sums (the D = 8 build: C3)
 extern "C" int am_debug_phase_cycles(uint64_t *out) {
   unsigned long long h[8] = {0};
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(amk_grp::amk_phase_cycles), sizeof(h)) != hipSuccess) return AM_ERR_HIP;

@@ -17,8 +17,9 @@ for pair in "$@"; do
     *) cp "$src" $W/antidote_amd/csrc/$dst ;;
   esac
 done
-# objects are newer than the overlaid sources otherwise
+# objects are newer than the overlaid sources otherwise; extra flags rebuild everything
 for pair in "$@"; do dst=${pair#*=}; touch $W/antidote_amd/csrc/$dst; done
+if [ -n "${EXTRA_FLAGS:-}" ]; then touch $W/antidote_amd/csrc/*.hip; fi
 make -s -j8 -C $W/antidote_amd/csrc OUT=$W/antidote_amd HIPFLAGS_EXTRA="${EXTRA_FLAGS:-}" >/dev/null
 mkdir -p scripts/ab
 cp $W/antidote_amd/libantidote_mat.so scripts/ab/lib_$NAME.so
