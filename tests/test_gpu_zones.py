@@ -114,3 +114,68 @@ def test_gpu_zone_fresh_exact_blocks(mat, t):
                 assert skipped > 0  # the clock covers whole blocks
     finally:
         st.close()
+
+
+@pytest.mark.parametrize("t", [abi.AM_AWSET, abi.AM_MVREG])
+def test_gpu_zone_cached_aligned_blocks(mat, t):
+    """Reads through the snapshot cache (read/6, the bench's cached mode) over device-generated
+    1024-op keys (aligned, exact blocks): the cache holds each key's q = 0.5 snapshot, the reads
+    come at q = 0.75, so the blocks inside the base are skipped and the others streamed.
+    Sampled keys against the oracle's materialize/4 with the q = 0.5 result as the base; the
+    counter shows skipped ops."""
+    import numpy as np
+    import torch
+    from antidote_amd import synth
+    from antidote_amd.devbatch import DeviceReads
+    from antidote_amd.oplog import HostBatch
+    from oracle import amo
+    kw = dict(n_keys=400, n_dc=8, type_=t, ops_per_key=1024)
+    if t == abi.AM_AWSET:
+        kw["universe"] = 64
+    p = synth.params(**kw)
+    st = mat.synth_store(p)
+    dlog = st.device_log()
+    hlog = synth.host_log(p, 0, p.n_keys)
+    half, clock = synth.read_clock(p, 0.5), synth.read_clock(p, 0.75)
+    pre = DeviceReads(p.n_keys, p.n_dc, t, half, set_cap=1100)
+    dr = DeviceReads(p.n_keys, p.n_dc, t, clock, set_cap=1100)
+    h = ctypes.c_void_p()
+    abi.check(mat.L.am_snapcache_create(mat.ctx, p.n_dc, p.n_keys, ctypes.byref(h)), "am_snapcache_create")
+    try:
+        b, r = pre.structs()
+        abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(dlog), ctypes.byref(b), ctypes.byref(r)), "populate")
+        torch.cuda.synchronize()
+        _skipped(mat)
+        b, r = dr.structs()
+        abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(dlog), ctypes.byref(b), ctypes.byref(r)), "read")
+        mat.sync()
+        skipped = _skipped(mat)
+        got_h = dr.host()
+        sample = np.sort(np.random.default_rng(7).choice(p.n_keys, 60, replace=False))
+        caps = [1100] * len(sample)
+        s = hlog.as_struct()
+        h0 = HostBatch(p.n_dc, [Read(int(k), t, {d: half[d] for d in range(p.n_dc)}) for k in sample], caps)
+        b0, r0 = h0.structs()
+        amo.lib().amo_materialize_range(ctypes.byref(s), ctypes.byref(b0), 0, len(sample), ctypes.byref(r0))
+        assert (h0.status[:len(sample)] == 0).all()
+        hb = HostBatch(p.n_dc, [Read(int(k), t, {d: clock[d] for d in range(p.n_dc)}) for k in sample], caps)
+        hb.base_ignore[:] = h0.last_ct_ignore
+        hb.base_vc[:] = h0.last_ct
+        hb.base_pres[:] = h0.last_ct_pres
+        hb.base_last_op[:] = h0.new_last_op
+        hb.b_v0[:], hb.b_v1[:], hb.b_vflag[:] = h0.v0, h0.v1, h0.vflag
+        hb.b_set_off, hb.b_set_len, hb.b_set_a, hb.b_set_b = h0.o_set_off, h0.o_set_len, h0.o_set_a, h0.o_set_b
+        hb._h0 = h0
+        b1, r1 = hb.structs()
+        amo.lib().amo_materialize_range(ctypes.byref(s), ctypes.byref(b1), 0, len(sample), ctypes.byref(r1))
+        vals = dr.values(sample)
+        for j, k in enumerate(sample):
+            ct = None if got_h["last_ct_ignore"][k] else {d: int(got_h["last_ct"][d, k]) for d in range(p.n_dc)
+                                                          if (int(got_h["last_ct_pres"][k]) >> d) & 1}
+            got = ("ok", vals[j], int(got_h["new_last_op"][k]), ct, bool(got_h["is_new_ss"][k]),
+                   int(got_h["count"][k]), int(got_h["flags"][k]))
+            assert got == hb.result(j), (int(k), got, hb.result(j))
+        assert skipped > 0
+    finally:
+        abi.check(mat.L.am_snapcache_destroy(h), "am_snapcache_destroy")
+        st.close()
