@@ -124,17 +124,6 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
     const uint32_t G = grouped ? am_ngrp_count(ng) : 0u;
     const uint64_t cap =
         (TYPE == AM_BCOUNTER || grouped) ? 1 : next_pow2((W > off1 - off0 ? W : off1 - off0) + nbase + 1);
-    if (TYPE == AM_BCOUNTER) {  // slots start from the base snapshot's orddicts
-      const uint32_t nd = L.n_dc, np = nd * nd;
-      for (uint32_t i = 0; i < SL.ns; ++i) {
-        uint32_t bp = 0;
-        const int64_t bv = bc_base(B, r, np, nd, i, bp);
-        const uint64_t q = (uint64_t)b * SL.ns + i;
-        SL.lo[q] = (uint64_t)bv;
-        SL.hi[q] = bv < 0 ? -1 : 0;
-        SL.pres[q] = bp;
-      }
-    }
     BigRead x;
     x.r = r, x.off0 = off0, x.off1 = off1, x.chunk0 = 0, x.rec0 = 0, x.cap = cap, x.h0 = 0, x.hmask = 2 * cap - 1;
     x.bm0 = 0, x.G = G, x.grouped = grouped ? 1u : 0u;
@@ -149,6 +138,18 @@ __global__ void k_big_prep(am_op_log L, am_read_batch B, const uint32_t *list, c
     a.min_excl = NONE;
     for (int d = 0; d < AM_MAX_DC; ++d) a.mx[d] = 0;
     acc[b] = a;
+  }
+  if (TYPE == AM_BCOUNTER) {  // slots start from the base snapshot's orddicts: one thread per slot
+    const uint32_t nd = L.n_dc, np = nd * nd;
+    const uint64_t nq = (uint64_t)nbig * SL.ns;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (uint64_t)gridDim.x * blockDim.x) {
+      const uint32_t b = (uint32_t)(q / SL.ns), i = (uint32_t)(q % SL.ns);
+      uint32_t bp = 0;
+      const int64_t bv = bc_base(B, list[b], np, nd, i, bp);
+      SL.lo[q] = (uint64_t)bv;
+      SL.hi[q] = bv < 0 ? -1 : 0;
+      SL.pres[q] = bp;
+    }
   }
 }
 
@@ -850,11 +851,18 @@ __global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch
       const uint32_t *born = G.bm + R0.bm0, *killed = born + gw;
       const uint64_t ooff = R.value.set_off[r], ocap = R.value.set_off[r + 1] - ooff;
       const uint64_t rk0 = L.rec_key_off[B.key[r]];
+      // FW consecutive words per thread: a hot key's bitmaps (tens of thousands of words) take
+      // a few rounds of loads, not one round per 256 words
+      constexpr uint32_t FW = 8;
       uint32_t base = 0;
-      for (uint32_t w0 = 0; w0 < gw; w0 += BLOCK) {
-        const uint32_t w = w0 + tid;
-        const uint32_t a = w < gw ? (born[w] & ~killed[w]) : 0u;
-        const uint32_t c = (uint32_t)__popc(a);
+      for (uint32_t w0 = 0; w0 < gw; w0 += BLOCK * FW) {
+        const uint32_t wt = w0 + tid * FW;
+        uint32_t a[FW], c = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < FW; ++k) {
+          a[k] = wt + k < gw ? (born[wt + k] & ~killed[wt + k]) : 0u;
+          c += (uint32_t)__popc(a[k]);
+        }
         const uint32_t inc = wave_incl_scan_u32(c, lane);
         if (lane == 63) s.ctr[wv] = inc;
         __syncthreads();
@@ -864,12 +872,12 @@ __global__ void __launch_bounds__(BLOCK) k_big_finish(am_op_log L, am_read_batch
           tot += s.ctr[v];
         }
         uint64_t o = base + woff + inc - c;
-        for (uint32_t bits = a; bits; bits &= bits - 1, ++o) {
-          if (o >= ocap) break;
-          const uint64_t g = (uint64_t)w * 32 + (uint32_t)__builtin_ctz(bits);
-          const u64x2 pr = *(const u64x2 *)(L.grp + 2 * (rk0 + g));
-          R.value.set_a[ooff + o] = pr.x, R.value.set_b[ooff + o] = pr.y;
-        }
+        for (uint32_t k = 0; k < FW; ++k)
+          for (uint32_t bits = a[k]; bits && o < ocap; bits &= bits - 1, ++o) {
+            const uint64_t g = (uint64_t)(wt + k) * 32 + (uint32_t)__builtin_ctz(bits);
+            const u64x2 pr = *(const u64x2 *)(L.grp + 2 * (rk0 + g));
+            R.value.set_a[ooff + o] = pr.x, R.value.set_b[ooff + o] = pr.y;
+          }
         base += tot;
         __syncthreads();
       }
@@ -1040,7 +1048,8 @@ int launch_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_
   SL.lo = (uint64_t *)((char *)meta + o_slo);
   SL.hi = (int64_t *)((char *)meta + o_shi);
   SL.pres = (uint32_t *)((char *)meta + o_spr);
-  const unsigned gp = (nbig + 255) / 256;
+  const uint64_t gq = ((uint64_t)nbig * SL.ns + 255) / 256, gcap = (uint64_t)ctx->n_cu * 8;
+  const unsigned gp = (unsigned)std::max<uint64_t>((nbig + 255) / 256, gq < gcap ? gq : gcap);
   hipLaunchKernelGGL(k_big_prep<TYPE>, dim3(gp), dim3(256), 0, ctx->stream, *L, *B, retry.list, retry.count, br, acc,
                      sz, SL);
   AM_HIP(hipGetLastError());
