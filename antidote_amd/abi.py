@@ -58,7 +58,7 @@ class am_op_log(ctypes.Structure):
         ("key_tbase", c_void_p), ("pk_vc", c_void_p),
         ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp", c_void_p),
         ("key_ngrp", c_void_p), ("key_end", c_void_p), ("rec_key_end", c_void_p), ("gmask", c_void_p),
-        ("zone_vc", c_void_p),
+        ("zone_vc", c_void_p), ("zone_gsum", c_void_p),
     ]
 
 
@@ -97,6 +97,8 @@ class am_synth_params(ctypes.Structure):
 
 AM_SYNTH_MV_BC = 6
 AM_STAT_OPS_SKIPPED = 0
+AM_STAT_RECS_SKIPPED = 1
+AM_STAT_GSUM_WORDS = 2
 AM_ZONE_OPS = 256
 AM_ERR_COLD_PATH = 5
 AM_SNAPSHOT_THRESHOLD = 10
@@ -215,7 +217,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 7:
+        if L.am_abi_version() != 8:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

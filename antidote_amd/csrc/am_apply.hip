@@ -234,7 +234,7 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   view.n_keys = m;
   view.key_off = V.off, view.key_end = V.end, view.key_id_base = V.idb, view.key_type = V.type, view.key_flags = V.flags;
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
-  view.gmask = nullptr, view.zone_vc = nullptr;
+  view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr;
   am_store *sub = nullptr;
   int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
                               false, nullptr, &sub);
@@ -361,7 +361,7 @@ int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint
   view.key_off = (uint64_t *)b, view.key_end = (uint64_t *)(b + o_end), view.key_id_base = (uint64_t *)(b + o_idb);
   view.key_type = (uint8_t *)(b + o_type), view.key_flags = (uint8_t *)(b + o_flags);
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
-  view.gmask = nullptr, view.zone_vc = nullptr;
+  view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr;
   hipLaunchKernelGGL(k_grow_view, dim3(grid_threads(n_new + 1)), dim3(256), 0, c->stream, L,
                      (const uint64_t *)st->counter, n_new, (uint64_t *)view.key_off, (uint64_t *)view.key_end,
                      (uint64_t *)view.key_id_base, (uint64_t *)(b + o_ctr), (uint8_t *)view.key_type,

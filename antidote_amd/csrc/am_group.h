@@ -575,7 +575,7 @@ struct GrpHint {
   uint32_t *pg;
   int64_t shift;       // pool word of result word o
   uint8_t *done;       // [read] its words are in the pool
-  unsigned long long *skipped;  // AM_STAT_OPS_SKIPPED (am_ctx_stat)
+  unsigned long long *skipped;  // the context's counters from AM_STAT_OPS_SKIPPED (am_ctx_stat)
   __device__ __forceinline__ void put(uint64_t o, uint64_t a, uint64_t b, uint32_t g) const {
     if (pa) {
       const uint64_t q = (uint64_t)((int64_t)o + shift);
@@ -721,6 +721,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
   ReadU<DMAX> u;
   if (!GENERAL) read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
   uint64_t n_skipped = 0;  // ops of zones inside a base snapshot (uniform)
+  uint64_t n_rskip = 0, n_gsw = 0;  // records not streamed, summary words read (uniform)
   PH_DECL();
   PH_BEGIN();
 
@@ -772,16 +773,12 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
       const uint32_t sh = (uint32_t)(off0 & (OPL - 1));
 
-      // the first record chunk is in flight while the ops are evaluated.  A chunk is 512
-      // records from the 16-byte-aligned qa: lane l holds records qa + 4 l + 256 j + {0..3}
-      // (two 16-byte loads; records outside [rk0, rk1) are masked when applied)
-      const uint64_t qa = rk0 & ~3ull;
+      // the first record chunk is in flight while the ops are evaluated (loaded after the zone
+      // test below).  A chunk is 512 records from the 16-byte-aligned qa: lane l holds records
+      // qa + 4 l + 256 j + {0..3} (two 16-byte loads; records outside [rk0, rk1) are masked when
+      // applied, and records re-applied are idempotent ORs)
+      uint64_t qa = rk0 & ~3ull;
       u32x4 rec[VRPT / 4];
-#pragma unroll
-      for (int jj = 0; jj < VRPT / 4; ++jj) {
-        const uint64_t q = qa + (uint64_t)jj * 4 * WAVE + 4 * lane;
-        rec[jj] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
-      }
       for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
 
       PH(0);
@@ -827,21 +824,45 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           off1 >= t0 + AM_ZONE_OPS) {
         zrows = (uint32_t)((off1 - t0) / AM_ZONE_OPS);  // the read's whole tiles
         if (zrows * (nd + 1) <= WAVE) {
+          // rows nd + 1, nd + 2 (group-summary offset, records end) in the same round when they fit
+          const uint32_t rows = (L.zone_gsum && zrows * (nd + 3) <= WAVE) ? nd + 3 : nd + 1;
           const uint32_t dl = lane / zrows, zl = lane % zrows;
           bool ok = true;
-          if (dl <= nd) {
+          if (dl < rows) {
             zval = L.zone_vc[(uint64_t)dl * nz + t0 / AM_ZONE_OPS + zl];
             uint64_t s0 = 0;
 #pragma unroll
             for (int d = 0; d < DMAX; ++d) s0 = (uint32_t)d == dl ? u.S[d] : s0;
-            ok = dl == nd ? zval == 1 : zval <= s0;
+            ok = dl > nd || (dl == nd ? zval == 1 : zval <= s0);
           }
           const uint64_t okm = __ballot(ok);
           zfull = zrows >= 64 ? ~0ull : ((1ull << zrows) - 1ull);
           for (uint32_t d = 0; d <= nd; ++d) zfull &= okm >> (d * zrows);
+          // the leading whole zones with group summaries: their born / killed words come from
+          // the summaries and their records are not streamed (the records start after them)
+          const uint64_t hm = __ballot(dl == nd + 1 && zval != ~0ull) >> ((nd + 1) * zrows);
+          const uint64_t f = rows > nd + 1 ? zfull & hm : 0ull;
+          const uint32_t P = f == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~f);
+          if (P) {
+            const uint32_t gw = (G + 31) / 32;
+            uint32_t bw = 0, kw = 0;
+            for (uint32_t z = 0; z < P; ++z) {
+              const uint64_t o = shfl_u64(zval, (nd + 1) * zrows + z);
+              if (lane < gw) bw |= L.zone_gsum[o + lane], kw |= L.zone_gsum[o + gw + lane];
+            }
+            if (lane < gw) s.born[lane] = bw, s.killed[lane] = kw;
+            qa = shfl_u64(zval, (nd + 2) * zrows + P - 1) & ~3ull;
+            n_rskip += qa - (rk0 & ~3ull);
+            n_gsw += (uint64_t)P * 2 * gw;
+          }
         } else {
           zrows = 0;
         }
+      }
+#pragma unroll
+      for (int jj = 0; jj < VRPT / 4; ++jj) {
+        const uint64_t q = qa + (uint64_t)jj * 4 * WAVE + 4 * lane;
+        rec[jj] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
       }
       for (uint64_t t = t0; t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
@@ -998,7 +1019,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
     }
     wave_sync();  // the slots are rewritten by the next batch
   }
-  if (n_skipped && lane == 0) atomicAdd(H.skipped, (unsigned long long)n_skipped);
+  if (n_skipped && lane == 0) atomicAdd(H.skipped + AM_STAT_OPS_SKIPPED, (unsigned long long)n_skipped);
+  if (n_rskip && lane == 0) atomicAdd(H.skipped + AM_STAT_RECS_SKIPPED, (unsigned long long)n_rskip);
+  if (n_gsw && lane == 0) atomicAdd(H.skipped + AM_STAT_GSUM_WORDS, (unsigned long long)n_gsw);
   PH_END();
 }
 
@@ -1185,7 +1208,7 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
     hipLaunchKernelGGL((k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>), dim3((unsigned)blocks), dim3(BLOCK), smem,
                        ctx->stream, *L, *B, *R, S, next, short_opl, GrpHint{ctx->grp_hint_in, ctx->tee_a, ctx->tee_b, ctx->tee_g, ctx->tee_shift,
                                                                   ctx->tee_done,
-                                                                  (unsigned long long *)(ctx->stats + AM_STAT_OPS_SKIPPED)});
+                                                                  (unsigned long long *)ctx->stats});
   } else if (tier == AM_GRP_ROW) {
     static int occ = 0;
     if (!occ) {

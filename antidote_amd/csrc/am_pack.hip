@@ -274,6 +274,74 @@ int build_records(am_store *st) {
   return AM_OK;
 }
 
+// the key holding op slot p: the last k with key_off[k] <= p
+__device__ __forceinline__ uint64_t key_of_slot(const am_op_log &L, uint64_t p) {
+  uint64_t lo = 0, hi = L.n_keys;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (L.key_off[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+// the first record of key k (records [rk0, rk1), op order) whose op is >= relative op `rel`
+__device__ __forceinline__ uint64_t rec_lower(const am_op_log &L, uint64_t rk0, uint64_t rk1, uint64_t rel) {
+  while (rk0 < rk1) {
+    const uint64_t mid = (rk0 + rk1) >> 1;
+    if (AM_REC_OP(L.rec_g[mid]) < rel) rk0 = mid + 1;
+    else rk1 = mid;
+  }
+  return rk0;
+}
+
+// zone group summaries (include/antidote_mat.h zone_gsum), pass 1, one thread per zone: the
+// summary's words (an exact zone of a grouped set key with <= AM_GRP_MAX_REC groups, else 0)
+// into cnt[z]; the zone's records end into row n_dc + 2
+__global__ void k_zsum_size(am_op_log L, uint64_t *zone, uint64_t nz, uint64_t *cnt) {
+  for (uint64_t z = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; z < nz; z += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t words = 0, rend = 0;
+    if (zone[(uint64_t)L.n_dc * nz + z] == 1) {
+      const uint64_t k = key_of_slot(L, z * AM_ZONE_OPS);
+      const uint32_t ng = L.key_ngrp[k], G = am_ngrp_count(ng);
+      const uint32_t t = L.key_type[k];
+      if ((t == AM_AWSET || t == AM_MVREG) && !am_ngrp_big(ng) && G >= 1 && G <= AM_GRP_MAX_REC) {
+        words = 2 * (uint64_t)((G + 31) / 32);
+        rend = rec_lower(L, L.rec_key_off[k], am_rkend(L, k), (z + 1) * AM_ZONE_OPS - L.key_off[k]);
+      }
+    }
+    cnt[z] = words;
+    zone[(uint64_t)(L.n_dc + 2) * nz + z] = rend;
+  }
+}
+
+// pass 2, one wave per zone: the OR of the zone's records into LDS bitmaps, written at the
+// scanned offset (row n_dc + 1 = that offset, or ~0)
+__global__ void __launch_bounds__(256) k_zsum_fill(am_op_log L, uint64_t *zone, uint64_t nz, const uint64_t *off,
+                                                   uint32_t *gsum) {
+  __shared__ uint32_t bits[4][2 * (AM_GRP_MAX_REC / 32)];
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+  uint32_t *bw = bits[wv];
+  const uint64_t waves = (uint64_t)gridDim.x * 4;
+  for (uint64_t z = (uint64_t)blockIdx.x * 4 + wv; z < nz; z += waves) {
+    const uint64_t o = off[z], words = off[z + 1] - o;
+    if (lane == 0) zone[(uint64_t)(L.n_dc + 1) * nz + z] = words ? o : ~0ull;
+    if (!words) continue;
+    const uint32_t gw = (uint32_t)(words / 2);
+    const uint64_t k = key_of_slot(L, z * AM_ZONE_OPS);
+    const uint64_t r0 = rec_lower(L, L.rec_key_off[k], am_rkend(L, k), z * AM_ZONE_OPS - L.key_off[k]);
+    const uint64_t r1 = zone[(uint64_t)(L.n_dc + 2) * nz + z];
+    for (uint32_t w = lane; w < 2 * gw; w += WAVE) bw[w] = 0;
+    wave_sync();
+    for (uint64_t q = r0 + lane; q < r1; q += WAVE) {
+      const uint32_t x = L.rec_g[q], g = AM_REC_GRP(x);
+      atomicOr(bw + ((x & AM_REC_KILL) ? gw : 0u) + (g >> 5), 1u << (g & 31));
+    }
+    wave_sync();
+    for (uint32_t w = lane; w < 2 * gw; w += WAVE) gsum[o + w] = bw[w];
+    wave_sync();
+  }
+}
+
 // the zone map of a device store (every op column written)
 int build_zones(am_store *st) {
   am_ctx *c = st->ctx;
@@ -282,12 +350,57 @@ int build_zones(am_store *st) {
   const uint64_t stride = d.snap_stride ? d.snap_stride : d.n_ops;
   const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
   void *zb = nullptr;
-  if (int rc = am_dev_alloc(c, (size_t)(d.n_dc + 1) * nz * 8 + 8, &zb)) return rc;  // + the exactness row
+  // rows: maxima, the exactness mark, the group-summary offset, the records end
+  if (int rc = am_dev_alloc(c, (size_t)(d.n_dc + 3) * nz * 8 + 8, &zb)) return rc;
   st->allocs.push_back(zb);
   const uint64_t blocks = (nz + 3) / 4 < 65536 ? (nz + 3) / 4 : 65536;
   hipLaunchKernelGGL(k_zone, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz);
   AM_HIP(hipGetLastError());
   d.zone_vc = (const uint64_t *)zb;
+  if (!d.rec_g || !d.key_ngrp || !d.rec_key_off || !d.pk_vc) return AM_OK;
+  // group summaries: sizes, exclusive scan, fill
+  uint64_t *cnt = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_b = 0;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(c->stream);
+    am_dev_release(c, cnt);
+    am_dev_release(c, tmp);
+  };
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_b, cnt, cnt, nz + 1, c->stream) != hipSuccess) {
+    am_set_error("zone summaries: scan sizing failed");
+    return AM_ERR_HIP;
+  }
+  if (am_dev_alloc(c, (nz + 1) * 8, (void **)&cnt) || am_dev_alloc(c, tmp_b + 16, &tmp)) {
+    cleanup();
+    am_set_error("zone summaries: out of device memory");
+    return AM_ERR_NOMEM;
+  }
+  uint64_t total = 0;
+  bool ok = hipMemsetAsync(cnt + nz, 0, 8, c->stream) == hipSuccess;
+  if (ok) {
+    hipLaunchKernelGGL(k_zsum_size, dim3(grid_of(nz)), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz, cnt);
+    ok = hipGetLastError() == hipSuccess &&
+         hipcub::DeviceScan::ExclusiveSum(tmp, tmp_b, cnt, cnt, nz + 1, c->stream) == hipSuccess &&
+         hipMemcpyAsync(&total, cnt + nz, 8, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+         hipStreamSynchronize(c->stream) == hipSuccess;
+  }
+  void *gs = nullptr;
+  if (ok && total) {
+    ok = am_dev_alloc(c, total * 4 + 16, &gs) == AM_OK;
+    if (ok) st->allocs.push_back(gs);
+  }
+  if (ok) {
+    hipLaunchKernelGGL(k_zsum_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz, cnt,
+                       (uint32_t *)gs);
+    ok = hipGetLastError() == hipSuccess;
+  }
+  cleanup();
+  if (!ok) {
+    am_set_error("zone summaries: build pass failed");
+    return AM_ERR_HIP;
+  }
+  d.zone_gsum = total ? (const uint32_t *)gs : nullptr;
   return AM_OK;
 }
 

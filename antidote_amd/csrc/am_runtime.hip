@@ -75,7 +75,7 @@ int am_ctx_sync(am_ctx *c) {
 }
 
 int am_ctx_stat(am_ctx *c, int which, uint64_t *value, int reset) {
-  if (!c || !value || which != AM_STAT_OPS_SKIPPED) return AM_ERR_INVALID;
+  if (!c || !value || which < AM_STAT_OPS_SKIPPED || which > AM_STAT_GSUM_WORDS) return AM_ERR_INVALID;
   AM_LOCK(c);
   AM_HIP(hipSetDevice(c->device));
   if (int rc = am_ctx_fetch(c, c->stats + which, 1, value)) return rc;

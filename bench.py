@@ -468,10 +468,14 @@ def main():
     #      each timed with HIP events on the library's stream ----
     kern_iters = max(5, args.steps)
 
-    def stat(reset):
+    def stat(reset, which=abi.AM_STAT_OPS_SKIPPED):
         v = ctypes.c_uint64()
-        abi.check(mat.L.am_ctx_stat(mat.ctx, abi.AM_STAT_OPS_SKIPPED, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
+        abi.check(mat.L.am_ctx_stat(mat.ctx, which, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
         return float(v.value)
+
+    def stats3(reset):
+        return np.array([stat(reset, w) for w in (abi.AM_STAT_OPS_SKIPPED, abi.AM_STAT_RECS_SKIPPED,
+                                                  abi.AM_STAT_GSUM_WORDS)])
 
     def event_ms(fn, pre_fn=None):
         if pre_fn is not None:
@@ -483,20 +487,21 @@ def main():
         abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms_)), "timer")
         return float(ms_.value)
 
-    skipped = 0.0
+    zs = np.zeros(3)  # per launch: ops skipped by the zone map, records skipped, summary words read
     if args.base == "cached":
         step_ev = [event_ms(lambda: (gst(), cached_read()), populate) for _ in range(args.steps)]
         kern_ev = []
         for _ in range(kern_iters):
             populate()
-            stat(True)
+            stats3(True)
             kern_ev.append(event_ms(cached_read))
-            skipped += stat(False) / kern_iters  # ops of zones inside the reads' base snapshots
+            zs += stats3(False) / kern_iters  # ops of zones inside the reads' base snapshots
     else:
         step_ev = [event_ms(step) for _ in range(args.steps)]
-        stat(True)
+        stats3(True)
         kern_ev = [event_ms(lambda: materialize(mat, dlog, reads)) for _ in range(kern_iters)]
-        skipped = stat(False) / kern_iters  # ops of exact zones inside the read clock
+        zs = stats3(False) / kern_iters  # ops of exact zones inside the read clock
+    skipped, rskip, gsw = (float(x) for x in zs)
     kern_ms = float(np.mean(kern_ev))
     packed = bool(dlog.pk_vc)
     alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed, mat)
@@ -506,6 +511,9 @@ def main():
     # an exact zone inside the read clock) are not streamed (zone map): counted out of
     # the layout bytes, reported as ops_skipped_per_launch
     alg_bytes -= skipped * bytes_per_vc(cfg["n_dc"], packed)
+    # the records of whole zones whose group summaries stood in for them: 4 B per record out,
+    # 4 B per summary word in
+    alg_bytes += 4.0 * (gsw - rskip)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     logical = logical_bytes(cfg, dlog, ko, kt, reads, cached=args.base == "cached")
 
@@ -551,7 +559,8 @@ def main():
                                  "bytes_per_s": logical / (kern_ms * 1e-3),
                                  "frac_of_peak": logical / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
                      "alg_bytes_per_launch": alg_bytes,
-                     "ops_skipped_per_launch": skipped,
+                     "ops_skipped_per_launch": skipped, "records_skipped_per_launch": rskip,
+                     "gsum_words_per_launch": gsw,
                      "layout": "packed (u32 commit vectors relative to a per-key time base); set effects as u32 token-group records"
                      if packed else "full"},
         "cpu_baseline": None,

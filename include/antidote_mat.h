@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 7
+#define AM_ABI_VERSION 8
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -217,8 +217,16 @@ typedef struct am_op_log {
    * of one key, none escaped from the packed view or invalid, and the bound is their maximum
    * (built so; an in-place apply clears the mark of the blocks it touches).  A read whose clock
    * covers an exact block's bound includes every op of it: its inclusion bits, count and
-   * LastOpCt maxima come from the mark and the bound, without the ops' commit vectors. */
+   * LastOpCt maxima come from the mark and the bound, without the ops' commit vectors.
+   * Rows n_dc + 1 and n_dc + 2 (zone_gsum non-NULL): an exact block of a grouped add-wins-set
+   * / MV-register key with at most AM_GRP_MAX_REC groups has its group summary at word
+   * zone_vc[(n_dc + 1) * n_zones + z] of zone_gsum (else ~0), and its records end (exclusive,
+   * a rec_g index) at zone_vc[(n_dc + 2) * n_zones + z]. */
   const uint64_t *zone_vc;
+  /* Zone group summaries (device stores, or NULL): for such a block, ceil(G/32) born words then
+   * ceil(G/32) killed words over the key's G groups -- the OR of its ops' token-group records,
+   * so a read including the whole block sets those bits without streaming its records. */
+  const uint32_t *zone_gsum;
 } am_op_log;
 #define AM_ZONE_OPS 256u
 #define AM_GMASK_MAX_GRP 32u
@@ -323,6 +331,10 @@ int am_timer_stop(am_ctx *ctx, float *ms);   /* records, syncs, returns elapsed 
  * commit vectors a read did not stream because their zone is inside its base snapshot
  * (am_op_log.zone_vc).  reset != 0 zeroes the counter after reading it. */
 #define AM_STAT_OPS_SKIPPED 0
+/* token-group records a read did not stream because their zones' group summaries stood in
+ * for them (am_op_log.zone_gsum), and the summary words it read instead */
+#define AM_STAT_RECS_SKIPPED 1
+#define AM_STAT_GSUM_WORDS 2
 int am_ctx_stat(am_ctx *ctx, int which, uint64_t *value, int reset);
 
 /* ---- device memory helpers (the NIF owns no framework allocator) ---- */

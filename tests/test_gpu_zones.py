@@ -25,9 +25,9 @@ def mat():
     m.close()
 
 
-def _skipped(mat, reset=True):
+def _skipped(mat, reset=True, which=abi.AM_STAT_OPS_SKIPPED):
     v = ctypes.c_uint64()
-    abi.check(mat.L.am_ctx_stat(mat.ctx, abi.AM_STAT_OPS_SKIPPED, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
+    abi.check(mat.L.am_ctx_stat(mat.ctx, which, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
     return v.value
 
 
@@ -73,7 +73,9 @@ def test_gpu_zone_skip_cached_reads(mat, t, n_dc):
 def test_gpu_zone_fresh_exact_blocks(mat, t):
     """Fresh reads at one batch clock (the bench's step): an aligned 256-op block that is EXACT
     (one key's ops, all in the packed view) and inside the clock is included whole from its
-    zone -- bits, count and LastOpCt maxima -- without streaming its commit vectors.  Device
+    zone -- bits, count and LastOpCt maxima -- without streaming its commit vectors, and the
+    leading such blocks' born / killed groups come from their group summaries (zone_gsum)
+    without streaming their records.  Device
     generated 1024-op keys (aligned blocks), sampled keys against the oracle on the host
     regeneration; the context counter shows blocks were taken from their zones."""
     import numpy as np
@@ -96,9 +98,11 @@ def test_gpu_zone_fresh_exact_blocks(mat, t):
             dr = DeviceReads(p.n_keys, p.n_dc, t, clock, set_cap=1100)
             torch.cuda.synchronize()
             _skipped(mat)
+            _skipped(mat, which=abi.AM_STAT_RECS_SKIPPED)
             materialize(mat, dlog, dr)
             mat.sync()
             skipped = _skipped(mat)
+            rskipped = _skipped(mat, which=abi.AM_STAT_RECS_SKIPPED)
             h = dr.host()
             sample = np.sort(rng.choice(p.n_keys, 60, replace=False))
             reads = [Read(int(k), t, {d: clock[d] for d in range(p.n_dc)}) for k in sample]
@@ -112,6 +116,7 @@ def test_gpu_zone_fresh_exact_blocks(mat, t):
                 assert got == ref.result(j), (q, int(k))
             if q >= 0.75:
                 assert skipped > 0  # the clock covers whole blocks
+                assert rskipped > 0  # their records came from the zones' group summaries
     finally:
         st.close()
 
