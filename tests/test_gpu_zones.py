@@ -125,7 +125,8 @@ def test_gpu_zone_fresh_exact_blocks(mat, t):
 def test_gpu_zone_cached_aligned_blocks(mat, t):
     """Reads through the snapshot cache (read/6, the bench's cached mode) over device-generated
     1024-op keys (aligned, exact blocks): the cache holds each key's q = 0.5 snapshot, the reads
-    come at q = 0.75, so the blocks inside the base are skipped and the others streamed.
+    come at q = 0.75, so the blocks inside the base are skipped (their commit vectors, and the
+    records of the leading ones) and the others streamed.
     Sampled keys against the oracle's materialize/4 with the q = 0.5 result as the base; the
     counter shows skipped ops."""
     import numpy as np
@@ -151,10 +152,12 @@ def test_gpu_zone_cached_aligned_blocks(mat, t):
         abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(dlog), ctypes.byref(b), ctypes.byref(r)), "populate")
         torch.cuda.synchronize()
         _skipped(mat)
+        _skipped(mat, which=abi.AM_STAT_RECS_SKIPPED)
         b, r = dr.structs()
         abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(dlog), ctypes.byref(b), ctypes.byref(r)), "read")
         mat.sync()
         skipped = _skipped(mat)
+        rskipped = _skipped(mat, which=abi.AM_STAT_RECS_SKIPPED)
         got_h = dr.host()
         sample = np.sort(np.random.default_rng(7).choice(p.n_keys, 60, replace=False))
         caps = [1100] * len(sample)
@@ -181,6 +184,7 @@ def test_gpu_zone_cached_aligned_blocks(mat, t):
                    int(got_h["count"][k]), int(got_h["flags"][k]))
             assert got == hb.result(j), (int(k), got, hb.result(j))
         assert skipped > 0
+        assert rskipped > 0  # the records of the leading blocks inside the base were not streamed
     finally:
         abi.check(mat.L.am_snapcache_destroy(h), "am_snapcache_destroy")
         st.close()
