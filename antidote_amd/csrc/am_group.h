@@ -801,17 +801,34 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       const uint64_t zb = t0 / AM_ZONE_OPS, nzr = (zskip && off1 > t0) ? (off1 - 1) / AM_ZONE_OPS - zb + 1 : 0;
       const bool zbatch = zskip && nzr * nd <= (uint64_t)WAVE;
       if (zbatch) {
+        // rows nd .. nd + 2 in the same round when they fit: the leading zones inside the base
+        // that are exact zones of a grouped key (a records end) hold no included op, so their
+        // records are not streamed either
+        const bool rrows = L.zone_gsum && nzr * (nd + 3) <= (uint64_t)WAVE;
         const uint32_t dl = lane / (uint32_t)nzr, zl = lane % (uint32_t)nzr;
         bool ok = true;
+        uint64_t zr = 0;
         if (dl < nd) {
           uint64_t c0 = 0;
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) c0 = (uint32_t)d == dl ? u.C0[d] : c0;
           ok = L.zone_vc[(uint64_t)dl * nz + zb + zl] <= c0;
+        } else if (rrows && dl <= nd + 2) {
+          zr = L.zone_vc[(uint64_t)dl * nz + zb + zl];
         }
         const uint64_t okm = __ballot(ok);
         zin = nzr >= 64 ? ~0ull : ((1ull << nzr) - 1ull);
         for (uint32_t d = 0; d < nd; ++d) zin &= okm >> (d * nzr);
+        if (rrows) {
+          const uint64_t em = __ballot(dl == nd && zr == 1) >> (nd * nzr);
+          const uint64_t vm = __ballot(dl == nd + 1 && zr != ~0ull) >> ((nd + 1) * nzr);
+          const uint64_t f = zin & em & vm;
+          const uint32_t Pb = f == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~f);
+          if (Pb) {
+            const uint64_t qe = shfl_u64(zr, (nd + 2) * (uint32_t)nzr + Pb - 1) & ~3ull;
+            if (qe > qa) n_rskip += qe - qa, qa = qe;
+          }
+        }
       }
       // fresh reads (the batch clock): an aligned tile that is one EXACT zone whose bound the
       // clock covers includes every op -- its bits, count and LastOpCt maxima come from the zone,
