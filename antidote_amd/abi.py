@@ -100,6 +100,7 @@ AM_STAT_OPS_SKIPPED = 0
 AM_STAT_RECS_SKIPPED = 1
 AM_STAT_GSUM_WORDS = 2
 AM_ZONE_OPS = 256
+AM_INDEX_NONE, AM_INDEX_ZONES, AM_INDEX_EXACT, AM_INDEX_SUMMARIES = 0, 1, 2, 3
 AM_ERR_COLD_PATH = 5
 AM_SNAPSHOT_THRESHOLD = 10
 AM_SNAPCACHE_ABSENT = 0xFFFFFFFF
@@ -126,6 +127,7 @@ SIGNATURES = [
     ("am_store_create", c_int, [c_void_p, POINTER(am_op_log), POINTER(c_void_p)]),
     ("am_store_log", c_int, [c_void_p, POINTER(am_op_log)]),
     ("am_store_destroy", c_int, [c_void_p]),
+    ("am_store_index", c_int, [c_void_p, c_void_p, c_int]),
     ("am_materialize", c_int, [c_void_p, POINTER(am_op_log), POINTER(am_read_batch), POINTER(am_read_result)]),
     ("am_materialize_host", c_int, [c_void_p, c_void_p, POINTER(am_read_batch), POINTER(am_read_result)]),
     ("am_gst_local_min", c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -217,7 +219,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 8:
+        if L.am_abi_version() != 9:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

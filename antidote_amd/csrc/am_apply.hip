@@ -16,9 +16,11 @@
 //      base, the variable words (offsets rebased), the records and group pairs, the key's
 //      header (end, OpCounter, id base, type, flags, group count).
 // Readers take a key's end from key_end (am_kend), so the free slots behind it are never read.
-#include "am_internal.h"
+#include "am_wave.h"
 
 namespace {
+using amk::wave_max_u64;
+using amk::wave_sync;
 
 constexpr int WAVE_SZ = 64;
 
@@ -69,9 +71,85 @@ __global__ void k_fit(am_op_log L, am_op_log S, const uint64_t *keys, uint64_t m
   }
 }
 
+// the first record of S's key range [r0, r1) (op order) whose op is >= relative op `rel`
+__device__ __forceinline__ uint64_t rec_lower_s(const am_op_log &S, uint64_t r0, uint64_t r1, uint64_t rel) {
+  while (r0 < r1) {
+    const uint64_t mid = (r0 + r1) >> 1;
+    if (AM_REC_OP(S.rec_g[mid]) < rel) r0 = mid + 1;
+    else r1 = mid;
+  }
+  return r0;
+}
+
+// the zone index of the blocks inside store key k's op range [d0, cap_end) (room included),
+// from the rebuilt key i of S written at d0: maxima over the used slots, the exact mark (every
+// slot a used op, none escaped / invalid; zlevel >= AM_INDEX_EXACT), and the group summary
+// rewritten into the block's slot when the key's new group count fits it (else retired: row
+// n_dc + 1 = ~0).  One wave; no other key shares these blocks.
+__device__ void zone_rewrite(const am_op_log &L, const am_op_log &S, uint64_t i, uint64_t d0, uint64_t n,
+                             uint64_t cap_end, uint64_t r0, int zlevel, uint32_t lane, uint32_t *bw) {
+  const uint64_t ls = L.snap_stride ? L.snap_stride : L.n_ops, ss = S.snap_stride ? S.snap_stride : S.n_ops;
+  const uint64_t nz = (ls + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
+  const uint32_t nd = L.n_dc;
+  uint64_t *Z = const_cast<uint64_t *>(L.zone_vc);
+  const uint64_t s0 = S.key_off[i];
+  const uint32_t t = S.key_type[i];
+  const uint32_t ng = (S.rec_key_off && S.key_ngrp) ? S.key_ngrp[i] : AM_NGRP_NONE, G = am_ngrp_count(ng);
+  const bool grouped = L.zone_gsum && (t == AM_AWSET || t == AM_MVREG) && !am_ngrp_big(ng) && G >= 1 &&
+                       G <= AM_GRP_MAX_REC;
+  const uint32_t gw = (G + 31) / 32;
+  for (uint64_t z = (d0 + AM_ZONE_OPS - 1) / AM_ZONE_OPS; (z + 1) * AM_ZONE_OPS <= cap_end; ++z) {
+    const uint64_t z0 = z * AM_ZONE_OPS;
+    bool ok = zlevel >= AM_INDEX_EXACT && z0 + AM_ZONE_OPS <= d0 + n && S.pk_vc && L.pk_vc;
+    uint64_t mx[AM_MAX_DC];
+    for (uint32_t d = 0; d < nd; ++d) mx[d] = 0;
+    for (uint64_t q = z0 + lane; q < z0 + AM_ZONE_OPS; q += WAVE_SZ) {
+      if (q >= d0 + n) continue;  // free room: never read
+      const uint64_t p = s0 + (q - d0);
+      const uint32_t meta = S.op_meta[p], dc = AM_META_DC(meta);
+      const uint32_t sp = S.snap_pres ? S.snap_pres[p] : 0xFFFFFFFFu;
+      for (uint32_t d = 0; d < nd; ++d) {
+        const uint64_t x = d == dc ? S.commit_time[p] : (((sp >> d) & 1u) ? S.snap_vc[(uint64_t)d * ss + p] : 0);
+        mx[d] = x > mx[d] ? x : mx[d];
+      }
+      if (S.pk_vc && (S.pk_vc[p] == AM_PK_ESC || (meta & AM_META_BAD))) ok = false;
+    }
+    for (uint32_t d = 0; d < nd; ++d) {
+      const uint64_t m = wave_max_u64(mx[d]);
+      if (lane == 0) Z[(uint64_t)d * nz + z] = m;
+    }
+    const bool exact = __ballot(!ok) == 0;
+    if (lane == 0) Z[(uint64_t)nd * nz + z] = exact ? 1u : 0u;
+    const uint64_t slot = Z[(uint64_t)(nd + 4) * nz + z];
+    const uint64_t cap = slot >> 48, o = slot & ((1ull << 48) - 1);
+    if (!(exact && grouped && slot && 2 * (uint64_t)gw <= cap)) {
+      if (lane == 0) Z[(uint64_t)(nd + 1) * nz + z] = ~0ull;
+      continue;
+    }
+    const uint64_t sr0 = S.rec_key_off[i], sr1 = am_rkend(S, i);
+    const uint64_t rb = rec_lower_s(S, sr0, sr1, z0 - d0), re = rec_lower_s(S, sr0, sr1, z0 + AM_ZONE_OPS - d0);
+    for (uint32_t w = lane; w < 2 * gw; w += WAVE_SZ) bw[w] = 0;
+    wave_sync();
+    for (uint64_t q = rb + lane; q < re; q += WAVE_SZ) {
+      const uint32_t x = S.rec_g[q], g = AM_REC_GRP(x);
+      if (x != 0xFFFFFFFFu) atomicOr(bw + ((x & AM_REC_KILL) ? gw : 0u) + (g >> 5), 1u << (g & 31));
+    }
+    wave_sync();
+    uint32_t *gs = const_cast<uint32_t *>(L.zone_gsum);
+    for (uint32_t w = lane; w < 2 * gw; w += WAVE_SZ) gs[o + w] = bw[w];
+    if (lane == 0) {
+      Z[(uint64_t)(nd + 1) * nz + z] = o;
+      Z[(uint64_t)(nd + 2) * nz + z] = r0 + (re - sr0);
+      Z[(uint64_t)(nd + 3) * nz + z] = r0 + (rb - sr0);
+    }
+    wave_sync();
+  }
+}
+
 // one wave per touched key: S's key i -> the store's key keys[i]
-__global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter, uint64_t *counter,
-                            const uint64_t *keys, uint64_t m) {
+__global__ void __launch_bounds__(256) k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter,
+                                                   uint64_t *counter, const uint64_t *keys, uint64_t m, int zlevel) {
+  __shared__ uint32_t zbits[4][2 * (AM_GRP_MAX_REC / 32)];  // per wave: a block's summary being rebuilt
   const uint32_t lane = threadIdx.x & (WAVE_SZ - 1);
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE_SZ);
   const uint64_t ls = L.snap_stride ? L.snap_stride : L.n_ops, ss = S.snap_stride ? S.snap_stride : S.n_ops;
@@ -100,22 +178,22 @@ __global__ void k_writeback(am_op_log L, am_op_log S, const uint64_t *s_counter,
           const_cast<uint32_t *>(L.pk_vc)[(uint64_t)d * ls + q] = S.pk_vc[(uint64_t)d * ss + p];
       if (L.var_off) const_cast<uint64_t *>(L.var_off)[q] = vb + (S.var_off ? S.var_off[p] - sv0 : 0);
       if (L.gmask) const_cast<uint64_t *>(L.gmask)[q] = S.gmask ? S.gmask[p] : 0;
-      if (L.zone_vc) {  // the zone map stays an upper bound of the ops written into it
+      const uint64_t zq = q / AM_ZONE_OPS;
+      if (L.zone_vc && !(zq * AM_ZONE_OPS >= d0 && (zq + 1) * AM_ZONE_OPS <= cap_end)) {
+        // a block shared with another key: its bound stays an upper bound of the ops written
         const uint64_t nz = (ls + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
         const uint32_t dc = AM_META_DC(S.op_meta[p]), sp = S.snap_pres ? S.snap_pres[p] : 0xFFFFFFFFu;
         for (uint32_t d = 0; d < L.n_dc; ++d) {
           const uint64_t x = d == dc ? S.commit_time[p] : (((sp >> d) & 1u) ? S.snap_vc[(uint64_t)d * ss + p] : 0);
-          atomicMax((unsigned long long *)const_cast<uint64_t *>(L.zone_vc) + (uint64_t)d * nz + q / AM_ZONE_OPS,
+          atomicMax((unsigned long long *)const_cast<uint64_t *>(L.zone_vc) + (uint64_t)d * nz + zq,
                     (unsigned long long)x);
         }
       }
     }
     for (uint64_t q = d0 + n + lane; L.gmask && q < cap_end; q += WAVE_SZ) const_cast<uint64_t *>(L.gmask)[q] = 0;
-    if (L.zone_vc && cap_end > d0) {  // the key's blocks are no longer exact (ops replaced in place)
-      const uint64_t nz = (ls + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
-      uint64_t *ex = const_cast<uint64_t *>(L.zone_vc) + (uint64_t)L.n_dc * nz;
-      for (uint64_t z = d0 / AM_ZONE_OPS + lane; z <= (cap_end - 1) / AM_ZONE_OPS; z += WAVE_SZ) ex[z] = 0;
-    }
+    if (L.zone_vc)  // the blocks inside the key: maxima, marks and summaries recomputed
+      zone_rewrite(L, S, i, d0, n, cap_end, L.rec_key_off ? L.rec_key_off[k] : 0, zlevel, lane,
+                   zbits[threadIdx.x / WAVE_SZ]);
     if (L.var_off) {
       uint64_t *vo = const_cast<uint64_t *>(L.var_off);
       for (uint64_t q = d0 + n + lane; q < cap_end; q += WAVE_SZ) vo[q] = vb + nv;  // the free slots
@@ -270,7 +348,7 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   }
   if (!rc && fit) {
     hipLaunchKernelGGL(k_writeback, dim3(grid_waves(m)), dim3(256), 0, c->stream, L, S,
-                       (const uint64_t *)sub->counter, st->counter, d_keys, m);
+                       (const uint64_t *)sub->counter, st->counter, d_keys, m, st->zone_level);
     if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
     if (!rc && h_new_len) {
       std::vector<uint64_t> so(m + 1);

@@ -313,6 +313,11 @@ __global__ void k_upd_scatter(UpdArgs A, const uint64_t *cnt, const uint64_t *vc
         O.commit_time[p] = 0;
         O.p0[p] = 0;
         O.p1[p] = 0;
+        // commit vectors too: the zone index's bounds over the room stay at the used ops
+        for (uint32_t d = 0; d < A.L.n_dc; ++d) O.snap_vc[(uint64_t)d * O.stride + p] = 0;
+        if (O.snap_pres) O.snap_pres[p] = 0;
+        if (O.pk_vc)
+          for (uint32_t d = 0; d < A.L.n_dc; ++d) O.pk_vc[(uint64_t)d * O.stride + p] = 0;
       }
       if (lane() == 0) O.key_end[k] = q;
     }

@@ -770,14 +770,20 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       const uint64_t r = uniform_u32(s.slot[j].r);
       const uint32_t G = uniform_u32(s.slot[j].G);
       if (GENERAL) read_inputs<DMAX, true, true>(L, nd, B, r, u);
-      const uint64_t t0 = off0 & ~(uint64_t)(OPL - 1);
-      const uint32_t sh = (uint32_t)(off0 & (OPL - 1));
+      // fresh reads over an exact-zone index stream tiles aligned to the zone blocks (a tile that
+      // is one exact block is taken whole); the first tile masks the slots before off0
+      const bool zal = !GENERAL && PACKED && TILE == AM_ZONE_OPS && L.zone_vc && off1 - off0 >= AM_ZONE_OPS;
+      const uint64_t t0 = off0 & ~(uint64_t)((zal ? AM_ZONE_OPS : OPL) - 1);
+      const uint32_t sh = (uint32_t)(off0 - t0);
 
       // the first record chunk is in flight while the ops are evaluated (loaded after the zone
       // test below).  A chunk is 512 records from the 16-byte-aligned qa: lane l holds records
       // qa + 4 l + 256 j + {0..3} (two 16-byte loads; records outside [rk0, rk1) are masked when
       // applied, and records re-applied are idempotent ORs)
       uint64_t qa = rk0 & ~3ull;
+      // records [qs, qe) are not streamed: their blocks' group summaries stood in for them (fresh),
+      // or their blocks are inside the base snapshot (cached: no included op)
+      uint64_t qs = ~0ull, qe = 0;
       u32x4 rec[VRPT / 4];
       for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
 
@@ -801,10 +807,10 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       const uint64_t zb = t0 / AM_ZONE_OPS, nzr = (zskip && off1 > t0) ? (off1 - 1) / AM_ZONE_OPS - zb + 1 : 0;
       const bool zbatch = zskip && nzr * nd <= (uint64_t)WAVE;
       if (zbatch) {
-        // rows nd .. nd + 2 in the same round when they fit: the leading zones inside the base
-        // that are exact zones of a grouped key (a records end) hold no included op, so their
-        // records are not streamed either
-        const bool rrows = L.zone_gsum && nzr * (nd + 3) <= (uint64_t)WAVE;
+        // rows nd .. nd + 3 in the same round when they fit: the first run of zones inside the
+        // base that are exact zones of a grouped key (records begin / end) hold no included op,
+        // so their records are not streamed either
+        const bool rrows = L.zone_gsum && nzr * (nd + 4) <= (uint64_t)WAVE;
         const uint32_t dl = lane / (uint32_t)nzr, zl = lane % (uint32_t)nzr;
         bool ok = true;
         uint64_t zr = 0;
@@ -813,7 +819,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) c0 = (uint32_t)d == dl ? u.C0[d] : c0;
           ok = L.zone_vc[(uint64_t)dl * nz + zb + zl] <= c0;
-        } else if (rrows && dl <= nd + 2) {
+        } else if (rrows && dl <= nd + 3) {
           zr = L.zone_vc[(uint64_t)dl * nz + zb + zl];
         }
         const uint64_t okm = __ballot(ok);
@@ -823,10 +829,11 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           const uint64_t em = __ballot(dl == nd && zr == 1) >> (nd * nzr);
           const uint64_t vm = __ballot(dl == nd + 1 && zr != ~0ull) >> ((nd + 1) * nzr);
           const uint64_t f = zin & em & vm;
-          const uint32_t Pb = f == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~f);
-          if (Pb) {
-            const uint64_t qe = shfl_u64(zr, (nd + 2) * (uint32_t)nzr + Pb - 1) & ~3ull;
-            if (qe > qa) n_rskip += qe - qa, qa = qe;
+          if (f) {
+            const uint32_t za = (uint32_t)__builtin_ctzll(f);
+            const uint32_t P = ~(f >> za) == 0 ? 64u - za : (uint32_t)__builtin_ctzll(~(f >> za));
+            qs = shfl_u64(zr, (nd + 3) * (uint32_t)nzr + za);
+            qe = shfl_u64(zr, (nd + 2) * (uint32_t)nzr + za + P - 1);
           }
         }
       }
@@ -837,12 +844,12 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       uint64_t zfull = 0;  // bit z - t0 / AM_ZONE_OPS: tile z is such a zone
       uint64_t zval = 0;   // this lane's bound (row d < nd)
       uint32_t zrows = 0;
-      if (!GENERAL && PACKED && L.zone_vc && !pk.never && TILE == AM_ZONE_OPS && t0 % AM_ZONE_OPS == 0 &&
-          off1 >= t0 + AM_ZONE_OPS) {
+      if (zal && !pk.never && off1 >= t0 + AM_ZONE_OPS) {
         zrows = (uint32_t)((off1 - t0) / AM_ZONE_OPS);  // the read's whole tiles
         if (zrows * (nd + 1) <= WAVE) {
-          // rows nd + 1, nd + 2 (group-summary offset, records end) in the same round when they fit
-          const uint32_t rows = (L.zone_gsum && zrows * (nd + 3) <= WAVE) ? nd + 3 : nd + 1;
+          // rows nd + 1 .. nd + 3 (group-summary offset, records end / begin) in the same round
+          // when they fit
+          const uint32_t rows = (L.zone_gsum && zrows * (nd + 4) <= WAVE) ? nd + 4 : nd + 1;
           const uint32_t dl = lane / zrows, zl = lane % zrows;
           bool ok = true;
           if (dl < rows) {
@@ -855,26 +862,31 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           const uint64_t okm = __ballot(ok);
           zfull = zrows >= 64 ? ~0ull : ((1ull << zrows) - 1ull);
           for (uint32_t d = 0; d <= nd; ++d) zfull &= okm >> (d * zrows);
-          // the leading whole zones with group summaries: their born / killed words come from
-          // the summaries and their records are not streamed (the records start after them)
+          // the first run of whole zones with group summaries: their born / killed words come
+          // from the summaries and their records are not streamed
           const uint64_t hm = __ballot(dl == nd + 1 && zval != ~0ull) >> ((nd + 1) * zrows);
           const uint64_t f = rows > nd + 1 ? zfull & hm : 0ull;
-          const uint32_t P = f == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~f);
-          if (P) {
+          if (f) {
+            const uint32_t za = (uint32_t)__builtin_ctzll(f);
+            const uint32_t P = ~(f >> za) == 0 ? 64u - za : (uint32_t)__builtin_ctzll(~(f >> za));
             const uint32_t gw = (G + 31) / 32;
             uint32_t bw = 0, kw = 0;
-            for (uint32_t z = 0; z < P; ++z) {
+            for (uint32_t z = za; z < za + P; ++z) {
               const uint64_t o = shfl_u64(zval, (nd + 1) * zrows + z);
               if (lane < gw) bw |= L.zone_gsum[o + lane], kw |= L.zone_gsum[o + gw + lane];
             }
             if (lane < gw) s.born[lane] = bw, s.killed[lane] = kw;
-            qa = shfl_u64(zval, (nd + 2) * zrows + P - 1) & ~3ull;
-            n_rskip += qa - (rk0 & ~3ull);
+            qs = shfl_u64(zval, (nd + 3) * zrows + za);
+            qe = shfl_u64(zval, (nd + 2) * zrows + za + P - 1);
             n_gsw += (uint64_t)P * 2 * gw;
           }
         } else {
           zrows = 0;
         }
+      }
+      if (qe > qs) {  // records not streamed; a leading range moves the stream's start
+        n_rskip += qe - qs;
+        if (qs <= rk0) qa = qe & ~3ull, qs = ~0ull;
       }
 #pragma unroll
       for (int jj = 0; jj < VRPT / 4; ++jj) {
@@ -934,7 +946,8 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       // ---- 2. records of included ops -> newest birth / kill per group (the next chunk's
       //      loads in flight while one chunk is applied) ----
       for (uint64_t q0 = qa;;) {
-        const uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
+        uint64_t q1 = q0 + (uint64_t)VRPT * WAVE;
+        if (q1 >= qs && q1 < qe) q1 = qe & ~3ull;  // past the records the zones stood in for
         u32x4 nxt[VRPT / 4];
 #pragma unroll
         for (int jj = 0; jj < VRPT / 4; ++jj) {
@@ -1261,10 +1274,17 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
 
 // kernel variants: the fast path (full clocks, no TxIds / bases / op ids: GENERAL false)
 // over the packed view, with the n_dc == D case specialised; everything else runs GENERAL
+// the group kernels' NewLastOp takes explicit op ids (a GC that kept non-consecutive ops) in
+// either variant, so the op_id column alone does not need the general one
+inline bool grp_batch_general(const am_op_log *L, const am_read_batch *B) {
+  return L->snap_pres || (B->txid && L->op_txid) || B->base_ignore || B->per_read_clock || B->base.v0 ||
+         B->base.set_off;
+}
+
 template <int D, int TYPE>
 int launch_v(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
              int tier) {
-  const bool general = am_batch_general(L, B), packed = am_log_packed(L);
+  const bool general = grp_batch_general(L, B), packed = am_log_packed(L);
   if (!general && packed)
     return L->n_dc == (uint32_t)D ? launch_d<D, TYPE, false, true, true>(ctx, L, B, R, S, next, tier)
                                   : launch_d<D, TYPE, false, true, false>(ctx, L, B, R, S, next, tier);

@@ -93,7 +93,11 @@ struct am_store {
   std::vector<void *> allocs;    // owned device allocations
   uint64_t *counter = nullptr;   // [n_keys] OpCounter (ops-cache tuple element 3) after
                                  // am_store_update; null => the newest op's id
+  int zone_level = AM_INDEX_SUMMARIES;  // the zone index it keeps (am_store_index)
 };
+// zone_vc rows after the n_dc maxima: exact mark, summary offset, records end, records begin,
+// summary slot (include/antidote_mat.h)
+constexpr uint32_t AM_ZONE_EXTRA_ROWS = 5;
 
 void am_set_error(const char *fmt, ...);
 

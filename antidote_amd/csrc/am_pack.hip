@@ -128,8 +128,9 @@ __global__ void k_rec_key_off(const uint64_t *key_off, const uint64_t *key_end, 
 
 // the zone map (include/antidote_mat.h zone_vc): one wave per block of AM_ZONE_OPS op slots,
 // the max of every op's commit vector X per DC (X[commit dc] = commit_time; a snapshot entry
-// the op does not carry reads as 0, as in is_op_in_snapshot/7)
-__global__ void k_zone(am_op_log L, uint64_t *zone, uint64_t nz) {
+// the op does not carry reads as 0, as in is_op_in_snapshot/7); with `exact_on`, row n_dc marks
+// the exact blocks
+__global__ void k_zone(am_op_log L, uint64_t *zone, uint64_t nz, int exact_on) {
   const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
@@ -150,7 +151,7 @@ __global__ void k_zone(am_op_log L, uint64_t *zone, uint64_t nz) {
     }
     // exact: every slot a used op of the block's first key, in the packed view, valid
     const uint64_t z0 = z * AM_ZONE_OPS, z1 = z0 + AM_ZONE_OPS;
-    bool exact = z1 <= L.n_ops && L.pk_vc && L.key_tbase;
+    bool exact = exact_on && z1 <= L.n_ops && L.pk_vc && L.key_tbase;
     if (exact) {
       uint64_t lo = 0, hi = L.n_keys;  // the key holding slot z0: last k with key_off[k] <= z0
       while (hi - lo > 1) {
@@ -294,28 +295,46 @@ __device__ __forceinline__ uint64_t rec_lower(const am_op_log &L, uint64_t rk0, 
   return rk0;
 }
 
+// the summary capacity (words) of the blocks of key k: a vnode store (room for appends) sizes
+// it for the key's groups to grow by a quarter + 32 before a rewrite no longer fits
+__device__ __forceinline__ uint64_t zsum_cap_words(const am_op_log &L, uint32_t G) {
+  uint32_t gc = G;
+  if (L.key_end) {
+    gc = G + G / 4 + 32;
+    gc = gc > AM_GRP_MAX_REC ? AM_GRP_MAX_REC : gc;
+  }
+  return 2 * (uint64_t)((gc + 31) / 32);
+}
+
 // zone group summaries (include/antidote_mat.h zone_gsum), pass 1, one thread per zone: the
-// summary's words (an exact zone of a grouped set key with <= AM_GRP_MAX_REC groups, else 0)
-// into cnt[z]; the zone's records end into row n_dc + 2
+// block's summary slot (a block inside the op range, room included, of a grouped set key with
+// <= AM_GRP_MAX_REC groups) into cnt[z]; an exact block's records begin / end into rows
+// n_dc + 3 / n_dc + 2
 __global__ void k_zsum_size(am_op_log L, uint64_t *zone, uint64_t nz, uint64_t *cnt) {
   for (uint64_t z = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; z < nz; z += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t words = 0, rend = 0;
-    if (zone[(uint64_t)L.n_dc * nz + z] == 1) {
-      const uint64_t k = key_of_slot(L, z * AM_ZONE_OPS);
+    uint64_t words = 0, rend = 0, rbeg = 0;
+    const uint64_t z0 = z * AM_ZONE_OPS;
+    if (z0 < L.key_off[L.n_keys]) {
+      const uint64_t k = key_of_slot(L, z0);
       const uint32_t ng = L.key_ngrp[k], G = am_ngrp_count(ng);
       const uint32_t t = L.key_type[k];
-      if ((t == AM_AWSET || t == AM_MVREG) && !am_ngrp_big(ng) && G >= 1 && G <= AM_GRP_MAX_REC) {
-        words = 2 * (uint64_t)((G + 31) / 32);
-        rend = rec_lower(L, L.rec_key_off[k], am_rkend(L, k), (z + 1) * AM_ZONE_OPS - L.key_off[k]);
+      if ((t == AM_AWSET || t == AM_MVREG) && !am_ngrp_big(ng) && G >= 1 && G <= AM_GRP_MAX_REC &&
+          z0 + AM_ZONE_OPS <= L.key_off[k + 1]) {
+        words = zsum_cap_words(L, G);
+        if (zone[(uint64_t)L.n_dc * nz + z] == 1) {
+          rend = rec_lower(L, L.rec_key_off[k], am_rkend(L, k), z0 + AM_ZONE_OPS - L.key_off[k]);
+          rbeg = rec_lower(L, L.rec_key_off[k], am_rkend(L, k), z0 - L.key_off[k]);
+        }
       }
     }
     cnt[z] = words;
     zone[(uint64_t)(L.n_dc + 2) * nz + z] = rend;
+    zone[(uint64_t)(L.n_dc + 3) * nz + z] = rbeg;
   }
 }
 
-// pass 2, one wave per zone: the OR of the zone's records into LDS bitmaps, written at the
-// scanned offset (row n_dc + 1 = that offset, or ~0)
+// pass 2, one wave per zone: row n_dc + 4 = the block's slot; an exact block's summary (the OR
+// of its records into LDS bitmaps) written into it, row n_dc + 1 = its offset (else ~0)
 __global__ void __launch_bounds__(256) k_zsum_fill(am_op_log L, uint64_t *zone, uint64_t nz, const uint64_t *off,
                                                    uint32_t *gsum) {
   __shared__ uint32_t bits[4][2 * (AM_GRP_MAX_REC / 32)];
@@ -323,18 +342,27 @@ __global__ void __launch_bounds__(256) k_zsum_fill(am_op_log L, uint64_t *zone, 
   uint32_t *bw = bits[wv];
   const uint64_t waves = (uint64_t)gridDim.x * 4;
   for (uint64_t z = (uint64_t)blockIdx.x * 4 + wv; z < nz; z += waves) {
-    const uint64_t o = off[z], words = off[z + 1] - o;
-    if (lane == 0) zone[(uint64_t)(L.n_dc + 1) * nz + z] = words ? o : ~0ull;
-    if (!words) continue;
-    const uint32_t gw = (uint32_t)(words / 2);
-    const uint64_t k = key_of_slot(L, z * AM_ZONE_OPS);
-    const uint64_t r0 = rec_lower(L, L.rec_key_off[k], am_rkend(L, k), z * AM_ZONE_OPS - L.key_off[k]);
+    const uint64_t o = off[z], cap = off[z + 1] - o;
+    const bool exact = zone[(uint64_t)L.n_dc * nz + z] == 1;
+    uint32_t gw = 0;
+    uint64_t k = 0;
+    if (cap && exact) {
+      k = key_of_slot(L, z * AM_ZONE_OPS);
+      gw = (am_ngrp_count(L.key_ngrp[k]) + 31) / 32;
+    }
+    const bool fill = cap && exact && 2 * (uint64_t)gw <= cap;
+    if (lane == 0) {
+      zone[(uint64_t)(L.n_dc + 4) * nz + z] = cap ? (cap << 48 | o) : 0ull;
+      zone[(uint64_t)(L.n_dc + 1) * nz + z] = fill ? o : ~0ull;
+    }
+    if (!fill) continue;
+    const uint64_t r0 = zone[(uint64_t)(L.n_dc + 3) * nz + z];
     const uint64_t r1 = zone[(uint64_t)(L.n_dc + 2) * nz + z];
     for (uint32_t w = lane; w < 2 * gw; w += WAVE) bw[w] = 0;
     wave_sync();
     for (uint64_t q = r0 + lane; q < r1; q += WAVE) {
       const uint32_t x = L.rec_g[q], g = AM_REC_GRP(x);
-      atomicOr(bw + ((x & AM_REC_KILL) ? gw : 0u) + (g >> 5), 1u << (g & 31));
+      if (x != 0xFFFFFFFFu) atomicOr(bw + ((x & AM_REC_KILL) ? gw : 0u) + (g >> 5), 1u << (g & 31));
     }
     wave_sync();
     for (uint32_t w = lane; w < 2 * gw; w += WAVE) gsum[o + w] = bw[w];
@@ -342,23 +370,32 @@ __global__ void __launch_bounds__(256) k_zsum_fill(am_op_log L, uint64_t *zone, 
   }
 }
 
-// the zone map of a device store (every op column written)
-int build_zones(am_store *st) {
+// the zone index of a device store (every op column written) at `level` (AM_INDEX_*)
+int build_zones(am_store *st, int level) {
   am_ctx *c = st->ctx;
   am_op_log &d = st->dev;
-  if (!d.commit_time || !d.op_meta || !d.n_ops || (d.n_dc && !d.snap_vc)) return AM_OK;
+  st->zone_level = level;
+  if (level <= AM_INDEX_NONE || !d.commit_time || !d.op_meta || !d.n_ops || (d.n_dc && !d.snap_vc)) return AM_OK;
   const uint64_t stride = d.snap_stride ? d.snap_stride : d.n_ops;
   const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
   void *zb = nullptr;
-  // rows: maxima, the exactness mark, the group-summary offset, the records end
-  if (int rc = am_dev_alloc(c, (size_t)(d.n_dc + 3) * nz * 8 + 8, &zb)) return rc;
+  // rows: maxima, the exactness mark, the group-summary offset, the records end / begin, the
+  // summary slot
+  const size_t rows = (size_t)d.n_dc + AM_ZONE_EXTRA_ROWS;
+  if (int rc = am_dev_alloc(c, rows * nz * 8 + 8, &zb)) return rc;
   st->allocs.push_back(zb);
+  AM_HIP(hipMemsetAsync((char *)zb + (size_t)(d.n_dc + 1) * nz * 8, 0xFF, nz * 8, c->stream));
+  AM_HIP(hipMemsetAsync((char *)zb + (size_t)(d.n_dc + 4) * nz * 8, 0, nz * 8, c->stream));
   const uint64_t blocks = (nz + 3) / 4 < 65536 ? (nz + 3) / 4 : 65536;
-  hipLaunchKernelGGL(k_zone, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz);
+  hipLaunchKernelGGL(k_zone, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz,
+                     level >= AM_INDEX_EXACT ? 1 : 0);
   AM_HIP(hipGetLastError());
   d.zone_vc = (const uint64_t *)zb;
-  if (!d.rec_g || !d.key_ngrp || !d.rec_key_off || !d.pk_vc) return AM_OK;
-  // group summaries: sizes, exclusive scan, fill
+  if (level < AM_INDEX_SUMMARIES || !d.rec_g || !d.key_ngrp || !d.rec_key_off || !d.pk_vc) {
+    AM_HIP(hipStreamSynchronize(c->stream));
+    return AM_OK;
+  }
+  // group summaries: slot sizes, exclusive scan, fill
   uint64_t *cnt = nullptr;
   void *tmp = nullptr;
   size_t tmp_b = 0;
@@ -390,7 +427,7 @@ int build_zones(am_store *st) {
     ok = am_dev_alloc(c, total * 4 + 16, &gs) == AM_OK;
     if (ok) st->allocs.push_back(gs);
   }
-  if (ok) {
+  if (ok && total) {
     hipLaunchKernelGGL(k_zsum_fill, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint64_t *)zb, nz, cnt,
                        (uint32_t *)gs);
     ok = hipGetLastError() == hipSuccess;
@@ -410,7 +447,29 @@ int build_zones(am_store *st) {
 // (am_gc.hip)
 int am_store_pack_records(am_store *st) {
   if (int rc = build_records(st)) return rc;
-  return build_zones(st);
+  return build_zones(st, st->zone_level);
+}
+
+// drop the store's zone index and rebuild it at `level`
+extern "C" int am_store_index(am_ctx *c, am_store *st, int level) {
+  if (!c || !st || st->ctx != c || level < AM_INDEX_NONE || level > AM_INDEX_SUMMARIES) return AM_ERR_INVALID;
+  AM_LOCK(c);
+  AM_HIP(hipSetDevice(c->device));
+  AM_HIP(hipStreamSynchronize(c->stream));
+  am_op_log &d = st->dev;
+  for (const void *p : {(const void *)d.zone_vc, (const void *)d.zone_gsum}) {
+    if (!p) continue;
+    for (size_t i = 0; i < st->allocs.size(); ++i)
+      if (st->allocs[i] == p) {
+        am_dev_release(c, st->allocs[i]);
+        st->allocs.erase(st->allocs.begin() + (long)i);
+        break;
+      }
+  }
+  d.zone_vc = nullptr, d.zone_gsum = nullptr;
+  if (int rc = build_zones(st, level)) return rc;
+  AM_HIP(hipStreamSynchronize(c->stream));
+  return AM_OK;
 }
 
 int am_store_pack(am_store *st) {
@@ -422,7 +481,7 @@ int am_store_pack(am_store *st) {
   if (!d.commit_time || !d.op_meta || (d.n_ops && !d.snap_vc)) return AM_OK;
   if (stride % 4 || d.snap_pres) {
     if (int rc = build_records(st)) return rc;
-    return build_zones(st);
+    return build_zones(st, st->zone_level);
   }
   void *tb = nullptr, *pk = nullptr;
   int rc = am_dev_alloc(c, d.n_keys * 8 + 8, &tb);
@@ -442,5 +501,5 @@ int am_store_pack(am_store *st) {
   d.key_tbase = (const uint64_t *)tb;
   d.pk_vc = (const uint32_t *)pk;
   if (int rc = build_records(st)) return rc;
-  return build_zones(st);
+  return build_zones(st, st->zone_level);
 }

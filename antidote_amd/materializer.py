@@ -84,6 +84,11 @@ class Store:
             if tmp_store is not None:
                 tmp_store.close()
 
+    def index(self, level: int = abi.AM_INDEX_SUMMARIES):
+        """Drop and rebuild the store's zone index at `level` (am_store_index: AM_INDEX_NONE,
+        _ZONES bounds only, _EXACT + exact marks, _SUMMARIES + group summaries, the default)."""
+        abi.check(self.mat.L.am_store_index(self.mat.ctx, self.handle, int(level)), "am_store_index")
+
     def reserve(self) -> "Store":
         """A copy with room for appends per key (am_store_reserve), the layout am_store_apply
         updates in place."""

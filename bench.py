@@ -297,18 +297,217 @@ def cpu_baseline(cfg, p, budget_s=10.0, cached=False):
                       f"C restatement of clocksi_materializer (oracle/am_oracle.c), not BEAM"}
 
 
-def load_traffic(config: str, workload: str):
-    """HBM bytes per materialize launch from the committed PMC summary, if it matches."""
+def load_traffic(config: str, workload: str, zone_index: str = "none"):
+    """HBM bytes per materialize launch from the committed PMC summary, if it matches the
+    workload and the store's zone index."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(config, d)
-        if e.get("workload") == workload:
+        if e.get("workload") == workload and e.get("zone_index", "") == zone_index:
             return e.get("calibrated_bytes_per_launch", e.get("bytes_per_launch"))
     except Exception:
         pass
     return None
+
+
+class Step:
+    """One config's store and read batch on this rank, with the GST feeding the batch clock."""
+
+    def __init__(self, mat, comm, cfg, rank, world, index_level):
+        self.mat, self.cfg = mat, cfg
+        n_dc, n_keys, type_ = cfg["n_dc"], cfg["n_keys"], cfg["type"]
+        self.p = synth_params(cfg, rank, world)
+        t0 = time.perf_counter()
+        self.store = mat.synth_store(self.p)   # generation + packed / token-group views + zone index
+        mat.sync()
+        self.build_s = time.perf_counter() - t0
+        self.index_build_ms = None
+        if index_level != abi.AM_INDEX_SUMMARIES:
+            self.store.index(index_level)
+        self.index_level = index_level
+        self.dlog = self.store.device_log()
+        self.ko, self.kt = key_columns(mat, self.dlog, n_keys)
+        self.n_ops = int(self.ko[-1])
+        # partition stable clocks (GST inputs): this rank owns partitions r, r+N, ...
+        self.clock = synth.read_clock(self.p, Q)
+        parts = [pp for pp in range(N_PARTITIONS) if (self.p.part_mask >> pp) & 1]
+        pvc = np.zeros((len(parts), n_dc), np.uint64)
+        for i, pp in enumerate(parts):
+            for d in range(n_dc):
+                off = 0 if pp == 0 else (np.uint64((pp * 7919 + d * 104729) % 997 + 1))
+                pvc[i, d] = np.uint64(self.clock[d]) + np.uint64(off)
+        self.n_parts = len(parts)
+        self.d_pvc = torch.from_numpy(pvc.view(np.int64)).cuda()
+        self.d_ppres = torch.full((len(parts),), (1 << n_dc) - 1, dtype=torch.int32, device="cuda")
+        self.lanes = torch.zeros(n_dc + 1, dtype=torch.int64, device="cuda")
+        self.last_vc = torch.zeros(n_dc, dtype=torch.int64, device="cuda")
+        self.last_pres = torch.zeros(1, dtype=torch.int32, device="cuda")
+        self.changed = torch.zeros(1, dtype=torch.uint8, device="cuda")
+        self.types = torch.from_numpy(self.kt.copy()).cuda() if type_ not in range(1, 6) else None
+        self.th = type_ if type_ in range(1, 6) else 0
+        self.reads = DeviceReads(n_keys, n_dc, self.th, self.clock, set_cap=max(cfg["set_cap"], 1), types=self.types)
+        self.comm = comm
+        self.cache = None
+        self.pre = None
+
+    def reindex(self, level):
+        """Rebuild the zone index at `level`; returns its build time (ms, wall clock)."""
+        self.mat.sync()
+        t0 = time.perf_counter()
+        self.store.index(level)
+        self.mat.sync()
+        ms = (time.perf_counter() - t0) * 1e3
+        self.dlog = self.store.device_log()
+        self.index_level = level
+        return ms
+
+    def gst(self):
+        L, ctx, nd = self.mat.L, self.mat.ctx, self.cfg["n_dc"]
+        abi.check(L.am_gst_local_min(ctx, nd, self.n_parts, self.d_pvc.data_ptr(), self.d_ppres.data_ptr(), None,
+                                     self.lanes.data_ptr()), "gst_local_min")
+        abi.check(L.am_gst_allreduce(self.comm, self.lanes.data_ptr(), nd), "gst_allreduce")
+        abi.check(L.am_gst_finalize(ctx, nd, self.lanes.data_ptr(), self.last_vc.data_ptr(), self.last_pres.data_ptr(),
+                                    0, self.reads.read_vc.data_ptr(), self.reads.read_pres.data_ptr(),
+                                    self.changed.data_ptr()), "gst_finalize")
+
+    def read(self):
+        materialize(self.mat, self.dlog, self.reads)
+
+    def step(self):
+        self.gst()
+        self.read()
+
+    # ---- cached mode: read/6 through the device snapshot cache holding q = 0.5 snapshots ----
+    def populate(self):
+        """The q = 0.5 reads that fill the snapshot cache (each key's first read caches its
+        snapshot: is_newest, >= MIN_OP_STORE_SS ops, src/materializer_vnode.erl:469-509)."""
+        cfg, mat = self.cfg, self.mat
+        if self.pre is None:
+            self.pre = DeviceReads(cfg["n_keys"], cfg["n_dc"], self.th, synth.read_clock(self.p, 0.5),
+                                   set_cap=max(cfg["set_cap"], 1), types=self.types)
+        if self.cache is not None:
+            abi.check(mat.L.am_snapcache_destroy(self.cache), "am_snapcache_destroy")
+        h = ctypes.c_void_p()
+        abi.check(mat.L.am_snapcache_create(mat.ctx, cfg["n_dc"], cfg["n_keys"], ctypes.byref(h)), "am_snapcache_create")
+        self.cache = h
+        b, r = self.pre.structs()
+        abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(self.dlog), ctypes.byref(b), ctypes.byref(r)),
+                  "am_snapcache_read (populate)")
+
+    def cached_read(self):
+        b, r = self.reads.structs()
+        abi.check(self.mat.L.am_snapcache_read(self.mat.ctx, self.cache, ctypes.byref(self.dlog), ctypes.byref(b),
+                                               ctypes.byref(r)), "am_snapcache_read")
+
+    def close(self):
+        if self.cache is not None:
+            self.mat.L.am_snapcache_destroy(self.cache)
+            self.cache = None
+        self.store.close()
+
+
+def measure(st: Step, base: str, steps: int, warmup: int, barrier, pg, timed_wall: bool = True):
+    """Time `steps` steps of one config (after `warmup`), then the read call alone.  Returns the
+    measured figures (max over ranks of the wall time when pg is given)."""
+    mat = st.mat
+
+    def stat(reset, which):
+        v = ctypes.c_uint64()
+        abi.check(mat.L.am_ctx_stat(mat.ctx, which, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
+        return float(v.value)
+
+    def stats3(reset):
+        return np.array([stat(reset, w) for w in (abi.AM_STAT_OPS_SKIPPED, abi.AM_STAT_RECS_SKIPPED,
+                                                  abi.AM_STAT_GSUM_WORDS)])
+
+    def event_ms(fn, pre_fn=None):
+        if pre_fn is not None:
+            pre_fn()
+        barrier()
+        abi.check(mat.L.am_timer_start(mat.ctx), "timer")
+        fn()
+        ms_ = ctypes.c_float()
+        abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms_)), "timer")
+        return float(ms_.value)
+
+    if base == "cached":
+        def timed_steps(k):
+            return sum(event_ms(lambda: (st.gst(), st.cached_read()), st.populate) * 1e-3 for _ in range(k))
+        timed_steps(warmup)
+        barrier()
+        dt = timed_steps(steps)
+        barrier()
+    else:
+        torch.cuda.synchronize()
+        for _ in range(warmup):
+            st.step()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st.step()
+        barrier()
+        dt = time.perf_counter() - t0
+    if pg is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        dt = float(t.item())
+    # sanity: the snapshot read used the GST and every read succeeded
+    stt = st.reads.status.cpu().numpy()
+    assert (stt == 0).all(), f"materialize returned errors: {np.unique(stt, return_counts=True)}"
+    gst_vc = st.reads.read_vc.cpu().numpy().view(np.uint64)
+    assert [int(x) for x in gst_vc] == [int(st.clock[d]) for d in range(st.cfg["n_dc"])], "GST mismatch"
+
+    kern_iters = max(5, steps)
+    zs = np.zeros(3)  # per launch: ops skipped by the zone index, records skipped, summary words read
+    if base == "cached":
+        step_ev = [event_ms(lambda: (st.gst(), st.cached_read()), st.populate) for _ in range(steps)]
+        kern_ev = []
+        for _ in range(kern_iters):
+            st.populate()
+            stats3(True)
+            kern_ev.append(event_ms(st.cached_read))
+            zs += stats3(False) / kern_iters
+    else:
+        step_ev = [event_ms(st.step) for _ in range(steps)]
+        stats3(True)
+        kern_ev = [event_ms(st.read) for _ in range(kern_iters)]
+        zs = stats3(False) / kern_iters
+    skipped, rskip, gsw = (float(x) for x in zs)
+    kern_ms = float(np.mean(kern_ev))
+    cfg = st.cfg
+    packed = bool(st.dlog.pk_vc)
+    alg_bytes = workload_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, packed, mat)
+    if base == "cached":
+        alg_bytes += cached_bytes(cfg, st.pre, st.reads)
+    # the commit vectors of ops whose zone decided them are not streamed, nor the records whose
+    # zones' group summaries stood in for them (4 B per record out, 4 B per summary word in)
+    alg_bytes -= skipped * bytes_per_vc(cfg["n_dc"], packed)
+    alg_bytes += 4.0 * (gsw - rskip)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    logical = logical_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, cached=base == "cached")
+    return {"dt": dt, "steps": steps, "step_ev": step_ev, "kern_ms": kern_ms, "kern_ms_median": float(np.median(kern_ev)),
+            "alg_bytes": alg_bytes, "achieved": achieved, "logical": logical, "skipped": skipped, "rskip": rskip,
+            "gsw": gsw, "packed": packed}
+
+
+def summary(st: Step, m, world: int, label: str):
+    """A compact record of one measured config (secondary / indexed lines)."""
+    ops = world * st.n_ops
+    return {"workload": label, "ops_per_gpu": st.n_ops, "ms_per_step": m["dt"] / m["steps"] * 1e3,
+            "ops_per_s": ops * m["steps"] / m["dt"],
+            "step_ms_hip_events_median": float(np.median(m["step_ev"])), "kernel_ms": m["kern_ms"],
+            "kernel_ms_median": m["kern_ms_median"], "alg_bytes_per_launch": m["alg_bytes"],
+            "roofline_frac": m["achieved"] / HBM_PEAK_GBS,
+            "logical_frac_of_peak": m["logical"] / (m["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "ops_skipped_per_launch": m["skipped"], "records_skipped_per_launch": m["rskip"],
+            "gsum_words_per_launch": m["gsw"], "zone_index": INDEX_NAMES[st.index_level],
+            "store_build_s": st.build_s}
+
+
+INDEX_NAMES = {abi.AM_INDEX_NONE: "none", abi.AM_INDEX_ZONES: "zones (bounds only)",
+               abi.AM_INDEX_EXACT: "zones + exact marks", abi.AM_INDEX_SUMMARIES: "zones + exact marks + group summaries"}
 
 
 def main():
@@ -321,6 +520,11 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--base", default="fresh", choices=["fresh", "cached"],
                     help="fresh: base ignore (first read); cached: base from the snapshot cache at q = 0.5")
+    ap.add_argument("--index", default="none", choices=["none", "zones", "exact", "summaries"],
+                    help="zone index of the headline store (am_store_index); the headline streams every op "
+                         "(none) unless asked otherwise")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary lines (c3: cached c3, the indexed reads and c4; single GPU only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -336,7 +540,6 @@ def main():
     torch.cuda.set_device(local_rank)
 
     cfg = CONFIGS[args.config]
-    n_dc, n_keys, type_ = cfg["n_dc"], cfg["n_keys"], cfg["type"]
     mat = Materializer(local_rank)
 
     # ---- RCCL communicator for the GST all-reduce (the only data-path collective) ----
@@ -359,168 +562,28 @@ def main():
         os.close(saved)
     abi.check(rc, "am_comm_init")
 
-    # ---- this GPU's op log, generated in HBM ----
-    p = synth_params(cfg, rank, world)
-    store = mat.synth_store(p)
-    dlog = store.device_log()
-    ko, kt = key_columns(mat, dlog, n_keys)
-    n_ops = int(ko[-1])
-
-    # ---- partition stable clocks (GST inputs): this rank owns partitions r, r+N, ... ----
-    clock = synth.read_clock(p, Q)
-    parts = [pp for pp in range(N_PARTITIONS) if (p.part_mask >> pp) & 1]
-    pvc = np.zeros((len(parts), n_dc), np.uint64)
-    for i, pp in enumerate(parts):
-        for d in range(n_dc):
-            off = 0 if pp == 0 else (np.uint64((pp * 7919 + d * 104729) % 997 + 1))
-            pvc[i, d] = np.uint64(clock[d]) + np.uint64(off)
-    d_pvc = torch.from_numpy(pvc.view(np.int64)).cuda()
-    d_ppres = torch.full((len(parts),), (1 << n_dc) - 1, dtype=torch.int32, device="cuda")
-    lanes = torch.zeros(n_dc + 1, dtype=torch.int64, device="cuda")
-    last_vc = torch.zeros(n_dc, dtype=torch.int64, device="cuda")
-    last_pres = torch.zeros(1, dtype=torch.int32, device="cuda")
-    changed = torch.zeros(1, dtype=torch.uint8, device="cuda")
-
-    types = torch.from_numpy(kt.copy()).cuda() if type_ not in range(1, 6) else None
-    reads = DeviceReads(n_keys, n_dc, type_ if type_ in range(1, 6) else 0, clock, set_cap=max(cfg["set_cap"], 1),
-                        types=types)
-    read_vc, read_pres = reads.read_vc, reads.read_pres   # the GST result is written here
-
-    def gst():
-        abi.check(mat.L.am_gst_local_min(mat.ctx, n_dc, len(parts), d_pvc.data_ptr(), d_ppres.data_ptr(), None,
-                                         lanes.data_ptr()), "gst_local_min")
-        abi.check(mat.L.am_gst_allreduce(comm, lanes.data_ptr(), n_dc), "gst_allreduce")
-        abi.check(mat.L.am_gst_finalize(mat.ctx, n_dc, lanes.data_ptr(), last_vc.data_ptr(), last_pres.data_ptr(),
-                                        0, read_vc.data_ptr(), read_pres.data_ptr(), changed.data_ptr()),
-                  "gst_finalize")
-
-    def step():
-        gst()
-        materialize(mat, dlog, reads)
-
     def barrier():
         torch.cuda.synchronize()
         mat.sync()
         if pg is not None:
             pg.barrier()
 
-    cache = [None]
+    level = {"none": abi.AM_INDEX_NONE, "zones": abi.AM_INDEX_ZONES, "exact": abi.AM_INDEX_EXACT,
+             "summaries": abi.AM_INDEX_SUMMARIES}[args.index]
+    # ---- this GPU's op log, generated in HBM ----
+    st = Step(mat, comm, cfg, rank, world, level)
     if args.base == "cached":
-        # the q = 0.5 reads that fill the snapshot cache (each key's first read caches its
-        # snapshot: is_newest, >= MIN_OP_STORE_SS ops, src/materializer_vnode.erl:469-509)
-        pre = DeviceReads(n_keys, n_dc, type_ if type_ in range(1, 6) else 0, synth.read_clock(p, 0.5),
-                          set_cap=max(cfg["set_cap"], 1), types=types)
+        st.populate()
+    m = measure(st, args.base, args.steps, args.warmup, barrier, pg)
+    if level == abi.AM_INDEX_NONE:
+        assert m["skipped"] == 0 and m["rskip"] == 0, "the op-streaming headline skipped ops"
 
-        def populate():
-            if cache[0] is not None:
-                abi.check(mat.L.am_snapcache_destroy(cache[0]), "am_snapcache_destroy")
-            h = ctypes.c_void_p()
-            abi.check(mat.L.am_snapcache_create(mat.ctx, n_dc, n_keys, ctypes.byref(h)), "am_snapcache_create")
-            cache[0] = h
-            b, r = pre.structs()
-            abi.check(mat.L.am_snapcache_read(mat.ctx, h, ctypes.byref(dlog), ctypes.byref(b), ctypes.byref(r)),
-                      "am_snapcache_read (populate)")
-
-        def cached_read():
-            b, r = reads.structs()
-            abi.check(mat.L.am_snapcache_read(mat.ctx, cache[0], ctypes.byref(dlog), ctypes.byref(b),
-                                              ctypes.byref(r)), "am_snapcache_read")
-
-        def timed_steps(k):
-            tot = 0.0
-            for _ in range(k):
-                populate()
-                barrier()
-                abi.check(mat.L.am_timer_start(mat.ctx), "timer")
-                gst()
-                cached_read()
-                ms_ = ctypes.c_float()
-                abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms_)), "timer")
-                tot += ms_.value * 1e-3
-            return tot
-
-        timed_steps(args.warmup)
-        barrier()
-        dt = timed_steps(args.steps)
-        barrier()
-    else:
-        torch.cuda.synchronize()
-        for _ in range(args.warmup):
-            step()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        barrier()
-        dt = time.perf_counter() - t0
-    if pg is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
-        pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        dt = float(t.item())
-
-    # sanity: the snapshot read used the GST and every read succeeded
-    st = reads.status.cpu().numpy()
-    assert (st == 0).all(), f"materialize returned errors: {np.unique(st, return_counts=True)}"
-    gst_vc = read_vc.cpu().numpy().view(np.uint64)
-    assert [int(x) for x in gst_vc] == [int(clock[d]) for d in range(n_dc)], "GST mismatch"
-
-    # ---- per-step HIP-event times (median and mean), and the read call alone,
-    #      each timed with HIP events on the library's stream ----
-    kern_iters = max(5, args.steps)
-
-    def stat(reset, which=abi.AM_STAT_OPS_SKIPPED):
-        v = ctypes.c_uint64()
-        abi.check(mat.L.am_ctx_stat(mat.ctx, which, ctypes.byref(v), 1 if reset else 0), "am_ctx_stat")
-        return float(v.value)
-
-    def stats3(reset):
-        return np.array([stat(reset, w) for w in (abi.AM_STAT_OPS_SKIPPED, abi.AM_STAT_RECS_SKIPPED,
-                                                  abi.AM_STAT_GSUM_WORDS)])
-
-    def event_ms(fn, pre_fn=None):
-        if pre_fn is not None:
-            pre_fn()
-        barrier()
-        abi.check(mat.L.am_timer_start(mat.ctx), "timer")
-        fn()
-        ms_ = ctypes.c_float()
-        abi.check(mat.L.am_timer_stop(mat.ctx, ctypes.byref(ms_)), "timer")
-        return float(ms_.value)
-
-    zs = np.zeros(3)  # per launch: ops skipped by the zone map, records skipped, summary words read
-    if args.base == "cached":
-        step_ev = [event_ms(lambda: (gst(), cached_read()), populate) for _ in range(args.steps)]
-        kern_ev = []
-        for _ in range(kern_iters):
-            populate()
-            stats3(True)
-            kern_ev.append(event_ms(cached_read))
-            zs += stats3(False) / kern_iters  # ops of zones inside the reads' base snapshots
-    else:
-        step_ev = [event_ms(step) for _ in range(args.steps)]
-        stats3(True)
-        kern_ev = [event_ms(lambda: materialize(mat, dlog, reads)) for _ in range(kern_iters)]
-        zs = stats3(False) / kern_iters  # ops of exact zones inside the read clock
-    skipped, rskip, gsw = (float(x) for x in zs)
-    kern_ms = float(np.mean(kern_ev))
-    packed = bool(dlog.pk_vc)
-    alg_bytes = workload_bytes(cfg, dlog, ko, kt, reads, packed, mat)
-    if args.base == "cached":
-        alg_bytes += cached_bytes(cfg, pre, reads)
-    # the commit vectors of ops whose zone decided them (cached: inside the base snapshot; fresh:
-    # an exact zone inside the read clock) are not streamed (zone map): counted out of
-    # the layout bytes, reported as ops_skipped_per_launch
-    alg_bytes -= skipped * bytes_per_vc(cfg["n_dc"], packed)
-    # the records of whole zones whose group summaries stood in for them: 4 B per record out,
-    # 4 B per summary word in
-    alg_bytes += 4.0 * (gsw - rskip)
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    logical = logical_bytes(cfg, dlog, ko, kt, reads, cached=args.base == "cached")
-
-    total_ops = world * n_ops * args.steps
-    value = total_ops / dt
+    n_dc, n_keys, type_ = cfg["n_dc"], cfg["n_keys"], cfg["type"]
+    total_ops = world * st.n_ops * args.steps
+    value = total_ops / m["dt"]
     workload = f"{args.config}: {cfg['desc']}"
     single = type_ in (abi.AM_PN, abi.AM_LWW)
+    dt, kern_ms, achieved, logical = m["dt"], m["kern_ms"], m["achieved"], m["logical"]
     out = {
         "metric": "CRDT ops materialized/sec (whole node) + % HBM peak",
         "value": value,
@@ -529,50 +592,83 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
-        "step_ms_hip_events": {"median": float(np.median(step_ev)), "mean": float(np.mean(step_ev)),
-                               "min": float(np.min(step_ev)), "n": len(step_ev)},
+        "step_ms_hip_events": {"median": float(np.median(m["step_ev"])), "mean": float(np.mean(m["step_ev"])),
+                               "min": float(np.min(m["step_ev"])), "n": len(m["step_ev"])},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": f"synthetic (counter-based splitmix64 op logs generated in HBM; seed {hex(p.seed)})",
-        "config": {"workload": workload, "keys_per_gpu": n_keys, "ops_per_gpu": n_ops, "n_dc": n_dc,
+        "data": f"synthetic (counter-based splitmix64 op logs generated in HBM; seed {hex(st.p.seed)})",
+        "config": {"workload": workload, "keys_per_gpu": n_keys, "ops_per_gpu": st.n_ops, "n_dc": n_dc,
                    "snapshot_quantile": Q, "partitions": N_PARTITIONS, "parallelism": f"partition-sharded x{world}",
                    "key_placement": "rank r holds the keys with am_key_partition(key, 64) % N == r",
                    "step": "GST min all-reduce (RCCL) + materialize all keys" if args.base == "fresh" else
                            "GST min all-reduce (RCCL) + am_snapcache_read of all keys (read/6: cached base at "
                            "q=0.5, materialize/4, write-back); cache rebuilt between steps, untimed; HIP-event "
                            "timing of each step",
-                   "base": args.base},
+                   "base": args.base, "zone_index": INDEX_NAMES[level],
+                   "store_build_s": st.build_s},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
                               "packed commit vectors 4*D per op, payload, 4 B per token-group record or 8 B per "
-                              "group-mask op, per-read metadata and outputs", "traffic": load_traffic(args.config if args.base == "fresh" else args.config + "_cached", workload),
+                              "group-mask op, per-read metadata and outputs; every op streamed (no zone index)"
+                              if level == abi.AM_INDEX_NONE else
+                              "layout bytes (DESIGN.md 4) minus the commit vectors / records the zone index stood in for",
+                     "traffic": load_traffic(args.config if args.base == "fresh" else args.config + "_cached", workload,
+                                             INDEX_NAMES[level]),
                      "kernel": ("am_snapcache_read (select + materialize tiers + store)" if args.base == "cached"
                                 else "k_stream" if single else
                                 "am_materialize (all tiers: k_stream, k_rows, k_grp_*, k_sets, k_big_*)"),
                      "kernel_ms": kern_ms,
-                     "kernel_ms_median": float(np.median(kern_ev)),
+                     "kernel_ms_median": m["kern_ms_median"],
                      "logical": {"model": "SURVEY.md 8(d) B_op / B_key (the reference's per-op record: "
                                           "8*D + 17 + P_type per op)", "bytes_per_launch": logical,
                                  "bytes_per_s": logical / (kern_ms * 1e-3),
                                  "frac_of_peak": logical / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                     "alg_bytes_per_launch": alg_bytes,
-                     "ops_skipped_per_launch": skipped, "records_skipped_per_launch": rskip,
-                     "gsum_words_per_launch": gsw,
+                     "alg_bytes_per_launch": m["alg_bytes"],
+                     "ops_skipped_per_launch": m["skipped"], "records_skipped_per_launch": m["rskip"],
+                     "gsum_words_per_launch": m["gsw"],
                      "layout": "packed (u32 commit vectors relative to a per-key time base); set effects as u32 token-group records"
-                     if packed else "full"},
+                     if m["packed"] else "full"},
         "cpu_baseline": None,
     }
+
+    secondary = world == 1 and args.config == "c3" and args.base == "fresh" and not args.no_secondary
+    if secondary:
+        sec = {}
+        ksteps = max(5, min(args.steps, 10))
+        # read/6 steady state: the same store through the snapshot cache, every op streamed
+        st.populate()
+        mc = measure(st, "cached", ksteps, 2, barrier, pg)
+        sec["c3_cached"] = summary(st, mc, world, "c3 --base cached: read/6 through the device snapshot cache "
+                                                  "(q = 0.5 bases), materialize/4, write-back")
+        # the zone index: its build cost, and what it buys a fresh and a cached read
+        ims = st.reindex(abi.AM_INDEX_SUMMARIES)
+        mi = measure(st, "fresh", ksteps, 2, barrier, pg)
+        st.populate()
+        mic = measure(st, "cached", ksteps, 2, barrier, pg)
+        out["indexed"] = {"index_build_ms": ims, "zone_index": INDEX_NAMES[abi.AM_INDEX_SUMMARIES],
+                          "note": "am_store_index rebuild (k_zone + k_zsum_size + scan + k_zsum_fill, wall clock); "
+                                  "am_store_apply keeps it current in place (DESIGN.md 4b)",
+                          "fresh": summary(st, mi, world, "c3 fresh, zone index on"),
+                          "cached": summary(st, mic, world, "c3 cached, zone index on")}
+        st.close()
+        st = None
+        # the north-star mix (BASELINE.json configs[3] per GPU)
+        s4 = Step(mat, comm, CONFIGS["c4"], rank, world, abi.AM_INDEX_NONE)
+        m4 = measure(s4, "fresh", ksteps, 2, barrier, pg)
+        sec["c4"] = summary(s4, m4, world, "c4: " + CONFIGS["c4"]["desc"])
+        s4.close()
+        out["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        p = st.p if st is not None else synth_params(cfg, rank, world)
         out["cpu_baseline"] = cpu_baseline(cfg, p, budget_s=args.cpu_budget, cached=args.base == "cached")
     if rank == 0:
         print(json.dumps(out), flush=True)
     mat.L.am_comm_destroy(comm)
-    if cache[0] is not None:
-        mat.L.am_snapcache_destroy(cache[0])
-    store.close()
+    if st is not None:
+        st.close()
     mat.close()
     if pg is not None:
         pg.destroy_process_group()

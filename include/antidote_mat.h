@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 8
+#define AM_ABI_VERSION 9
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -214,14 +214,21 @@ typedef struct am_op_log {
    * (belongs_to_snapshot_op/3), so none counts, none is applied and none bounds NewLastOp --
    * the ops already folded into the cached snapshot are not streamed again.
    * Row n_dc, zone_vc[n_dc * n_zones + z] = 1 marks an EXACT block: all its slots are used ops
-   * of one key, none escaped from the packed view or invalid, and the bound is their maximum
-   * (built so; an in-place apply clears the mark of the blocks it touches).  A read whose clock
-   * covers an exact block's bound includes every op of it: its inclusion bits, count and
-   * LastOpCt maxima come from the mark and the bound, without the ops' commit vectors.
-   * Rows n_dc + 1 and n_dc + 2 (zone_gsum non-NULL): an exact block of a grouped add-wins-set
-   * / MV-register key with at most AM_GRP_MAX_REC groups has its group summary at word
-   * zone_vc[(n_dc + 1) * n_zones + z] of zone_gsum (else ~0), and its records end (exclusive,
-   * a rec_g index) at zone_vc[(n_dc + 2) * n_zones + z]. */
+   * of one key, none escaped from the packed view or invalid, and the bound is their maximum.
+   * A read whose clock covers an exact block's bound includes every op of it: its inclusion
+   * bits, count and LastOpCt maxima come from the mark and the bound, without the ops' commit
+   * vectors.
+   * Rows n_dc + 1 .. n_dc + 3 (zone_gsum non-NULL): an exact block of a grouped add-wins-set /
+   * MV-register key with at most AM_GRP_MAX_REC groups has its group summary at word
+   * zone_vc[(n_dc + 1) * n_zones + z] of zone_gsum (else ~0 -- rows n_dc + 2 and n_dc + 3 are
+   * then meaningless), its records end (exclusive, a rec_g index) at row n_dc + 2 and its records
+   * begin at row n_dc + 3.  Row n_dc + 4 is the block's summary slot, (capacity in words << 48) |
+   * word offset, or 0: a block inside a grouped key's op range (room included) owns one, so
+   * am_store_apply can rewrite the summary in place when the block becomes exact again.
+   * Maintenance: am_store_apply recomputes, for every block inside a key it writes (room
+   * included), the exact maxima over the used slots, the mark, and the summary when the key's
+   * new group count fits the slot (else row n_dc + 1 = ~0); a block shared with another key only
+   * has its bound raised.  am_store_index drops or (re)builds the whole index. */
   const uint64_t *zone_vc;
   /* Zone group summaries (device stores, or NULL): for such a block, ceil(G/32) born words then
    * ceil(G/32) killed words over the key's G groups -- the OR of its ops' token-group records,
@@ -349,6 +356,16 @@ int am_store_create(am_ctx *ctx, const am_op_log *host_log, am_store **out);
 /* Device view of the store (pointers are device pointers). */
 int am_store_log(const am_store *st, am_op_log *out);
 int am_store_destroy(am_store *st);
+/* The zone index of a device store (am_op_log.zone_vc / zone_gsum): level AM_INDEX_NONE drops it,
+ * AM_INDEX_ZONES keeps the per-block upper bounds only (base-snapshot reads skip the blocks
+ * inside their base; no exact marks), AM_INDEX_EXACT adds the exact marks (fresh reads take an
+ * exact block inside their clock whole), AM_INDEX_SUMMARIES adds the group summaries (the
+ * default every store builder leaves).  Rebuilds from the op columns; blocks until done. */
+#define AM_INDEX_NONE 0
+#define AM_INDEX_ZONES 1
+#define AM_INDEX_EXACT 2
+#define AM_INDEX_SUMMARIES 3
+int am_store_index(am_ctx *ctx, am_store *st, int level);
 
 /* ---- the hot path ---- */
 /* Device pointers; runs on the ctx stream.  Asynchronous except for two data-dependent

@@ -16,5 +16,5 @@ def test_pmc_traffic_records_match_bench_workloads():
         cfg = key[:-len("_cached")] if key.endswith("_cached") else key  # bench.py --base cached
         assert cfg in bench.CONFIGS, key
         w = f"{cfg}: {bench.CONFIGS[cfg]['desc']}"
-        assert bench.load_traffic(key, w) == e.get("calibrated_bytes_per_launch", e["bytes_per_launch"]), key
+        assert bench.load_traffic(key, w, e["zone_index"]) == e.get("calibrated_bytes_per_launch", e["bytes_per_launch"]), key
         assert e["bytes_per_launch"] > 0
