@@ -30,9 +30,11 @@ struct ViewCols {
 };
 
 // per touched key: its range and header in the store -> the view's columns
+// (a key outside the store reads as key 0: the caller's key check fails the call before any
+// write)
 __global__ void k_view(am_op_log L, const uint64_t *counter, const uint64_t *keys, uint64_t m, ViewCols V) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = keys[i];
+    const uint64_t k = keys[i] < L.n_keys ? keys[i] : 0;
     V.off[i] = L.key_off[k];
     V.end[i] = am_kend(L, k);
     V.idb[i] = L.key_id_base ? L.key_id_base[k] : 1;
@@ -48,7 +50,7 @@ __global__ void k_thr_gather(const uint64_t *keys, uint64_t m, uint32_t n_dc, ui
                              const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *omask, uint64_t *ovc,
                              uint32_t *opres) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = keys[i];
+    const uint64_t k = keys[i] < n_keys ? keys[i] : 0;
     omask[i] = mask[k];
     opres[i] = thr_pres[k];
     for (uint32_t d = 0; d < n_dc; ++d) ovc[(uint64_t)d * m + i] = thr_vc[(uint64_t)d * n_keys + k];
@@ -60,7 +62,7 @@ __device__ __forceinline__ bool set_type(uint32_t t) { return t == AM_AWSET || t
 // does key i of the rebuilt view S fit key keys[i]'s room in L?
 __global__ void k_fit(am_op_log L, am_op_log S, const uint64_t *keys, uint64_t m, uint32_t *nofit) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = keys[i];
+    const uint64_t k = keys[i] < L.n_keys ? keys[i] : 0;
     const uint64_t c0 = L.key_off[k], c1 = L.key_off[k + 1];
     const uint64_t s0 = S.key_off[i], s1 = S.key_off[i + 1];
     bool ok = s1 - s0 + 1 <= c1 - c0;
@@ -249,17 +251,18 @@ __global__ void k_fill_ids(am_op_log L, uint64_t *op_id, uint64_t *op_txid) {
   }
 }
 
-// the caller's key list: every key in range and none twice (a claim bit per store key); bad |= 1
-// for a key >= n_keys, 2 for a repeated key
+// the caller's key list: every key in range and none twice (a claim bit per store key); bad |=
+// AM_BADKEY_RANGE for a key >= n_keys, AM_BADKEY_DUP for a repeated key
+constexpr uint32_t AM_BADKEY_RANGE = 2u, AM_BADKEY_DUP = 4u;
 __global__ void k_check_keys(const uint64_t *keys, uint64_t m, uint64_t n_keys, uint32_t *claim, uint32_t *bad) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = keys[i];
     if (k >= n_keys) {
-      atomicOr(bad, 1u);
+      atomicOr(bad, AM_BADKEY_RANGE);
       continue;
     }
     const uint32_t bit = 1u << (k & 31);
-    if (atomicOr(&claim[k >> 5], bit) & bit) atomicOr(bad, 2u);
+    if (atomicOr(&claim[k >> 5], bit) & bit) atomicOr(bad, AM_BADKEY_DUP);
   }
 }
 
@@ -268,24 +271,56 @@ unsigned grid_waves(uint64_t n) { return (unsigned)((n + 3) / 4 < 65536 ? ((n + 
 
 }  // namespace
 
+// the caller's key list checked the synchronous way (stores am_store_apply_ex does not update
+// in place)
+int check_keys_sync(am_ctx *c, const am_store *st, uint64_t m, const uint64_t *keys) {
+  const uint64_t words = (st->dev.n_keys + 31) / 32;
+  void *scr = nullptr;
+  if (int rc = am_dev_alloc(c, words * 4 + 256, &scr)) return rc;
+  uint32_t *bad = (uint32_t *)scr, *claim = bad + 64;
+  uint64_t w = 0;
+  int rc = hipMemsetAsync(scr, 0, words * 4 + 256, c->stream) == hipSuccess ? AM_OK : AM_ERR_HIP;
+  if (!rc) {
+    hipLaunchKernelGGL(k_check_keys, dim3(grid_threads(m)), dim3(256), 0, c->stream, keys, m, st->dev.n_keys, claim,
+                       bad);
+    rc = hipGetLastError() == hipSuccess ? AM_OK : AM_ERR_HIP;
+  }
+  if (!rc) rc = am_ctx_fetch(c, bad, 1, &w);
+  (void)hipStreamSynchronize(c->stream);
+  am_dev_release(c, scr);
+  if (rc) {
+    am_set_error("am_store_apply: key check failed");
+    return rc;
+  }
+  if (w & (AM_BADKEY_RANGE | AM_BADKEY_DUP)) {
+    am_set_error("am_store_apply: %s", (w & AM_BADKEY_RANGE) ? "a touched key is outside the store's key space"
+                                                             : "a touched key appears twice in the list");
+    return AM_ERR_INVALID;
+  }
+  return AM_OK;
+}
+
 int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_keys, const am_op_log *dev_new,
                    const uint8_t *d_mask_full, const uint64_t *d_thr_vc_full, const uint32_t *d_thr_pres_full,
-                   uint8_t *d_gc_flags, uint64_t *h_new_len, int *applied) {
+                   uint8_t *d_gc_flags, uint64_t *h_new_len, int *applied, bool check_keys) {
   AM_LOCK(c);
   *applied = 0;
   am_op_log &L = st->dev;
   // in place needs the slack layout with its per-key header columns and OpCounter
-  if (!L.key_end || !L.key_id_base || !st->counter || (L.rec_key_off && !L.rec_key_end) || m == 0) return AM_OK;
-  if (dev_new && (dev_new->n_keys != m || (dev_new->snap_pres && !L.snap_pres) || (dev_new->var_off && !L.var_off)))
-    return AM_OK;
+  const bool inplace = L.key_end && L.key_id_base && st->counter && !(L.rec_key_off && !L.rec_key_end) && m &&
+                       !(dev_new && (dev_new->n_keys != m || (dev_new->snap_pres && !L.snap_pres) ||
+                                     (dev_new->var_off && !L.var_off)));
+  if (!inplace) return (check_keys && m) ? check_keys_sync(c, st, m, d_keys) : AM_OK;
   AM_HIP(hipSetDevice(c->device));
   const uint64_t nd = L.n_dc;
-  // scratch: the view's columns, the gathered prune arguments, the fit flag
+  // scratch: the view's columns, the gathered prune arguments, the fit / key-check word, the
+  // key claim bitmap
   const size_t o_end = am_round_up((m + 1) * 8, 256), o_idb = o_end + am_round_up(m * 8, 256);
   const size_t o_ctr = o_idb + am_round_up(m * 8, 256), o_type = o_ctr + am_round_up(m * 8, 256);
   const size_t o_flags = o_type + am_round_up(m, 256), o_mask = o_flags + am_round_up(m, 256);
   const size_t o_tvc = o_mask + am_round_up(m, 256), o_tpres = o_tvc + am_round_up(nd * m * 8, 256);
-  const size_t o_fit = o_tpres + am_round_up(m * 4, 256), total = o_fit + 256;
+  const size_t o_fit = o_tpres + am_round_up(m * 4, 256), o_claim = o_fit + 256;
+  const size_t claim_b = check_keys ? am_round_up((L.n_keys + 31) / 32 * 4, 256) : 0, total = o_claim + claim_b + 256;
   void *scr = nullptr;
   if (int rc = am_dev_alloc(c, total, &scr)) return rc;
   char *b = (char *)scr;
@@ -299,12 +334,20 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
     am_dev_release(c, scr);
     return rc;
   };
+  if (check_keys) {  // into the fit word: one readback covers both
+    if (hipMemsetAsync(b + o_fit, 0, 256 + claim_b, c->stream) != hipSuccess) {
+      am_set_error("am_store_apply: key check failed");
+      return done(AM_ERR_HIP);
+    }
+    hipLaunchKernelGGL(k_check_keys, dim3(grid_threads(m)), dim3(256), 0, c->stream, d_keys, m, L.n_keys,
+                       (uint32_t *)(b + o_claim), nofit);
+  }
   hipLaunchKernelGGL(k_view, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, (const uint64_t *)st->counter, d_keys,
                      m, V);
   if (mask)
     hipLaunchKernelGGL(k_thr_gather, dim3(grid_threads(m)), dim3(256), 0, c->stream, d_keys, m, L.n_dc, L.n_keys,
                        d_mask_full, d_thr_vc_full, d_thr_pres_full, mask, tvc, tpres);
-  if (hipGetLastError() != hipSuccess || hipMemsetAsync(nofit, 0, 4, c->stream) != hipSuccess) {
+  if (hipGetLastError() != hipSuccess || (!check_keys && hipMemsetAsync(nofit, 0, 4, c->stream) != hipSuccess)) {
     am_set_error("am_store_apply: view failed");
     return done(AM_ERR_HIP);
   }
@@ -316,7 +359,14 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   am_store *sub = nullptr;
   int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
                               false, nullptr, &sub);
-  if (rc) return done(rc);
+  if (rc) {
+    if (check_keys) {  // a bad key list is the caller's error, whatever it did to the rebuild
+      uint64_t w = 0;
+      if (am_ctx_fetch(c, nofit, 1, &w) == AM_OK && (w & (AM_BADKEY_RANGE | AM_BADKEY_DUP))) rc = AM_ERR_INVALID;
+      if (rc == AM_ERR_INVALID) am_set_error("am_store_apply: a touched key is outside the store or repeated");
+    }
+    return done(rc);
+  }
   const am_op_log &S = sub->dev;
   bool cols = !(S.snap_pres && !L.snap_pres) && !(S.var_off && !L.var_off) && !(L.pk_vc && !S.pk_vc) &&
               !(S.rec_key_off && !L.rec_key_off) && !(S.gmask && !L.gmask);
@@ -339,12 +389,17 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
     if (tx) st->allocs.push_back(tx), L.op_txid = (const uint64_t *)tx;
   }
   uint64_t fit = 0;
-  if (cols) {
-    hipLaunchKernelGGL(k_fit, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, S, d_keys, m, nofit);
+  if (cols || check_keys) {
+    if (cols) hipLaunchKernelGGL(k_fit, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, S, d_keys, m, nofit);
     if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
     uint64_t w = 0;
     if (!rc) rc = am_ctx_fetch(c, nofit, 1, &w);
-    fit = (w & 0xFFFFFFFFull) == 0;
+    if (!rc && (w & (AM_BADKEY_RANGE | AM_BADKEY_DUP))) {
+      am_set_error("am_store_apply: %s", (w & AM_BADKEY_RANGE) ? "a touched key is outside the store's key space"
+                                                               : "a touched key appears twice in the list");
+      rc = AM_ERR_INVALID;
+    }
+    fit = cols && (w & 0xFFFFFFFFull) == 0;
   }
   if (!rc && fit) {
     hipLaunchKernelGGL(k_writeback, dim3(grid_waves(m)), dim3(256), 0, c->stream, L, S,
@@ -477,33 +532,11 @@ int am_store_apply(am_ctx *c, am_store *st, uint64_t n_touched, const uint64_t *
                  (unsigned long long)n_touched);
     return AM_ERR_INVALID;
   }
-  {  // the key list comes from the caller: in range and distinct, or nothing runs
-    AM_HIP(hipSetDevice(c->device));
-    const uint64_t words = (st->dev.n_keys + 31) / 32;
-    void *scr = nullptr;
-    if (int rc = am_dev_alloc(c, words * 4 + 256, &scr)) return rc;
-    uint32_t *bad = (uint32_t *)scr, *claim = bad + 64;
-    uint64_t w = 0;
-    int rc = hipMemsetAsync(scr, 0, words * 4 + 256, c->stream) == hipSuccess ? AM_OK : AM_ERR_HIP;
-    if (!rc) {
-      hipLaunchKernelGGL(k_check_keys, dim3(grid_threads(n_touched)), dim3(256), 0, c->stream, keys, n_touched,
-                         st->dev.n_keys, claim, bad);
-      rc = hipGetLastError() == hipSuccess ? AM_OK : AM_ERR_HIP;
-    }
-    if (!rc) rc = am_ctx_fetch(c, bad, 1, &w);
-    (void)hipStreamSynchronize(c->stream);
-    am_dev_release(c, scr);
-    if (rc) {
-      am_set_error("am_store_apply: key check failed");
-      return rc;
-    }
-    if (w & 3u) {
-      am_set_error("am_store_apply: %s", (w & 1u) ? "a touched key is outside the store's key space"
-                                                  : "a touched key appears twice in the list");
-      return AM_ERR_INVALID;
-    }
-  }
-  return am_store_apply_ex(c, st, n_touched, keys, dev_new, prune_mask, thr_vc, thr_pres, gc_flags, nullptr, applied);
+  AM_HIP(hipSetDevice(c->device));
+  // the key list comes from the caller: checked on the device (in range, distinct) inside the
+  // apply, in the fit readback it already does; nothing is written when it fails
+  return am_store_apply_ex(c, st, n_touched, keys, dev_new, prune_mask, thr_vc, thr_pres, gc_flags, nullptr, applied,
+                           true);
 }
 
 }  // extern "C"

@@ -187,7 +187,7 @@ int am_store_update_ex(am_ctx *c, const am_op_log &L, const uint64_t *counter, c
 // rebuild the whole store instead.
 int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_keys, const am_op_log *dev_new,
                    const uint8_t *d_mask_full, const uint64_t *d_thr_vc_full, const uint32_t *d_thr_pres_full,
-                   uint8_t *d_gc_flags, uint64_t *h_new_len, int *applied);
+                   uint8_t *d_gc_flags, uint64_t *h_new_len, int *applied, bool check_keys = false);
 int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint64_t *cap_hint, am_store **out);  // am_apply.hip
 struct am_snapcache;
 extern "C" int am_snapcache_grow(am_snapcache *c, uint64_t new_n);  // am_snapcache.hip (not exported in the header)

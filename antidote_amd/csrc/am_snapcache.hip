@@ -51,6 +51,10 @@ struct am_snapcache {
   uint32_t *pool_g = nullptr;                     // set pairs: token-group hint (am_ctx::grp_hint_in)
   uint64_t pool_cap = 0;                          // words
   uint64_t *ctr = nullptr;     // device [0] pool words used
+  // the last batch's stored value words end, per wave of k_sc_store (the pool counter advances
+  // to their maximum at the next batch's k_sc_sizes, not by the batch's whole result capacity)
+  uint64_t *wend = nullptr;
+  uint32_t wend_n = 0;         // entries pending (0: consumed)
   std::vector<void *> allocs;
 };
 
@@ -219,9 +223,9 @@ __device__ __forceinline__ uint32_t value_words(const am_read_result &R, uint64_
 // (tee_done[r]); k_sc_copy moves the others' from the result CSR.
 __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read_batch B, am_read_result R, ScSel S,
                                                   const uint8_t *should_gc, ScGc G, uint64_t used, uint64_t so0,
-                                                  uint64_t new_used, const uint8_t *teed) {
-  if (blockIdx.x == 0 && threadIdx.x == 0 && new_used != ~0ull) C.ctr[0] = new_used;
+                                                  uint64_t *wend, const uint8_t *teed) {
   const uint32_t nd = C.n_dc;
+  uint64_t wmax = 0;  // the end of the value words this wave stored (wend, or null: none reserved)
   const uint64_t n = B.n_reads;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
@@ -322,6 +326,11 @@ __global__ void __launch_bounds__(256) k_sc_store(ScView C, am_op_log L, am_read
       }
     }
     if (r < n) S.cp_dst[r] = off, S.cp_len[r] = (off && !(teed && teed[r])) ? w : 0u;
+    if (ins && off) wmax = off + w > wmax ? off + w : wmax;
+  }
+  if (wend) {
+    wmax = amk::wave_max_u64(wmax);
+    if ((threadIdx.x & 63u) == 0) wend[(uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = wmax;
   }
 }
 
@@ -393,11 +402,19 @@ uint64_t reserved_words(uint32_t nd) { return (uint64_t)nd * nd + nd + 1; }
 
 // a batch's sizes in one readback: the result CSR's first and last offsets and the pool
 // counters (words used, room-missing flag)
-__global__ void k_sc_sizes(const uint64_t *set_off, uint64_t n, const uint64_t *ctr, uint64_t *out) {
+// The pool counter first advances past the previous batch's stored words (the max of its
+// per-wave ends, nw of them).  One wave.
+__global__ void k_sc_sizes(const uint64_t *set_off, uint64_t n, uint64_t *ctr, const uint64_t *wend, uint32_t nw,
+                           uint64_t *out) {
+  uint64_t m = 0;
+  for (uint32_t i = threadIdx.x; i < nw; i += 64) m = wend[i] > m ? wend[i] : m;
+  m = amk::wave_max_u64(m);
   if (threadIdx.x == 0) {
+    const uint64_t used = m > ctr[0] ? m : ctr[0];
+    ctr[0] = used;
     out[0] = set_off ? set_off[0] : 0;
     out[1] = set_off ? set_off[n] : 0;
-    out[2] = ctr[0];
+    out[2] = used;
     out[3] = ctr[1];
   }
 }
@@ -535,6 +552,7 @@ int am_snapcache_create(am_ctx *ctx, uint32_t n_dc, uint64_t n_keys, am_snapcach
   if (!rc) rc = alloc(ne * 8, (void **)&c->poff);
   if (!rc) rc = alloc(ne * 4, (void **)&c->plen);
   if (!rc) rc = alloc(16, (void **)&c->ctr);
+  if (!rc) rc = alloc(4096 * 4 * 8, (void **)&c->wend);  // k_sc_store's grid (grid(): <= 4096 blocks of 4 waves)
   const uint64_t res = reserved_words(n_dc);
   c->pool_cap = 4 * res + 4096;
   if (!rc && (hipMalloc((void **)&c->pool_a, c->pool_cap * 8) != hipSuccess ||
@@ -681,19 +699,20 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
   if (n == 0) return AM_OK;
   const uint32_t nd = c->n_dc;
   // value pool room for every value this batch could store
-  uint64_t need = 0, so0 = 0, used = 0, new_used = ~0ull;  // ~0: the pool counter stays
+  uint64_t need = 0, so0 = 0, used = 0;
   if ((th == 0 || th == AM_AWSET || th == AM_MVREG || th == AM_BCOUNTER) && R->value.set_off) {
     void *sz = nullptr;
     if (int rc = am_ctx_scratch(ctx, AM_SCR_SIZES, 64, &sz)) return rc;
-    hipLaunchKernelGGL(k_sc_sizes, dim3(1), dim3(64), 0, ctx->stream, R->value.set_off, n, c->ctr, (uint64_t *)sz);
+    hipLaunchKernelGGL(k_sc_sizes, dim3(1), dim3(64), 0, ctx->stream, R->value.set_off, n, c->ctr, c->wend, c->wend_n,
+                       (uint64_t *)sz);
     AM_HIP(hipGetLastError());
     uint64_t w[4] = {0, 0, 0, 0};
     if (int rc = am_ctx_fetch(ctx, sz, 4, w)) return rc;
+    c->wend_n = 0;  // consumed: the counter holds them
     need = w[1] - w[0];
     so0 = w[0];
-    if (need) {
+    if (need) {  // this batch's room: one pool word per result word, from `used`
       if (int rc = pool_reserve(c, need, w + 2, &used)) return rc;
-      new_used = used + need;  // this batch's words: one pool word per result word
     }
   }
   // scratch: code, newest, base_ignore, vflag [n] u8 | base_pres, set_len [n] u32 |
@@ -755,7 +774,8 @@ int am_snapcache_read_gc(am_ctx *ctx, am_snapcache *c, const am_op_log *L, const
     if (rc == AM_OK) {
       const ScGc G{gc_mask, thr_vc, thr_pres};
       hipLaunchKernelGGL(k_sc_store, dim3(grid(n)), dim3(256), 0, ctx->stream, V, *L, *B, *R, S, should_gc, G, used,
-                         so0, new_used, tee ? (const uint8_t *)teed : nullptr);
+                         so0, need ? c->wend : nullptr, tee ? (const uint8_t *)teed : nullptr);
+      if (need) c->wend_n = grid(n) * 4;
       const uint64_t rows = (n + 15) / 16;
       hipLaunchKernelGGL(k_sc_copy, dim3((unsigned)(rows < 65536 ? rows : 65536)), dim3(256), 0, ctx->stream, V, *R, S,
                          n);

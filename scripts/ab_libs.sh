@@ -10,7 +10,7 @@ CFG=${CFG:-c4}
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $VARS; do
     cp scripts/ab/lib_$v.so antidote_amd/libantidote_mat.so
-    timeout -k 10 300 python bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_EXTRA:-} > $OUT/ab_${CFG}_${v}_$r.json 2> $OUT/ab_${CFG}_${v}_$r.err
+    timeout -k 10 300 python bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-secondary ${BENCH_EXTRA:-} > $OUT/ab_${CFG}_${v}_$r.json 2> $OUT/ab_${CFG}_${v}_$r.err
     rc=$?; echo "[ab $CFG $v $r] rc=$rc $(python -c "import json;d=json.load(open('$OUT/ab_${CFG}_${v}_$r.json'));print(round(d['ms_per_step'],3), round(d['roofline']['kernel_ms'],3))" 2>/dev/null)" | tee -a $OUT/steps.log
     if [ $rc -ge 124 ]; then exit $rc; fi  # a time limit or a signal: stop; an error: next variant
   done

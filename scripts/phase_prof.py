@@ -16,6 +16,8 @@ def main():
     mat = Materializer(0)
     p = bench.synth_params(cfg)
     store = mat.synth_store(p)
+    if "--index" not in sys.argv:  # the bench headline's store: every op streamed
+        store.index(abi.AM_INDEX_NONE)
     dlog = store.device_log()
     clock = synth.read_clock(p, 0.75)
     reads = bench.DeviceReads(cfg["n_keys"], cfg["n_dc"], cfg["type"], clock, set_cap=cfg["set_cap"])

@@ -338,10 +338,13 @@ class GpuBackend:
 
 
 class Txn:
-    def __init__(self, cl: "Cluster", dc: int, clock: Optional[Dict[int, int]]):
+    def __init__(self, cl: "Cluster", dc: int, clock: Optional[Dict[int, int]], now: bool = False):
         self.cl, self.dc = cl, dc
         cl.wait_for(dc, clock)
         self.snap = cl.view(dc, clock)
+        if now:  # ClockSI: the snapshot time is the DC's physical clock, prepared commits below it
+            self.snap[dc] = max(self.snap[dc], cl.now[dc])
+        self.prepared: Optional[int] = None
         cl.txn_seq += 1
         # #tx_id{local_start_time, server_pid}: a pid of the DC's node
         from antidote_amd.etf import Atom, Pid
@@ -359,10 +362,18 @@ class Txn:
         eff = downstream(t, op, arg, self.read(key), self.dc, self.cl.token)
         self.ws.setdefault(key, []).append(eff)
 
+    def prepare(self):
+        """clocksi_iprepare: the commit time is fixed now, the writes become visible at commit."""
+        self.cl.now[self.dc] += 10
+        self.prepared = self.cl.now[self.dc]
+        out = dict(self.snap)
+        out[self.dc] = self.prepared
+        return out
+
     def commit(self, abort=False):
         if abort or not self.ws:
             return dict(self.snap)
-        return self.cl.commit(self.dc, self.snap, self.txid, self.ws)
+        return self.cl.commit(self.dc, self.snap, self.txid, self.ws, ct=self.prepared)
 
 
 class Cluster:
@@ -424,9 +435,10 @@ class Cluster:
             if d not in self.down:
                 self._deliver(d)
 
-    def commit(self, dc, snap, txid, ws):
-        self.now[dc] += 10
-        ct = self.now[dc]
+    def commit(self, dc, snap, txid, ws, ct=None):
+        if ct is None:
+            self.now[dc] += 10
+            ct = self.now[dc]
         items = [(key, self.keys[key], eff, dict(snap), dc, ct, txid) for key, effs in ws.items() for eff in effs]
         self.b.deliver(dc, items)
         self.seen[dc][dc] = ct
@@ -496,8 +508,8 @@ def _expand(steps, env=None):
         if "foreach" in s:
             f = s["foreach"]
             a, b = f["range"]
-            for v in range(a, b + 1):
-                yield from _expand(f["steps"], dict(env, **{f["var"]: v}))
+            for v in range(a, b + 1):   # {N} and {N-1}
+                yield from _expand(f["steps"], dict(env, **{f["var"]: v, f["var"] + "-1": v - 1}))
         else:
             yield _subst_step(s, env)
 
@@ -557,7 +569,12 @@ def run_case(case, backend_factory) -> List[Tuple[str, Any, Any]]:
                     clocks[a["save"]] = ct
             elif "begin" in s:
                 a = s["begin"]
-                txns[a["name"]] = Txn(cl, a["dc"], clk(a.get("clock")))
+                txns[a["name"]] = Txn(cl, a["dc"], clk(a.get("clock")), now=a.get("at") == "now")
+            elif "prepare" in s:
+                a = s["prepare"]
+                ct = txns[a["txn"]].prepare()
+                if "save" in a:
+                    clocks[a["save"]] = ct
             elif "t_read" in s:
                 a = s["t_read"]
                 tx = txns[a["txn"]]

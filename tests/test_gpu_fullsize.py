@@ -1,5 +1,5 @@
 """BASELINE.json configs at their FULL bench sizes (bench.CONFIGS: C2 1M keys x 256 ops, C3
-1M x 1024, C4 8M x 16, C5 2M keys / 99.9M Zipf ops), read exactly as bench.py reads them
+1M x 1024, C4 8M x 16, C5 2M keys / 1.34e8 Zipf ops after the 2^20 hot-key cap), read exactly as bench.py reads them
 (one batch over every key of the GPU at the q = 0.75 clock).  Size-independent properties on
 every read (status ok, Count <= the key's ops, LastOpCt within the read clock), and
 bit-exact parity with the oracle on keys sampled across the whole key space -- eight
@@ -34,12 +34,17 @@ def _ranges(n_keys, hot):
     return spread + [(int(h), 1) for h in hot if not any(s <= int(h) < s + n for s, n in spread)]
 
 
-@pytest.mark.parametrize("cfg_name", ["c2", "c3", "c4", "c5"])
-def test_fullsize_config(mat, cfg_name):
+@pytest.mark.parametrize("cfg_name,index", [("c2", 3), ("c3", 3), ("c3", 0), ("c4", 3), ("c5", 3)],
+                         ids=["c2", "c3", "c3-stream", "c4", "c5"])
+def test_fullsize_config(mat, cfg_name, index):
+    """index: the store's zone index (am_store_index level; 0 = none, every op streamed: the bench
+    headline's store)."""
     cfg = bench.CONFIGS[cfg_name]
     p = bench.synth_params(cfg)
     st = mat.synth_store(p)
     try:
+        if index != 3:
+            st.index(index)
         dlog = st.device_log()
         ko, kt = bench.key_columns(mat, dlog, p.n_keys)
         clock = synth.read_clock(p, bench.Q)
