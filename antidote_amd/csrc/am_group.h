@@ -222,6 +222,21 @@ __device__ __forceinline__ void esc_pass(const am_op_log &L, uint32_t nd, const 
   }
 }
 
+// the same for a fresh read whose bits live in the global bitmap gbm (bit = op slot)
+template <int DMAX>
+__device__ void esc_pass_g(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t off0, uint64_t off1,
+                           uint64_t stride, uint32_t lane, uint32_t *gbm, Acc<DMAX> &a) {
+  for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
+    if (L.pk_vc[p] != AM_PK_ESC) continue;
+    uint64_t sv[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+    const uint32_t meta = L.op_meta[p];
+    if (eval_op<DMAX, false>(u, meta, L.commit_time[p], sv, u.allmask, false, p, a) && !(meta & AM_META_BAD))
+      atomicOr(&gbm[p >> 5], 1u << (p & 31));
+  }
+}
+
 // a wave's scalar outputs (in every lane): packed partials (u32, relative to K) and, when
 // `full` (wave-uniform: the full view, or escaped ops), full-width partials.  mxl: lane d's
 // max X[d] over the included ops (0 when none)
@@ -522,6 +537,16 @@ __device__ __forceinline__ bool base_ok(const am_op_log &L, const am_read_batch 
   return !txid && B.base.set_len[r] <= KB;
 }
 
+// The wave tier takes a read (metadata mm, status ok): grouped within the LDS limits, its base
+// acceptable, and not a short read the lane tier takes next (short_opl != 0).  The inclusion
+// pass and the record pass of the split read (k_grp_incl, k_grp_wave<BM>) use the same test.
+__device__ __forceinline__ bool wave_takes(const am_op_log &L, const am_read_batch &B, const GMeta &mm,
+                                           uint32_t short_opl) {
+  return !(mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || !base_ok(L, B, mm.r) ||
+           (short_opl && mm.G <= 64 && mm.off1 - (mm.off0 & ~(uint64_t)(short_opl - 1)) <= 64 &&
+            !has_base_pairs(B, mm.r)));
+}
+
 // key order of the merge: AW elem (a); MV (value, token) (a, b)
 template <int TYPE>
 __device__ __forceinline__ bool key_lt(uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1) {
@@ -701,10 +726,13 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
   return true;
 }
 
-template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
+// BM (the split fresh read, after k_grp_incl): the inclusion bits come from the global bitmap
+// ibm (bit p = op slot p) and the scalar outputs are already written; this pass streams the
+// records and gathers the survivors only.
+template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT, bool BM = false>
 __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
                                                                   am_sel S, am_retry next, uint32_t short_opl,
-                                                                  GrpHint H) {
+                                                                  GrpHint H, const uint32_t *ibm = nullptr) {
   constexpr int OPL = vopl<DMAX, PACKED>();
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
   constexpr uint32_t LPW = 32 / OPL;  // lanes per bitmap word
@@ -725,9 +753,10 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
   PH_DECL();
   PH_BEGIN();
 
-  for (uint64_t b0 = gw; b0 < nsel; b0 += (uint64_t)WB * W) {
-    // ---- lane j < WB: read b0 + j*W -> slot j (errors and hand-offs leave here) ----
-    const uint64_t ii = b0 + (uint64_t)lane * W;
+  for (uint64_t b0 = gw * WB; b0 < nsel; b0 += (uint64_t)WB * W) {
+    // ---- lane j < WB: read b0 + j -> slot j (errors and hand-offs leave here).  A wave takes
+    //      consecutive reads: its single-lane output stores fill whole lines of the columns ----
+    const uint64_t ii = b0 + lane;
     bool elig = false, hand = false;
     uint64_t rr = 0;
     if (lane < WB && ii < nsel) {
@@ -735,11 +764,11 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       read_meta(L, B, S.idx ? (uint64_t)S.idx[sel0 + ii] : ii, TYPE, mm);
       rr = mm.r;
       if (mm.st != AM_OK) {
-        R.status[mm.r] = mm.st, R.flags[mm.r] = 0;
-      } else if (mm.G == AM_NGRP_NONE || mm.G > VG || mm.off1 - mm.off0 > VOPS || !base_ok(L, B, mm.r) ||
-                 (short_opl && mm.G <= 64 && mm.off1 - (mm.off0 & ~(uint64_t)(short_opl - 1)) <= 64 &&
-                  !has_base_pairs(B, mm.r))) {
-        hand = true;  // (short_opl: a short read the lane tier takes next)
+        if (!BM) R.status[mm.r] = mm.st, R.flags[mm.r] = 0;
+      } else if (!wave_takes(L, B, mm, short_opl)) {
+        hand = !BM;  // (short_opl: a short read the lane tier takes next; BM: handed on by k_grp_incl)
+      } else if (BM && R.status[mm.r] != AM_OK) {
+        // the inclusion pass ended the read (an invalid effect included)
       } else {
         elig = true;
         WSlot &w = s.slot[lane];
@@ -772,8 +801,8 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       if (GENERAL) read_inputs<DMAX, true, true>(L, nd, B, r, u);
       // fresh reads over an exact-zone index stream tiles aligned to the zone blocks (a tile that
       // is one exact block is taken whole); the first tile masks the slots before off0
-      const bool zal = !GENERAL && PACKED && TILE == AM_ZONE_OPS && L.zone_vc && off1 - off0 >= AM_ZONE_OPS;
-      const uint64_t t0 = off0 & ~(uint64_t)((zal ? AM_ZONE_OPS : OPL) - 1);
+      const bool zal = !BM && !GENERAL && PACKED && TILE == AM_ZONE_OPS && L.zone_vc && off1 - off0 >= AM_ZONE_OPS;
+      const uint64_t t0 = off0 & ~(uint64_t)((BM ? 32 : zal ? AM_ZONE_OPS : OPL) - 1);
       const uint32_t sh = (uint32_t)(off0 - t0);
 
       // the first record chunk is in flight while the ops are evaluated (loaded after the zone
@@ -798,7 +827,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       bool esc = false;  // some op of this lane did not fit the packed view
       // zone map: with a base snapshot (and no TxId), a tile whose zones are vectorclock:le the
       // base clock holds no candidate (belongs_to_snapshot_op/3) -- not streamed
-      const bool zskip = GENERAL && L.zone_vc && !u.base_ignore && !u.has_txid;
+      const bool zskip = !BM && GENERAL && L.zone_vc && !u.base_ignore && !u.has_txid;
       const uint64_t nz = (stride + AM_ZONE_OPS - 1) / AM_ZONE_OPS;
       // the read's zones in one round of loads: lane (d, z) tests zone z of DC d against the
       // base clock; a zone is inside the base when every DC's lane passes (reads spanning more
@@ -893,7 +922,11 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         const uint64_t q = qa + (uint64_t)jj * 4 * WAVE + 4 * lane;
         rec[jj] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
       }
-      for (uint64_t t = t0; t < off1; t += TILE) {
+      if (BM) {  // the inclusion pass's bits of [t0, off1), word-aligned
+        const uint32_t nw = (uint32_t)((off1 - t0 + 31) / 32);
+        for (uint32_t i = lane; i < nw; i += WAVE) s.incl[i] = ibm[(t0 >> 5) + i];
+      }
+      for (uint64_t t = t0; !BM && t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
         if (!GENERAL && zfull) {
           const uint32_t zi = (uint32_t)((t - t0) / AM_ZONE_OPS);
@@ -936,7 +969,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         if (lane % LPW == 0) s.incl[(uint32_t)((t - t0) / 32) + lane / LPW] = word;
       }
       wave_sync();
-      const bool full = !PACKED || __ballot(esc);
+      const bool full = !BM && (!PACKED || __ballot(esc));
       if (PACKED && full) {  // rare: ops outside the packed view, from the full columns
         esc_pass<DMAX, GENERAL>(L, nd, u, off0, off1, t0, stride, lane, WAVE, s.incl, a);
         wave_sync();
@@ -976,10 +1009,11 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
 
       PH(2);
       // ---- 3. scalar outputs (VGPR wave reductions) ----
-      uint32_t count, flags, pres;
-      uint64_t min_excl, mxl;
-      wave_scalars<DMAX, PACKED>(ap, a, full, PACKED ? pk.K : 0, u.allmask, nd, lane, count, flags, pres, min_excl,
-                                 mxl);
+      uint32_t count = 0, flags = 0, pres = 0;
+      uint64_t min_excl = NONE, mxl = 0;
+      if (!BM)
+        wave_scalars<DMAX, PACKED>(ap, a, full, PACKED ? pk.K : 0, u.allmask, nd, lane, count, flags, pres, min_excl,
+                                   mxl);
       int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
       const bool ign = u.base_ignore && count == 0;
       const uint32_t opres = ign ? 0u : (pres | u.cpres);
@@ -1030,6 +1064,14 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         if (ns > ocap) status = AM_ERR_CAPACITY;
       }
       PH(4);
+      if (BM) {  // the inclusion pass wrote the scalar outputs
+        if (lane == 0) {
+          if (status == AM_OK) R.value.set_len[r] = ns;
+          else R.status[r] = status;
+        }
+        wave_sync();
+        continue;
+      }
       if (status == AM_OK && lane < nd) R.last_ct[(uint64_t)lane * B.n_reads + r] = myct;
       if (lane == 0) {
         R.status[r] = status;
@@ -1053,6 +1095,235 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
   if (n_rskip && lane == 0) atomicAdd(H.skipped + AM_STAT_RECS_SKIPPED, (unsigned long long)n_rskip);
   if (n_gsw && lane == 0) atomicAdd(H.skipped + AM_STAT_GSUM_WORDS, (unsigned long long)n_gsw);
   PH_END();
+}
+
+// ---------------------------------------------------------------- split fresh read, pass 1
+// A fresh read (the batch clock, no base, no TxId; packed view, no zone index) in two passes:
+// k_grp_incl streams the read's commit vectors -- 256-op tiles, one 16-byte load per DC and lane,
+// the wave's only live state the tile and the partials -- and writes its inclusion bits into the
+// global bitmap ibm (bit p = op slot p) and its scalar outputs {NewLastOp, LastOpCt, IsNewSS,
+// Count, status}; k_grp_wave<BM> then streams the records against those bits and gathers the
+// survivors.  A wave takes 32 CONSECUTIVE reads at a time and their scalar outputs leave through
+// LDS as one coalesced store per column (single-lane stores of reads far apart write partial
+// lines of the output columns, each line written back once per writer).
+constexpr uint32_t IWB = 32;  // reads per wave batch
+__device__ __forceinline__ uint32_t wave_min_u32_v(uint32_t v) {
+#define S_(C) v = min(v, dpp32<C>(v));
+  AMK_ROW_STEPS(S_)
+#undef S_
+  v = min(v, (uint32_t)__shfl_xor((int)v, 16, WAVE));
+  return min(v, (uint32_t)__shfl_xor((int)v, 32, WAVE));
+}
+struct ISlot {
+  uint64_t off0, K, idb;
+  uint32_t r, nops;
+};
+template <int DMAX>
+struct ISmem {
+  ISlot slot[IWB];
+  uint32_t mx[DMAX][WAVE];      // one read's per-lane LastOpCt maxima, transposed for the reduction
+  uint64_t ct[DMAX][IWB];       // the batch's outputs, by read
+  int64_t nlo[IWB];
+  uint32_t count[IWB], pres[IWB];
+  int32_t status[IWB];
+  uint32_t flags[IWB];
+};
+
+// ops [g, g + OPL) of the lane (OPL consecutive slots, g OPL-aligned), packed view: inclusion
+// bits (is_op_in_snapshot/7 against the batch clock: every entry X[d] - K <= S[d] - K) and the
+// partials.  RANGE: the tile may hold slots outside [off0, off1); escaped ops (x[0] == ESC)
+// are left to the caller (esc bit k).
+template <int DMAX, int OPL, bool RANGE>
+__device__ __forceinline__ uint32_t incl_tile(const uint32_t (&x)[OPL][DMAX], const PkRead<DMAX> &pk, uint64_t g,
+                                              uint64_t off0, uint64_t off1, uint32_t (&mx)[DMAX], uint32_t &esc,
+                                              uint32_t &cand) {
+  uint32_t ib = 0;
+#pragma unroll
+  for (int k = 0; k < OPL; ++k) {
+    const bool e = x[k][0] == AM_PK_ESC;
+    const bool inr = !RANGE || (g + k >= off0 && g + k < off1);
+    bool in = inr && !e;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) in = in && x[k][d] <= pk.thr[d];
+    esc |= (uint32_t)(inr && e) << k;
+    cand |= (uint32_t)(inr && !e) << k;
+    if (in) {
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) mx[d] = max(mx[d], x[k][d]);
+    }
+    ib |= (uint32_t)in << k;
+  }
+  return ib;
+}
+
+template <int DMAX, int TYPE, bool EXACT>
+__global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                       am_retry next, uint32_t short_opl, uint32_t *ibm) {
+  constexpr int OPL = 4;
+  constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
+  constexpr uint32_t LPW = 32 / OPL;
+  __shared__ ISmem<DMAX> smem[NW];
+  ISmem<DMAX> &sm = smem[threadIdx.x >> 6];
+  ISlot *sl = sm.slot;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t nd = EXACT ? (uint32_t)DMAX : L.n_dc;
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+  const uint64_t W = (uint64_t)gridDim.x * NW;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6);
+  const uint64_t n = B.n_reads;
+  ReadU<DMAX> u;
+  read_inputs<DMAX, false, true>(L, nd, B, 0, u);  // one clock, no bases / TxIds
+
+  for (uint64_t b0 = gw * IWB; b0 < nsel; b0 += (uint64_t)IWB * W) {
+    // ---- lane j < IWB: read b0 + j -> slot j (errors and hand-offs leave here) ----
+    const uint64_t ii = b0 + lane;
+    bool elig = false, hand = false;
+    uint64_t rr = 0;
+    if (lane < IWB && ii < nsel) {
+      GMeta mm;
+      read_meta(L, B, S.idx ? (uint64_t)S.idx[sel0 + ii] : ii, TYPE, mm);
+      rr = mm.r;
+      if (mm.st != AM_OK) {
+        R.status[mm.r] = mm.st, R.flags[mm.r] = 0;
+      } else if (!wave_takes(L, B, mm, short_opl)) {
+        hand = true;
+      } else {
+        elig = true;
+        ISlot &w = sl[lane];
+        w.off0 = mm.off0, w.K = L.key_tbase[mm.key], w.idb = L.key_id_base ? L.key_id_base[mm.key] : 1;
+        w.r = (uint32_t)mm.r, w.nops = (uint32_t)(mm.off1 - mm.off0);
+      }
+    }
+    const uint64_t hm = __ballot(hand);
+    if (hm) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(next.count, (uint32_t)__popcll(hm));
+      base = uniform_u32(base);
+      if (hand) next.list[base + (uint32_t)__popcll(hm & lt)] = (uint32_t)rr;
+    }
+    const uint64_t emask = __ballot(elig);
+    wave_sync();
+
+    for (uint64_t em = emask; em; em &= em - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(em);
+      const uint64_t off0 = uniform_u64(sl[j].off0), off1 = off0 + uniform_u32(sl[j].nops);
+      PkRead<DMAX> pk;
+      pk_setup(u, nd, uniform_u64(sl[j].K), pk);
+      uint32_t mx[DMAX];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) mx[d] = 0;
+      uint32_t cnt = 0, minex = 0xFFFFFFFFu, anyc = 0, anyesc = 0;
+      const uint64_t t0 = off0 & ~31ull;  // 32-op aligned: lane groups of LPW fill whole bitmap words
+      for (uint64_t t = t0; t < off1; t += TILE) {
+        const uint64_t g = t + (uint64_t)lane * OPL;
+        uint32_t x[OPL][DMAX];
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          uint32_t q[OPL] = {};
+          if (d < (int)nd && g < off1) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
+        }
+        uint32_t esc = 0, cand = 0, ib;
+        if (t >= off0 && t + TILE <= off1) ib = incl_tile<DMAX, OPL, false>(x, pk, g, off0, off1, mx, esc, cand);
+        else ib = incl_tile<DMAX, OPL, true>(x, pk, g, off0, off1, mx, esc, cand);
+        if (pk.never) ib = 0;
+        cnt += (uint32_t)__popc(ib);
+        anyc |= cand;
+        anyesc |= esc;
+        const uint32_t ex = cand & ~ib;
+        if (ex) minex = min(minex, (uint32_t)(g - t0) + (uint32_t)__builtin_ctz(ex));
+        uint32_t word = ib << (OPL * (lane % LPW));
+#pragma unroll
+        for (uint32_t xo = 1; xo < LPW; xo <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)xo);
+        const uint64_t w0 = g & ~31ull;  // this lane group's word: ops [w0, w0 + 32)
+        if (lane % LPW == 0 && w0 < off1) {
+          if (w0 >= off0 && w0 + 32 <= off1) {
+            ibm[w0 >> 5] = word;
+          } else {  // a word shared with a neighbouring key: only this read's bits change
+            const uint32_t lo = off0 > w0 ? (uint32_t)(off0 - w0) : 0u;
+            const uint32_t hi = off1 < w0 + 32 ? (uint32_t)(off1 - w0) : 32u;
+            const uint32_t mask = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+            atomicAnd(ibm + (w0 >> 5), ~mask);
+            atomicOr(ibm + (w0 >> 5), word & mask);
+          }
+        }
+      }
+      // ---- the read's scalar outputs: LastOpCt maxima reduced through LDS (lane 8 d + c takes
+      //      DC d's entries of lanes 8 c .. 8 c + 7, then an 8-lane max), the rest by DPP ----
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) sm.mx[d][lane] = mx[d];
+      const uint32_t count_p = wave_sum_u32_v(cnt);
+      minex = wave_min_u32_v(minex);
+      const bool cands = __ballot(anyc != 0) != 0;
+      const bool escs = __ballot(anyesc != 0) != 0;
+      wave_sync();
+      uint32_t m = 0;
+      {
+        const uint32_t d = lane >> 3, c = lane & 7u;
+        if (d < (uint32_t)DMAX) {
+          const u32x4 a0 = *(const u32x4 *)&sm.mx[d][8 * c], a1 = *(const u32x4 *)&sm.mx[d][8 * c + 4];
+          m = max(max(max(a0.x, a0.y), max(a0.z, a0.w)), max(max(a1.x, a1.y), max(a1.z, a1.w)));
+        }
+        m = max(m, (uint32_t)__shfl_xor((int)m, 1));
+        m = max(m, (uint32_t)__shfl_xor((int)m, 2));
+        m = max(m, (uint32_t)__shfl_xor((int)m, 4));
+      }
+      // lane d: DC d's packed maximum (relative to K)
+      const uint32_t mxd = (uint32_t)__shfl((int)m, (int)((lane & 7u) << 3));
+      uint64_t mxl = (lane < nd && count_p) ? pk.K + mxd : 0;
+      uint32_t count = count_p, flags = cands ? pk.miss : 0u, pres = count_p ? u.allmask : 0u;
+      uint64_t min_excl = minex == 0xFFFFFFFFu ? NONE : t0 + minex;
+      if (escs) {  // rare: ops outside the packed view, from the full columns (bits ORed in)
+        Acc<DMAX> a;
+        a.reset();
+        __builtin_amdgcn_s_waitcnt(0);
+        esc_pass_g<DMAX>(L, nd, u, off0, off1, stride, lane, ibm, a);
+        count += wave_sum_u32_v(a.count), flags |= wave_or_u32_v(a.flags), pres |= wave_or_u32_v(a.pres);
+        min_excl = wave_min_u64_v(umin64(min_excl, a.min_excl));
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          if (d >= (int)nd) continue;
+          const uint64_t am = wave_max_u64_v(a.mx[d]);
+          if ((uint32_t)d == lane) mxl = umax64(mxl, am);
+        }
+      }
+      // the read's outputs into the batch's LDS rows (slot j); they leave with the batch
+      const bool ign = count == 0;  // base ignore
+      const uint32_t opres = ign ? 0u : pres;
+      if (lane < nd) sm.ct[lane][j] = ((opres >> lane) & 1u) ? mxl : 0;
+      if (lane == 0) {
+        sm.status[j] = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
+        sm.flags[j] = flags & 0xFFu;
+        sm.count[j] = count;
+        sm.pres[j] = opres;
+        sm.nlo[j] = new_last_op_b(L, uniform_u64(sl[j].idb), off0, off1, min_excl);
+      }
+      wave_sync();  // sm.mx is rewritten by the next read
+    }
+    // ---- the batch's outputs: one coalesced store per column (lane j: read b0 + j) ----
+    if ((emask >> lane) & 1ull) {
+      const uint64_t r = rr;
+      const int32_t st = sm.status[lane];
+      R.status[r] = st;
+      R.flags[r] = (uint8_t)sm.flags[lane];
+      if (st == AM_OK) {
+        const uint32_t c = sm.count[lane];
+        R.new_last_op[r] = sm.nlo[lane];
+        R.last_ct_ignore[r] = c == 0 ? 1 : 0;
+        R.last_ct_pres[r] = sm.pres[lane];
+        R.is_new_ss[r] = c > 0;
+        R.count[r] = c;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          if (d < (int)nd) R.last_ct[(uint64_t)d * n + r] = sm.ct[d][lane];
+      }
+    }
+    wave_sync();  // the slots are rewritten by the next batch
+  }
 }
 
 // ---------------------------------------------------------------- 16-lane row per short read
@@ -1218,12 +1489,50 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
 }
 
 // ---------------------------------------------------------------- launchers
+// the split fresh read: k_grp_incl (op stream -> inclusion bitmap + scalars), then the record /
+// survivor pass k_grp_wave<BM>
+template <int D, int TYPE, bool EXACT>
+int launch_split(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
+                 am_retry next, uint32_t short_opl) {
+  const uint64_t stride = L->snap_stride ? L->snap_stride : L->n_ops;
+  void *ibm = nullptr;
+  if (int rc = am_ctx_scratch(ctx, AM_SCR_INCL, (stride / 32 + 4) * 4, &ibm)) return rc;
+  static int occ_i = 0, occ_w = 0;
+  constexpr size_t smem = sizeof(WaveSmem) * NW;
+  if (!occ_i) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_i, k_grp_incl<D, TYPE, EXACT>, BLOCK, 0) != hipSuccess ||
+        occ_i < 1)
+      occ_i = 2;
+    AM_HIP(hipFuncSetAttribute((const void *)k_grp_wave<D, TYPE, false, true, EXACT, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, k_grp_wave<D, TYPE, false, true, EXACT, true>, BLOCK,
+                                                     smem) != hipSuccess ||
+        occ_w < 1)
+      occ_w = 1;
+  }
+  const uint64_t want_i = (B->n_reads + NW * IWB - 1) / (NW * IWB), want_w = (B->n_reads + NW - 1) / NW;
+  const uint64_t bi = want_i < (uint64_t)ctx->n_cu * occ_i ? want_i : (uint64_t)ctx->n_cu * occ_i;
+  const uint64_t bw = want_w < (uint64_t)ctx->n_cu * occ_w ? want_w : (uint64_t)ctx->n_cu * occ_w;
+  if (bi == 0) return AM_OK;
+  hipLaunchKernelGGL((k_grp_incl<D, TYPE, EXACT>), dim3((unsigned)bi), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S,
+                     next, short_opl, (uint32_t *)ibm);
+  hipLaunchKernelGGL((k_grp_wave<D, TYPE, false, true, EXACT, true>), dim3((unsigned)bw), dim3(BLOCK), smem,
+                     ctx->stream, *L, *B, *R, S, next, short_opl,
+                     GrpHint{nullptr, nullptr, nullptr, nullptr, 0, nullptr, (unsigned long long *)ctx->stats},
+                     (const uint32_t *)ibm);
+  AM_HIP(hipGetLastError());
+  return AM_OK;
+}
+
 template <int D, int TYPE, bool GENERAL, bool PACKED, bool EXACT>
 int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
              int tier) {
   if ((tier & 0xFF) == AM_GRP_WAVE) {
     const uint32_t short_opl = (tier & AM_GRP_HAND_SHORT) ? (D <= 8 ? 8u : 4u) : 0u;  // am_lanes.hip lopl
     constexpr size_t smem = sizeof(WaveSmem) * NW;
+    if constexpr (!GENERAL && PACKED && D <= 8) {
+      if (!L->zone_vc && !ctx->tee_a) return launch_split<D, TYPE, EXACT>(ctx, L, B, R, S, next, short_opl);
+    }
     static int occ = 0;
     if (!occ) {
       AM_HIP(hipFuncSetAttribute((const void *)k_grp_wave<D, TYPE, GENERAL, PACKED, EXACT>,

@@ -13,7 +13,7 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_SCR_MISC = 9, AM_N_SCR = 10 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_SCR_MISC = 9, AM_SCR_INCL = 10, AM_N_SCR = 11 };
 
 struct am_ctx {
   int device = 0;
