@@ -1326,6 +1326,159 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
   }
 }
 
+// ---------------------------------------------------------------- split fresh read, pass 2
+// k_grp_recs: the records of the reads k_grp_incl took, against its bitmap, and the survivors'
+// pairs.  Latency-bound (a read is a few KB), so a wave keeps the NEXT read's bitmap words and
+// first two record chunks in flight while it applies this read's records and gathers its
+// survivors; LDS per wave is a few KB (survivor list in rounds), so ~5 waves per SIMD.
+constexpr uint32_t RCH = 512;    // records per chunk: two 16-byte loads per lane
+constexpr uint32_t RLIST = 512;  // survivor-list entries per gather round
+struct RSlot {
+  uint64_t off0, rk0, ooff;
+  uint32_t r, nops, nrec, G, ocap, ok;
+};
+struct RSmem {
+  uint32_t born[VG / 32], killed[VG / 32];
+  uint32_t incl[VWORDS];
+  uint16_t list[RLIST];
+  RSlot slot[IWB];
+};
+struct RPre {  // a read's prefetched inputs: one bitmap word and two record chunks per lane
+  uint32_t w;
+  u32x4 c[4];
+};
+
+template <int DMAX, int TYPE>
+__global__ void __launch_bounds__(BLOCK, 5) k_grp_recs(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+                                                       uint32_t short_opl, const uint32_t *ibm) {
+  __shared__ RSmem smem[NW];
+  RSmem &s = smem[threadIdx.x >> 6];
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
+  const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
+  const uint64_t W = (uint64_t)gridDim.x * NW;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6);
+
+  // prefetch read j of the slot table: bitmap words [t0 / 32, ...) (lane i: word i, the first
+  // 64), records [rk0 & ~3, + 2 RCH)
+  auto pre = [&](uint32_t j, RPre &p) {
+    const uint64_t off0 = s.slot[j].off0, rk0 = s.slot[j].rk0;
+    const uint32_t nops = s.slot[j].nops, nrec = s.slot[j].nrec;
+    const uint64_t t0 = off0 & ~31ull, rk1 = rk0 + nrec;
+    const uint32_t nw = (uint32_t)((off0 + nops - t0 + 31) / 32);
+    p.w = lane < nw ? ibm[(t0 >> 5) + lane] : 0u;
+    const uint64_t qa = rk0 & ~3ull;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint64_t q = qa + (uint64_t)c * 4 * WAVE + 4 * lane;
+      p.c[c] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
+    }
+  };
+  // records [q, q + 4) against the LDS bitmap (bit = op + sh) -> born / killed bits
+  auto apply4 = [&](u32x4 v, uint64_t q, uint64_t rk0, uint64_t rk1, uint32_t sh) {
+    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = xs[k];
+      if (x == 0xFFFFFFFFu || q + k < rk0 || q + k >= rk1) continue;
+      const uint32_t bit = AM_REC_OP(x) + sh;
+      if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
+      atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
+    }
+  };
+
+  for (uint64_t b0 = gw * IWB; b0 < nsel; b0 += (uint64_t)IWB * W) {
+    // ---- lane j < IWB: read b0 + j -> slot j (the reads k_grp_incl took and left ok) ----
+    const uint64_t ii = b0 + lane;
+    bool ok = false;
+    if (lane < IWB && ii < nsel) {
+      GMeta mm;
+      read_meta(L, B, S.idx ? (uint64_t)S.idx[sel0 + ii] : ii, TYPE, mm);
+      ok = mm.st == AM_OK && wave_takes(L, B, mm, short_opl) && R.status[mm.r] == AM_OK;
+      if (ok) {
+        RSlot &w = s.slot[lane];
+        const uint64_t o0 = R.value.set_off[mm.r], o1 = R.value.set_off[mm.r + 1];
+        w.off0 = mm.off0, w.rk0 = mm.rk0, w.ooff = o0;
+        w.r = (uint32_t)mm.r, w.nops = (uint32_t)(mm.off1 - mm.off0), w.nrec = (uint32_t)(mm.rk1 - mm.rk0);
+        w.G = mm.G, w.ocap = o1 - o0 < 0xFFFFFFFFull ? (uint32_t)(o1 - o0) : 0xFFFFFFFFu;
+      }
+    }
+    uint64_t em = __ballot(ok);
+    wave_sync();
+    RPre cur;
+    if (em) pre((uint32_t)__builtin_ctzll(em), cur);
+    uint32_t setlen = 0;  // lane j: read j's survivor count
+    int32_t cap_err = 0;  // lane j: read j overflowed its capacity
+    for (; em; em &= em - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(em);
+      const uint64_t off0 = uniform_u64(s.slot[j].off0), rk0 = uniform_u64(s.slot[j].rk0);
+      const uint64_t off1 = off0 + uniform_u32(s.slot[j].nops), rk1 = rk0 + uniform_u32(s.slot[j].nrec);
+      const uint32_t G = uniform_u32(s.slot[j].G);
+      const uint64_t t0 = off0 & ~31ull;
+      const uint32_t sh = (uint32_t)(off0 - t0), nw = (uint32_t)((off1 - t0 + 31) / 32);
+      // this read's bitmap into LDS (words past the first 64 straight from memory: long logs)
+      if (lane < nw) s.incl[lane] = cur.w;
+      for (uint32_t i = WAVE + lane; i < nw; i += WAVE) s.incl[i] = ibm[(t0 >> 5) + i];
+      for (uint32_t g = lane; g < (G + 31) / 32; g += WAVE) s.born[g] = 0, s.killed[g] = 0;
+      u32x4 c[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c[k] = cur.c[k];
+      // the next read's inputs in flight from here on
+      const uint64_t rest = em & (em - 1);
+      if (rest) pre((uint32_t)__builtin_ctzll(rest), cur);
+      wave_sync();
+      // ---- records: the two prefetched chunks, then the rest two chunks at a time ----
+      const uint64_t qa = rk0 & ~3ull;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) apply4(c[k], qa + (uint64_t)k * 4 * WAVE + 4 * lane, rk0, rk1, sh);
+      for (uint64_t q0 = qa + 2 * RCH; q0 < rk1; q0 += 2 * RCH) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t q = q0 + (uint64_t)k * 4 * WAVE + 4 * lane;
+          c[k] = q < rk1 ? *(const u32x4 *)(L.rec_g + q) : u32x4{~0u, ~0u, ~0u, ~0u};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) apply4(c[k], q0 + (uint64_t)k * 4 * WAVE + 4 * lane, rk0, rk1, sh);
+      }
+      wave_sync();
+      // ---- survivors in group order: lane w owns alive word w; listed in rounds of RLIST ----
+      const uint32_t nwd = (G + 31) / 32;
+      const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
+      const uint32_t cnt = (uint32_t)__popc(aw);
+      const uint32_t inc = wave_incl_scan_u32(cnt, lane);
+      const uint32_t ns = (uint32_t)__shfl((int)inc, 63, WAVE);
+      const uint64_t ooff = uniform_u64(s.slot[j].ooff);
+      const uint32_t ocap = uniform_u32(s.slot[j].ocap);
+      const uint32_t nput = ns < ocap ? ns : ocap;
+      for (uint32_t base = 0; base < nput; base += RLIST) {
+        uint32_t o = inc - cnt;
+        for (uint32_t bits = aw; bits; bits &= bits - 1, ++o)
+          if (o >= base && o < base + RLIST) s.list[o - base] = (uint16_t)(lane * 32 + __builtin_ctz(bits));
+        wave_sync();
+        const uint32_t end = nput - base < RLIST ? nput - base : RLIST;
+        for (uint32_t j0 = 0; j0 < end; j0 += 2 * WAVE) {
+          const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
+          u64x2 p1 = {0, 0}, p2 = {0, 0};
+          if (j1 < end) p1 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j1]));
+          if (j2 < end) p2 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j2]));
+          if (j1 < end) R.value.set_a[ooff + base + j1] = p1.x, R.value.set_b[ooff + base + j1] = p1.y;
+          if (j2 < end) R.value.set_a[ooff + base + j2] = p2.x, R.value.set_b[ooff + base + j2] = p2.y;
+        }
+        wave_sync();
+      }
+      if (lane == j) setlen = ns, cap_err = ns > ocap;
+      wave_sync();
+    }
+    // ---- the batch's outputs (lane j: read b0 + j): set_len, or the capacity status ----
+    if (ok) {
+      const uint64_t r = s.slot[lane].r;
+      if (cap_err) R.status[r] = AM_ERR_CAPACITY;
+      else R.value.set_len[r] = setlen;
+    }
+    wave_sync();  // the slots are rewritten by the next batch
+  }
+}
+
 // ---------------------------------------------------------------- 16-lane row per short read
 // A wave takes 64 reads at a time: lane i checks read i against the row limits (the others
 // leave through one hand-off atomic per wave), then the four 16-lane rows walk the
@@ -1490,7 +1643,7 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
 
 // ---------------------------------------------------------------- launchers
 // the split fresh read: k_grp_incl (op stream -> inclusion bitmap + scalars), then the record /
-// survivor pass k_grp_wave<BM>
+// survivor pass k_grp_recs
 template <int D, int TYPE, bool EXACT>
 int launch_split(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S,
                  am_retry next, uint32_t short_opl) {
@@ -1498,28 +1651,22 @@ int launch_split(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_rea
   void *ibm = nullptr;
   if (int rc = am_ctx_scratch(ctx, AM_SCR_INCL, (stride / 32 + 4) * 4, &ibm)) return rc;
   static int occ_i = 0, occ_w = 0;
-  constexpr size_t smem = sizeof(WaveSmem) * NW;
   if (!occ_i) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_i, k_grp_incl<D, TYPE, EXACT>, BLOCK, 0) != hipSuccess ||
         occ_i < 1)
       occ_i = 2;
-    AM_HIP(hipFuncSetAttribute((const void *)k_grp_wave<D, TYPE, false, true, EXACT, true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, k_grp_wave<D, TYPE, false, true, EXACT, true>, BLOCK,
-                                                     smem) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, k_grp_recs<D, TYPE>, BLOCK, 0) != hipSuccess ||
         occ_w < 1)
       occ_w = 1;
   }
-  const uint64_t want_i = (B->n_reads + NW * IWB - 1) / (NW * IWB), want_w = (B->n_reads + NW - 1) / NW;
+  const uint64_t want_i = (B->n_reads + NW * IWB - 1) / (NW * IWB), want_w = want_i;
   const uint64_t bi = want_i < (uint64_t)ctx->n_cu * occ_i ? want_i : (uint64_t)ctx->n_cu * occ_i;
   const uint64_t bw = want_w < (uint64_t)ctx->n_cu * occ_w ? want_w : (uint64_t)ctx->n_cu * occ_w;
   if (bi == 0) return AM_OK;
   hipLaunchKernelGGL((k_grp_incl<D, TYPE, EXACT>), dim3((unsigned)bi), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S,
                      next, short_opl, (uint32_t *)ibm);
-  hipLaunchKernelGGL((k_grp_wave<D, TYPE, false, true, EXACT, true>), dim3((unsigned)bw), dim3(BLOCK), smem,
-                     ctx->stream, *L, *B, *R, S, next, short_opl,
-                     GrpHint{nullptr, nullptr, nullptr, nullptr, 0, nullptr, (unsigned long long *)ctx->stats},
-                     (const uint32_t *)ibm);
+  hipLaunchKernelGGL((k_grp_recs<D, TYPE>), dim3((unsigned)bw), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S,
+                     short_opl, (const uint32_t *)ibm);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }
