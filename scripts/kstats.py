@@ -1,12 +1,12 @@
-#!/usr/bin/env python3
-"""Print the top kernels of rocprofv3 --stats summaries: kstats.py DIR [DIR...]"""
+"""Print the read kernels of rocprofv3 kernel-stats CSVs side by side: kstats.py DIR... [--match k_grp]"""
 import csv
-import glob
-import os
 import sys
 
-for d in sys.argv[1:]:
-    for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
-        print("==", f)
-        for r in list(csv.DictReader(open(f)))[:8]:
-            print(f"  {r['Name'][:72]:72s} {r['Calls']:>4s} {float(r['AverageNs'])/1e6:9.3f} ms {float(r['Percentage']):6.2f}%")
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+match = next((a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--match=")), "")
+for d in args:
+    rows = list(csv.DictReader(open(f"{d}/run_kernel_stats.csv")))
+    print("==", d)
+    for x in rows:
+        if match in x["Name"] and int(x["Calls"]) >= 10:
+            print(f"  {x['Name'][:60]:60s} {x['Calls']:>5s} {float(x['AverageNs']) / 1e3:9.1f} us")

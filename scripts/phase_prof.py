@@ -1,5 +1,6 @@
-"""Experiments only: phase cycle breakdown of the wave-per-read group kernel on the C3 bench
-workload.  Needs a library built with -DAMK_PHASE_PROF (AM_LIB=...)."""
+"""Experiments only: phase cycle breakdown of the wave-per-read group kernel (k_grp_wave) on the
+C3 bench workload: --cached (read/6 through the snapshot cache; fresh reads take the split
+kernels), --index (zone index on).  Needs a library built with -DAMK_PHASE_PROF (AM_LIB=...)."""
 import ctypes
 import sys
 
@@ -7,30 +8,30 @@ import torch
 
 sys.path.insert(0, ".")
 import bench  # noqa: E402
-from antidote_amd import abi, synth  # noqa: E402
+from antidote_amd import abi  # noqa: E402
 from antidote_amd.materializer import Materializer  # noqa: E402
 
 
 def main():
     cfg = bench.CONFIGS["c3"]
     mat = Materializer(0)
-    p = bench.synth_params(cfg)
-    store = mat.synth_store(p)
-    if "--index" not in sys.argv:  # the bench headline's store: every op streamed
-        store.index(abi.AM_INDEX_NONE)
-    dlog = store.device_log()
-    clock = synth.read_clock(p, 0.75)
-    reads = bench.DeviceReads(cfg["n_keys"], cfg["n_dc"], cfg["type"], clock, set_cap=cfg["set_cap"])
+    level = abi.AM_INDEX_SUMMARIES if "--index" in sys.argv else abi.AM_INDEX_NONE
+    st = bench.Step(mat, None, cfg, 0, 1, level)
+    if "--cached" in sys.argv:  # read/6 through the snapshot cache (q = 0.5 bases)
+        st.populate()
+        run = st.cached_read
+    else:
+        run = st.read
     f = abi.lib().am_debug_phase_cycles
     f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p]
     out = (ctypes.c_uint64 * 8)()
     for _ in range(3):
-        bench.materialize(mat, dlog, reads)
+        run()
     torch.cuda.synchronize()
     f(out)
     n = 5
     for _ in range(n):
-        bench.materialize(mat, dlog, reads)
+        run()
     torch.cuda.synchronize()
     f(out)
     tot = sum(out[:6])
