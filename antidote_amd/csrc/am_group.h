@@ -123,6 +123,58 @@ __device__ __forceinline__ void read_inputs(const am_op_log &L, uint32_t nd, con
   u.txid = u.has_txid ? u64(B.txid[r]) : 0;
 }
 
+// read_inputs (GENERAL, uniform) in two halves, so that a wave's NEXT read's inputs are in
+// flight while it reads this one: in_load issues every load of read r at once as vector loads
+// (lane d < nd: DC d's clock and base clock entries; lanes 0-4 one scalar each) -- the chain
+// read_pres -> clock, base_ignore -> base_pres -> base clock, txid_valid -> txid is not
+// waited on link by link -- and in_take builds the ReadU from them.  A base column is read
+// whenever the batch has one (its [n_dc][n_reads] extent), its entries used only as
+// read_inputs uses them.
+struct InPre {
+  uint64_t s, c, x;  // lane d: S[d] / C0[d] candidates; lane 4: the TxId
+  uint32_t w;        // lane 0 read_pres, 1 base_ignore, 2 base_pres, 3 txid_valid
+};
+// Marks registers as used here: the compiler waits for their loads at this point (where the
+// wave waits for older loads anyway) instead of at their real use, which can sit behind this
+// read's output stores -- a wave's loads and stores retire through one counter (vmcnt), and a
+// wait placed at a loop head cannot count them, so it would wait for every store.
+template <typename T>
+__device__ __forceinline__ void hold(const T &v) {
+  asm volatile("" ::"v"(v));
+}
+__device__ __forceinline__ void hold(const InPre &p) { hold(p.s), hold(p.c), hold(p.x), hold(p.w); }
+
+__device__ __forceinline__ void in_load(const am_op_log &L, uint32_t nd, const am_read_batch &B, uint64_t r,
+                                        uint32_t lane, InPre &p) {
+  const uint64_t n = B.n_reads;
+  const bool prc = B.per_read_clock;
+  p.s = p.c = p.x = 0, p.w = 0;
+  if (lane < nd) {
+    p.s = B.read_vc[prc ? (uint64_t)lane * n + r : (uint64_t)lane];
+    if (B.base_ignore && B.base_vc) p.c = B.base_vc[(uint64_t)lane * n + r];
+  }
+  if (lane == 0) p.w = (uint32_t)B.read_pres[prc ? r : 0];
+  if (lane == 1) p.w = B.base_ignore ? (uint32_t)B.base_ignore[r] : 1u;
+  if (lane == 2 && B.base_ignore && B.base_pres) p.w = (uint32_t)B.base_pres[r];
+  if (lane == 3) p.w = B.txid_valid ? (uint32_t)B.txid_valid[r] : 1u;
+  if (lane == 4 && B.txid && L.op_txid) p.x = B.txid[r];
+}
+template <int DMAX>
+__device__ __forceinline__ void in_take(const am_op_log &L, uint32_t nd, const am_read_batch &B, const InPre &p,
+                                        ReadU<DMAX> &u) {
+  u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+  u.spres = lane_u32(p.w, 0) & u.allmask;
+  u.base_ignore = !B.base_ignore || lane_u32(p.w, 1) != 0;
+  u.cpres = u.base_ignore ? 0u : (lane_u32(p.w, 2) & u.allmask);
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? lane_u64(p.s, d) : 0;
+    u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? lane_u64(p.c, d) : 0;
+  }
+  u.has_txid = B.txid && lane_u32(p.w, 3) != 0 && L.op_txid;
+  u.txid = u.has_txid ? lane_u64(p.x, 4) : 0;
+}
+
 // N consecutive elements per lane (N = 1, 2 or a multiple of 4 / 2; 16-byte loads)
 template <int N>
 __device__ __forceinline__ void ld_n64(const uint64_t *p, uint64_t *o) {
@@ -791,14 +843,21 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       if (hand) next.list[base + (uint32_t)__popcll(hm & lt)] = (uint32_t)rr;
     }
     wave_sync();
+    InPre ip{};  // GENERAL: the next read's inputs, in flight
+    uint64_t em0 = __ballot(elig);
+    if (GENERAL && em0) in_load(L, nd, B, uniform_u32(s.slot[__builtin_ctzll(em0)].r), lane, ip), hold(ip);
 
-    for (uint64_t em = __ballot(elig); em; em &= em - 1) {
+    for (uint64_t em = em0; em; em &= em - 1) {
       const uint32_t j = (uint32_t)__builtin_ctzll(em);
       const uint64_t off0 = uniform_u64(s.slot[j].off0), rk0 = uniform_u64(s.slot[j].rk0);
       const uint64_t off1 = off0 + uniform_u32(s.slot[j].nops), rk1 = rk0 + uniform_u32(s.slot[j].nrec);
       const uint64_t r = uniform_u32(s.slot[j].r);
       const uint32_t G = uniform_u32(s.slot[j].G);
-      if (GENERAL) read_inputs<DMAX, true, true>(L, nd, B, r, u);
+      if (GENERAL) {
+        in_take<DMAX>(L, nd, B, ip, u);
+        const uint64_t rest = em & (em - 1);
+        if (rest) in_load(L, nd, B, uniform_u32(s.slot[__builtin_ctzll(rest)].r), lane, ip);
+      }
       // fresh reads over an exact-zone index stream tiles aligned to the zone blocks (a tile that
       // is one exact block is taken whole); the first tile masks the slots before off0
       const bool zal = !BM && !GENERAL && PACKED && TILE == AM_ZONE_OPS && L.zone_vc && off1 - off0 >= AM_ZONE_OPS;
@@ -1006,6 +1065,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         q0 = q1;
       }
       wave_sync();
+      if (GENERAL) hold(ip);  // the next read's inputs, before this read's stores
 
       PH(2);
       // ---- 3. scalar outputs (VGPR wave reductions) ----
