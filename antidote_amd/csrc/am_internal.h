@@ -51,10 +51,10 @@ struct am_ctx {
   int64_t tee_shift = 0;
   uint8_t *tee_done = nullptr;
   // The mixed-batch planner's per-type streams (am_plan.hip): sub-contexts of the set types
-  // on the same device, sharing the counters, each with its own stream, scratch slots and
+  // (and [3]: the big-MV reads started beside the lane tier) on the same device, sharing the counters, each with its own stream, scratch slots and
   // pinned buffer, so one type's tiers overlap another's.  ev_fork orders them after the
   // planner; their ev0 joins them back.
-  am_ctx *sub[3] = {};
+  am_ctx *sub[4] = {};
   bool is_sub = false;
   hipEvent_t ev_fork = nullptr;
   // the CRDT types present in a log's keys, by key_type array: {n_keys, 1 << type mask}

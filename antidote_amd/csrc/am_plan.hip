@@ -21,6 +21,8 @@
 // big-read path, which sizes its scratch on the host (one synchronization).  In a mixed
 // batch every set type's chain runs on a stream of its own (am_ctx::sub), joined back
 // before the call returns: a type's latency-bound tiers overlap the other types' tiers.
+#include <sched.h>
+
 #include "am_wave.h"
 
 using namespace amk;
@@ -30,18 +32,22 @@ namespace {
 constexpr int PB = 256;              // planner block
 constexpr int PER = 4;               // reads per thread
 constexpr uint32_t PCHUNK = PB * PER;
-constexpr int NCLS = 8;              // classes: 0..4 = type-1, 5 = done (status written)
-constexpr uint32_t CLS_DONE = 5;
+// classes: 1..5 = the type, 6 = done (status written), 0 = an MV read of a key in the chunked
+// big view when `mvbig` (the big-read tier takes it straight from the batch, beside the other
+// tiers; class 0 starts at 0, so its list is the plan's index array and its count range[1])
+constexpr int NCLS = 8;
+constexpr uint32_t CLS_MVBIG = 0, CLS_DONE = 6;
 
 __device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read_batch &B, am_read_result &R,
-                                               uint64_t r, bool write_status) {
+                                               uint64_t r, bool write_status, bool mvbig) {
   const uint32_t t = B.type[r];
   const uint64_t key = B.key[r];
   if (t < AM_PN || t > AM_BCOUNTER || key >= L.n_keys) {
     if (write_status) R.status[r] = AM_ERR_INVALID;
     return CLS_DONE;
   }
-  return t - 1;
+  if (mvbig && t == AM_MVREG && L.key_type[key] == AM_MVREG && am_ngrp_big(L.key_ngrp[key])) return CLS_MVBIG;
+  return t;
 }
 
 // the planner's input: the whole batch, or a selection (the lane tier's hand-off list)
@@ -53,14 +59,14 @@ __device__ __forceinline__ uint64_t in_read(am_sel in, uint64_t i) {
 }
 
 __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
-                                                   uint32_t *cnt, uint32_t *tot, bool write_status) {
+                                                   uint32_t *cnt, uint32_t *tot, bool write_status, bool mvbig) {
   __shared__ uint32_t c[NCLS];
   if (threadIdx.x < NCLS) c[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
-    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), write_status)], 1u);
+    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), write_status, mvbig)], 1u);
   }
   __syncthreads();
   if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = atomicAdd(&tot[threadIdx.x], c[threadIdx.x]);
@@ -68,7 +74,7 @@ __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B,
 
 __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
                                                      const uint32_t *off, const uint32_t *tot, uint32_t *range,
-                                                     uint32_t *idx) {
+                                                     uint32_t *idx, bool mvbig) {
   __shared__ uint32_t run[NCLS];
   __shared__ uint32_t wcnt[PB / WAVE][NCLS];
   const uint32_t tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
@@ -82,7 +88,7 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = base + (uint64_t)j * PB + tid;
     const uint64_t r = i < nin ? in_read(in, i) : 0;
-    const uint32_t c = i < nin ? read_class(L, B, R, r, false) : NCLS;
+    const uint32_t c = i < nin ? read_class(L, B, R, r, false, mvbig) : NCLS;
     uint32_t rank = 0;
     for (uint32_t k = 0; k < NCLS; ++k) {
       const uint64_t m = __ballot(c == k);
@@ -105,19 +111,24 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
   }
 }
 
-__global__ void __launch_bounds__(PB) k_type_mask(const uint8_t *key_type, uint64_t n, uint32_t *out) {
+// bit t: a key of type t; TYPES_MVBIG: an MV key in the chunked big view
+constexpr uint32_t TYPES_MVBIG = 1u << 31;
+__global__ void __launch_bounds__(PB) k_type_mask(const uint8_t *key_type, const uint32_t *key_ngrp, uint64_t n,
+                                                  uint32_t *out) {
   uint32_t m = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * PB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * PB) {
     const uint32_t t = key_type[i];
-    m |= t < 32 ? 1u << t : 0u;
+    m |= t < 31 ? 1u << t : 0u;
+    if (t == AM_MVREG && key_ngrp && am_ngrp_big(key_ngrp[i])) m |= TYPES_MVBIG;
   }
   m = wave_or_u32(m);
   if ((threadIdx.x & (WAVE - 1)) == 0 && m) atomicOr(out, m);
 }
 
 // The types present in the log's keys (one pass + readback per key_type array, cached on the
-// context).  It only picks the order of the mixed batch's chains: a stale entry (a store
-// rebuilt over a reused block) costs time, never a result.
+// context).  It only picks the order of the mixed batch's chains and whether the big MV reads
+// are planned early: a stale entry (a store rebuilt over a reused block) costs time, never a
+// result.
 int log_types(am_ctx *ctx, const am_op_log *L, uint32_t *mask) {
   auto it = ctx->type_masks.find(L->key_type);
   if (it != ctx->type_masks.end() && it->second.first == L->n_keys) {
@@ -128,8 +139,9 @@ int log_types(am_ctx *ctx, const am_op_log *L, uint32_t *mask) {
   if (int rc = am_ctx_scratch(ctx, AM_SCR_MISC, 256, &w)) return rc;
   AM_HIP(hipMemsetAsync(w, 0, sizeof(uint64_t), ctx->stream));
   const uint64_t cap = (uint64_t)ctx->n_cu * 4, nb = (L->n_keys + PB - 1) / PB;
-  if (nb) hipLaunchKernelGGL(k_type_mask, dim3((unsigned)(nb < cap ? nb : cap)), dim3(PB), 0, ctx->stream, L->key_type,
-                             L->n_keys, (uint32_t *)w);
+  if (nb)
+    hipLaunchKernelGGL(k_type_mask, dim3((unsigned)(nb < cap ? nb : cap)), dim3(PB), 0, ctx->stream, L->key_type,
+                       L->key_ngrp, L->n_keys, (uint32_t *)w);
   AM_HIP(hipGetLastError());
   uint64_t h = 0;
   if (int rc = am_ctx_fetch(ctx, w, 1, &h)) return rc;
@@ -233,6 +245,32 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   return rc ? rc : am_launch_big(ctx, L, B, R, type, retry);
 }
 
+// The set chains' big tiers, each launched once its chain's front has drained (its hand-off
+// count is read back to size the big tier): in the order the chains finish, not in type order
+// -- a host readback that waits on a slow chain would hold back a finished one's big tier
+// (C5: the bounded-counter chain drains ~1 ms before the MV chain).
+int launch_bigs_when_ready(am_ctx *const sub[3], const am_op_log *L, const am_read_batch *B, am_read_result *R,
+                           const am_retry retry[3]) {
+  bool pend[3];
+  for (int i = 0; i < 3; ++i) {
+    pend[i] = sub[i] != nullptr;
+    if (pend[i]) AM_HIP(hipEventRecord(sub[i]->ev1, sub[i]->stream));
+  }
+  for (int left = pend[0] + pend[1] + pend[2]; left;) {
+    int done = 0;
+    for (int i = 0; i < 3; ++i) {
+      if (!pend[i]) continue;
+      const hipError_t q = hipEventQuery(sub[i]->ev1);
+      if (q == hipErrorNotReady) continue;
+      AM_HIP(q);
+      pend[i] = false, --left, ++done;
+      if (int rc = am_launch_big(sub[i], L, B, R, AM_AWSET + (uint32_t)i, retry[i])) return rc;
+    }
+    if (left && !done) sched_yield();
+  }
+  return AM_OK;
+}
+
 }  // namespace
 
 int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R) {
@@ -287,10 +325,12 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   const uint32_t lanes = am_lane_accept(L, R, (1u << AM_PN) | (1u << AM_LWW) | (1u << AM_AWSET) | (1u << AM_MVREG));
   am_ctx *sub[3] = {};
   am_retry retry[3];
+  am_ctx *ms = nullptr;  // the early big-MV tier's sub-context
   int rc = AM_OK;
   auto join = [&]() {
     for (am_ctx *s : sub)
       if (s && hipEventRecord(s->ev0, s->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, s->ev0, 0);
+    if (ms && hipEventRecord(ms->ev0, ms->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, ms->ev0, 0);
   };
   // type t's set chain over class range `range` of selection idx, on its sub-context
   auto start_chain = [&](uint32_t t, const uint32_t *idx, const uint32_t *range, bool forked) -> int {
@@ -307,7 +347,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     if (!e) e = am_ctx_scratch(s, AM_SCR_PLAN, (n + 64) * sizeof(uint32_t), &sp);
     am_sel S;
     S.idx = idx;
-    S.range = range + 2 * (t - 1);
+    S.range = range + 2 * t;
     if (!e)
       e = run_sets_front(s, L, B, R, S, t, (uint32_t *)sp, (uint32_t *)sr, (uint32_t *)sg, ((lanes >> t) & 1u) != 0,
                          &retry[t - AM_AWSET]);
@@ -315,7 +355,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   };
   // the planner over selection `in` (n_in reads) on c's stream, scratch slot `slot`:
   // [range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
-  auto plan = [&](am_ctx *c, int slot, am_sel in, uint64_t n_in, bool write_status, uint32_t **range,
+  auto plan = [&](am_ctx *c, int slot, am_sel in, uint64_t n_in, bool write_status, bool mvbig, uint32_t **range,
                   uint32_t **idx) -> int {
     const uint64_t n_blk = (n_in + PCHUNK - 1) / PCHUNK;
     void *scr = nullptr;
@@ -325,10 +365,10 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     *idx = cnt + n_blk * NCLS;
     AM_HIP(hipMemsetAsync(tot, 0, NCLS * sizeof(uint32_t), c->stream));
     hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, c->stream, *L, *B, *R, in, cnt, tot,
-                       write_status);
+                       write_status, mvbig);
     AM_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, c->stream, *L, *B, *R, in, cnt, tot,
-                       *range, *idx);
+                       *range, *idx, mvbig);
     AM_HIP(hipGetLastError());
     return AM_OK;
   };
@@ -336,19 +376,34 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   uint64_t n_in = n;  // reads the planner partitions
   uint32_t types = 0;
   if (lanes && (rc = log_types(ctx, L, &types))) return rc;
+  // Reads whose tier is known from their key alone are planned from the whole batch and start
+  // beside the lane tier: the bounded-counter chain, and the MV reads of keys in the chunked
+  // big view (straight to the big-read tier; the later planner leaves them out)
   const bool bc_early = lanes && ((types >> AM_BCOUNTER) & 1u);
+  const bool mv_early = lanes && (types & TYPES_MVBIG);
+  uint32_t *erange = nullptr, *eidx = nullptr;
   if (lanes) {
     void *lscr = nullptr;
     rc = am_ctx_scratch(ctx, AM_SCR_SPARE, (n + 64) * sizeof(uint32_t), &lscr);
     if (rc) return rc;
     AM_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-    if (bc_early) {
-      am_ctx *bs = am_ctx_sub(ctx, (int)(AM_BCOUNTER - AM_AWSET));
-      if (!bs) return AM_ERR_HIP;
-      AM_HIP(hipStreamWaitEvent(bs->stream, ctx->ev_fork, 0));
-      uint32_t *brange = nullptr, *bidx = nullptr;
-      rc = plan(bs, AM_SCR_SPARE, all, n, false, &brange, &bidx);
-      if (!rc) rc = start_chain(AM_BCOUNTER, bidx, brange, true);
+    if (bc_early || mv_early) {
+      am_ctx *es = am_ctx_sub(ctx, bc_early ? (int)(AM_BCOUNTER - AM_AWSET) : 3);
+      if (!es) return AM_ERR_HIP;
+      AM_HIP(hipStreamWaitEvent(es->stream, ctx->ev_fork, 0));
+      rc = plan(es, AM_SCR_SPARE, all, n, false, mv_early, &erange, &eidx);
+      if (!rc && mv_early) {
+        ms = am_ctx_sub(ctx, 3);
+        if (!ms) return AM_ERR_HIP;
+        ms->grp_hint_in = ctx->grp_hint_in;
+        ms->tee_a = ctx->tee_a, ms->tee_b = ctx->tee_b, ms->tee_g = ctx->tee_g, ms->tee_shift = ctx->tee_shift;
+        ms->tee_done = ctx->tee_done;
+        if (ms != es) {
+          AM_HIP(hipEventRecord(es->ev0, es->stream));
+          AM_HIP(hipStreamWaitEvent(ms->stream, es->ev0, 0));
+        }
+      }
+      if (!rc && bc_early) rc = start_chain(AM_BCOUNTER, eidx, erange, true);
     }
     uint32_t *lbuf = (uint32_t *)lscr;  // [0] = 0, [1] = hand-off count, list at +64
     am_retry nx;
@@ -356,6 +411,12 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     nx.list = lbuf + 64;
     if (!rc && hipMemsetAsync(lbuf, 0, 2 * sizeof(uint32_t), ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
     if (!rc) rc = am_launch_lanes(ctx, L, B, R, all, nx, lanes);
+    if (!rc && mv_early) {  // class 0 of the early plan: the list from 0, its count range[1]
+      am_retry big;
+      big.count = erange + 1;
+      big.list = eidx;
+      rc = am_launch_big(ms, L, B, R, AM_MVREG, big);
+    }
     // one counter readback: a batch of short reads (the common case) ends here instead of
     // launching the planner and every class's kernels over empty selections
     uint64_t hc = 0;
@@ -370,18 +431,17 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     in.range = lbuf;
   }
   uint32_t *range = nullptr, *idx = nullptr;
-  rc = plan(ctx, AM_SCR_PLAN, in, n_in, true, &range, &idx);
+  rc = plan(ctx, AM_SCR_PLAN, in, n_in, true, mv_early, &range, &idx);
   if (!rc && hipEventRecord(ctx->ev_fork, ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
   for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t)
     if (t != AM_BCOUNTER || !bc_early) rc = start_chain(t, idx, range, false);
   for (uint32_t t = AM_PN; t <= AM_LWW && !rc; ++t) {
     am_sel S;
     S.idx = idx;
-    S.range = range + 2 * (t - 1);
+    S.range = range + 2 * t;
     rc = run_scalar(ctx, L, B, R, S, t, (uint32_t *)rows_scr);
   }
-  for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t)
-    rc = am_launch_big(sub[t - AM_AWSET], L, B, R, t, retry[t - AM_AWSET]);
+  if (!rc) rc = launch_bigs_when_ready(sub, L, B, R, retry);
   join();
   return rc;
 }
