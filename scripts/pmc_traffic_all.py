@@ -2,14 +2,15 @@
 stream, group, LDS-sort and big-read tiers and the planner) from rocprofv3 --pmc FETCH_SIZE
 and WRITE_SIZE passes (separate runs) of `bench.py --config CFG`; one launch = one k_lane
 (or k_grp_wave) dispatch.  Writes profiles/pmc_traffic.json[CFG].
-Usage: pmc_traffic_all.py FETCH_DIR WRITE_DIR CFG WORKLOAD LAUNCH_KERNEL [OUT]"""
+Usage: pmc_traffic_all.py FETCH_DIR WRITE_DIR CFG WORKLOAD LAUNCH_KERNEL [OUT [ZONE_INDEX]]
+(ZONE_INDEX: the store's zone index level name, bench.py INDEX_NAMES; default "none")"""
 import csv
 import glob
 import json
 import sys
 
-MAT = ("k_lane", "k_plan", "k_rows", "k_bc_rows", "k_stream", "k_grp_wave", "k_grp_wg", "k_grp_row", "k_sets", "k_big_",
-       "k_bc_wave")
+MAT = ("k_lane", "k_plan", "k_rows", "k_bc_rows", "k_stream", "k_grp_wave", "k_grp_wg", "k_grp_row", "k_grp_incl",
+       "k_grp_recs", "k_sets", "k_big_", "k_bc_wave")
 
 
 def totals(d, counter, launch):
@@ -27,11 +28,12 @@ def totals(d, counter, launch):
 def main():
     fdir, wdir, cfg, workload, launch = sys.argv[1:6]
     out = sys.argv[6] if len(sys.argv) > 6 else "profiles/pmc_traffic.json"
+    zone_index = sys.argv[7] if len(sys.argv) > 7 else "none"
     f, nf = totals(fdir, "FETCH_SIZE", launch)
     w, nw = totals(wdir, "WRITE_SIZE", launch)
     fetch_raw = sum(f.values()) / nf
     write = sum(w.values()) / nw
-    d = {"workload": workload, "kernel": "all materialize kernels (" + ", ".join(MAT) + ")", "launches": [nf, nw],
+    d = {"workload": workload, "zone_index": zone_index, "kernel": "all materialize kernels (" + ", ".join(MAT) + ")", "launches": [nf, nw],
          "fetch_raw_bytes_per_launch": fetch_raw, "fetch_bytes_per_launch": 2 * fetch_raw,
          "write_bytes_per_launch": write, "bytes_per_launch": 2 * fetch_raw + write,
          "per_kernel_fetch_raw": {k[:80]: v / nf for k, v in sorted(f.items(), key=lambda x: -x[1])},
