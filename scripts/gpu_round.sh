@@ -25,8 +25,8 @@ for s in $STEPS; do
     ingest) timeout -k 10 400 python scripts/bench_ingest.py ${INGEST_ARGS:-} > $OUT/ingest.json 2> $OUT/ingest.err; ok $? ingest ;;
     prof) for c in ${PROF_CFGS:-c2 c3 c4 c5}; do timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline ${PROF_ARGS:-} > $OUT/prof_$c.json 2> $OUT/prof_$c.log; ok $? prof_$c; done ;;
     pmc) for c in ${PMC_CFGS:-c4 c5}; do
-           timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$c -o pmc --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmcf_$c.log 2>&1; ok $? pmcf_$c
-           timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$c -o pmc --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $OUT/pmcw_$c.log 2>&1; ok $? pmcw_$c
+           timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_$c -o pmc --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/pmcf_$c.log 2>&1; ok $? pmcf_$c
+           timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_$c -o pmc --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-secondary > $OUT/pmcw_$c.log 2>&1; ok $? pmcw_$c
          done ;;
   esac
 done

@@ -4,7 +4,7 @@ and WRITE_SIZE passes (separate runs).  bench.py alternates an untimed populate 
 reads that fill the cache) with the timed q = 0.75 call, so the dispatches are split into calls
 at every k_sc_claim and only the odd (timed) calls are averaged.  Writes
 profiles/pmc_traffic.json[CFG].
-Usage: pmc_traffic_cached.py FETCH_DIR WRITE_DIR CFG WORKLOAD [OUT]"""
+Usage: pmc_traffic_cached.py FETCH_DIR WRITE_DIR CFG WORKLOAD [OUT [ZONE_INDEX]]  (default "none")"""
 import csv
 import glob
 import json
@@ -37,11 +37,12 @@ def calls(d, counter):
 def main():
     fdir, wdir, cfg, workload = sys.argv[1:5]
     out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
+    zone_index = sys.argv[6] if len(sys.argv) > 6 else "none"
     fc, wc = calls(fdir, "FETCH_SIZE"), calls(wdir, "WRITE_SIZE")
     ft, wt = fc[1::2], wc[1::2]  # the timed calls
     fetch_raw = sum(sum(c.values()) for c in ft) / len(ft)
     write = sum(sum(c.values()) for c in wt) / len(wt)
-    d = {"workload": workload, "kernel": "am_snapcache_read: k_sc_* + every materialize tier", "calls": [len(ft), len(wt)],
+    d = {"workload": workload, "zone_index": zone_index, "kernel": "am_snapcache_read: k_sc_* + every materialize tier", "calls": [len(ft), len(wt)],
          "fetch_raw_bytes_per_launch": fetch_raw, "fetch_bytes_per_launch": 2 * fetch_raw,
          "write_bytes_per_launch": write, "bytes_per_launch": 2 * fetch_raw + write,
          "per_kernel_fetch_raw": {k: sum(c.get(k, 0.0) for c in ft) / len(ft) for k in sorted({k for c in ft for k in c})},
