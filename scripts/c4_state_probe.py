@@ -1,6 +1,6 @@
 """Experiments only: C4 step time in a fresh process against the same after other device
 work (the bench line's secondary C4 ran 1.17 ms after C3, 1.43 ms in its own process).
-Usage: c4_state_probe.py MODE...  (plain | c3first | c3keep | torchpool | padN | heatN)"""
+Usage: c4_state_probe.py MODE...  (plain | c3first | c3keep | c3store | c3reads | torchpool | padN | heatN)"""
 import ctypes
 import sys
 import time
@@ -34,6 +34,12 @@ def main():
                 keep.append(s3)
             else:
                 s3.close()
+        elif mode == "c3store":  # the C3 store only (library allocations), kept
+            keep.append(mat.synth_store(bench.synth_params(bench.CONFIGS["c3"])))
+        elif mode == "c3reads":  # a C3-sized read batch only (torch allocations), kept
+            c3 = bench.CONFIGS["c3"]
+            keep.append(bench.DeviceReads(c3["n_keys"], c3["n_dc"], c3["type"], [1] * c3["n_dc"],
+                                          set_cap=c3["set_cap"]))
         elif mode == "torchpool":
             x = torch.empty(40 << 30, dtype=torch.uint8, device="cuda")
             del x
@@ -54,7 +60,7 @@ def main():
             print(f"{mode} rep{rep}: {m['dt'] / 20 * 1e3:.3f} ms/step, kernel {m['kern_ms']:.3f} ms", flush=True)
         s4.close()
     for s in keep:
-        if isinstance(s, bench.Step):
+        if hasattr(s, "close"):
             s.close()
     keep.clear()
     mat.L.am_comm_destroy(comm)
