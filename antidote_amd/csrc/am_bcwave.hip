@@ -35,9 +35,33 @@ struct BcSmem {
   uint64_t lo[NS];
   int64_t hi[NS];
   uint32_t pres[NS];
+  uint64_t emx[DMAX];  // batch-clock kernel: LastOpCt maxima of the included escaped ops
 };
 
-template <int DMAX>
+// per-read inputs, wave-uniform (every lane reads the same read; GENERAL false: the batch clock)
+template <int DMAX, bool GENERAL>
+__device__ __forceinline__ void bc_inputs(const am_op_log &L, const am_read_batch &B, uint32_t nd, uint64_t r,
+                                          ReadU<DMAX> &u) {
+  const uint64_t n = B.n_reads;
+  u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+  const uint64_t rstride = (GENERAL && B.per_read_clock) ? n : 1, ridx = (GENERAL && B.per_read_clock) ? r : 0;
+  u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
+  u.base_ignore = !GENERAL || !B.base_ignore || B.base_ignore[r];
+  u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
+    u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
+  }
+  u.has_txid = GENERAL && B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
+  u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
+}
+
+// GENERAL false (the batch clock, no bases / TxIds / op presence): the clock is read once per
+// wave and the tile loop tests the packed entries only; escaped ops (outside the packed view)
+// are evaluated from the full columns in a pass of their own after the loop, so the loop holds
+// neither the base thresholds nor the full-width accumulators (C5: 252 -> fewer VGPRs).
+template <int DMAX, bool GENERAL>
 __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                    am_retry next) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -49,6 +73,8 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
   const uint32_t sel0 = S.idx ? uniform_u32(S.range[0]) : 0u;
   const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : n;
   const uint64_t W = (uint64_t)gridDim.x * NW;
+  ReadU<DMAX> u;
+  if (!GENERAL) bc_inputs<DMAX, false>(L, B, nd, 0, u);
   for (uint64_t i = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6); i < nsel; i += W) {
     const uint64_t r = S.idx ? (uint64_t)uniform_u32(S.idx[sel0 + i]) : i;
     const uint64_t key = uniform_u64(B.key[r]);
@@ -73,60 +99,139 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
       if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
       continue;
     }
-    ReadU<DMAX> u;
-    {  // per-read inputs, wave-uniform (every lane reads the same read)
-      u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
-      const uint64_t rstride = B.per_read_clock ? n : 1, ridx = B.per_read_clock ? r : 0;
-      u.spres = uniform_u32(B.read_pres[ridx]) & u.allmask;
-      u.base_ignore = !B.base_ignore || B.base_ignore[r];
-      u.cpres = u.base_ignore ? 0u : (uniform_u32(B.base_pres[r]) & u.allmask);
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[(uint64_t)d * rstride + ridx]) : 0;
-        u.C0[d] = (d < (int)nd && ((u.cpres >> d) & 1u)) ? uniform_u64(B.base_vc[(uint64_t)d * n + r]) : 0;
-      }
-      u.has_txid = B.txid && (!B.txid_valid || B.txid_valid[r]) && L.op_txid;
-      u.txid = u.has_txid ? uniform_u64(B.txid[r]) : 0;
-    }
+    if (GENERAL) bc_inputs<DMAX, true>(L, B, nd, r, u);
     PkRead<DMAX> pk;
     pk_setup(u, nd, uniform_u64(L.key_tbase[key]), pk);
     // slots start at the base value (orddict entries present in the base stay present)
+    if (lane < DMAX) s.emx[lane] = 0;
     for (uint32_t k = lane; k < ns; k += WAVE) {
       uint32_t bp = 0;
-      const int64_t bv = bc_base(B, r, np, nd, k, bp);
+      const int64_t bv = GENERAL ? bc_base(B, r, np, nd, k, bp) : 0;
       s.lo[k] = (uint64_t)bv;
       s.hi[k] = bv < 0 ? -1 : 0;
       s.pres[k] = bp;
     }
     wave_sync();
 
-    Acc<DMAX> a;
+    Acc<DMAX> a;  // GENERAL false: only after the tile loop (escaped ops, the fold)
     AccP<DMAX> ap;
-    a.reset();
+    if (GENERAL) a.reset();
     ap.reset();
-    for (uint64_t t = off0 & ~(uint64_t)(OPL - 1); t < off1; t += TILE) {
-      const uint64_t g = t + (uint64_t)lane * OPL;
+    // an included op's amount into its slot (exact 128-bit LDS sum) and the slot's presence
+    auto apply = [&](uint32_t meta, int64_t v, uint64_t ft) {
+      if (meta & AM_META_BAD) return;  // reported through FLAG_BAD
+      const uint32_t kind = AM_META_KIND(meta);
+      const uint32_t from = (uint32_t)(ft & 0xFF), to = (uint32_t)((ft >> 8) & 0xFF);
+      if (kind > AM_BC_TRANSFER || from >= nd || to >= nd) {  // Type:update/2 would raise
+        a.flags |= FLAG_BAD;
+        return;
+      }
+      const uint32_t slot = kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
+      acc128_atomic(&s.lo[slot], &s.hi[slot], v < 0 ? -1 : 0, (uint64_t)v);
+      atomicOr(&s.pres[slot], 1u);
+    };
+    bool esc = false;
+    // ops per lane: 4 (16-byte loads); the batch-clock kernel at D > 8 takes 2 so the loaded
+    // entries (OL x D) leave room for a third wave per SIMD
+    constexpr int OL = (!GENERAL && DMAX > 8) ? 2 : OPL;
+    constexpr uint64_t TL = (uint64_t)WAVE * OL;
+    for (uint64_t t = off0 & ~(uint64_t)(OL - 1); t < off1; t += TL) {
+      const uint64_t g = t + (uint64_t)lane * OL;
       if (g >= off1) continue;
-      const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
-      const u64x2 a01 = *(const u64x2 *)(L.p0 + g), a23 = *(const u64x2 *)(L.p0 + g + 2);
-      const u64x2 f01 = *(const u64x2 *)(L.p1 + g), f23 = *(const u64x2 *)(L.p1 + g + 2);
-      const uint64_t amt[OPL] = {a01.x, a01.y, a23.x, a23.y}, ft[OPL] = {f01.x, f01.y, f23.x, f23.y};
-      const uint32_t ib = incl4<DMAX, true>(L, nd, stride, u, pk, g, off0, off1, ap, a);
+      uint32_t meta4;
+      uint64_t amt[OL], ft[OL];
+      if constexpr (OL == 4) {
+        meta4 = *(const uint32_t *)(L.op_meta + g);
+        const u64x2 a01 = *(const u64x2 *)(L.p0 + g), a23 = *(const u64x2 *)(L.p0 + g + 2);
+        const u64x2 f01 = *(const u64x2 *)(L.p1 + g), f23 = *(const u64x2 *)(L.p1 + g + 2);
+        amt[0] = a01.x, amt[1] = a01.y, amt[2] = a23.x, amt[3] = a23.y;
+        ft[0] = f01.x, ft[1] = f01.y, ft[2] = f23.x, ft[3] = f23.y;
+      } else {
+        meta4 = *(const uint16_t *)(L.op_meta + g);
+        const u64x2 a01 = *(const u64x2 *)(L.p0 + g), f01 = *(const u64x2 *)(L.p1 + g);
+        amt[0] = a01.x, amt[1] = a01.y, ft[0] = f01.x, ft[1] = f01.y;
+      }
+      uint32_t ib;
+      if constexpr (GENERAL) {
+        ib = incl4<DMAX, true>(L, nd, stride, u, pk, g, off0, off1, ap, a);
+      } else {
+        uint32_t x[OL][DMAX];
+        uint64_t tx[OL];
 #pragma unroll
-      for (int k = 0; k < OPL; ++k) {
-        if (!((ib >> k) & 1u)) continue;
-        const uint32_t meta = (meta4 >> (8 * k)) & 0xFFu;
-        if (meta & AM_META_BAD) continue;  // reported through FLAG_BAD
-        const uint32_t kind = AM_META_KIND(meta);
-        const uint32_t from = (uint32_t)(ft[k] & 0xFF), to = (uint32_t)((ft[k] >> 8) & 0xFF);
-        if (kind > AM_BC_TRANSFER || from >= nd || to >= nd) {  // Type:update/2 would raise
-          a.flags |= FLAG_BAD;
-          continue;
+        for (int k = 0; k < OL; ++k) tx[k] = 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          uint32_t q[OL];
+          if constexpr (OL == 4) {
+            u32x4 v = {0, 0, 0, 0};
+            if (d < (int)nd) v = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
+            q[0] = v.x, q[1] = v.y, q[2] = v.z, q[3] = v.w;
+          } else {
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            u32x2_t v = {0, 0};
+            if (d < (int)nd) v = *(const u32x2_t *)(L.pk_vc + (uint64_t)d * stride + g);
+            q[0] = v.x, q[1] = v.y;
+          }
+#pragma unroll
+          for (int k = 0; k < OL; ++k) x[k][d] = q[k];
         }
-        const uint32_t slot = kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
-        const int64_t v = (int64_t)amt[k];
-        acc128_atomic(&s.lo[slot], &s.hi[slot], v < 0 ? -1 : 0, (uint64_t)v);
-        atomicOr(&s.pres[slot], 1u);
+        ib = pk_tile<DMAX, OL, false>(u, pk, x, tx, g, off0, off1, ap, esc);
+      }
+#pragma unroll
+      for (int k = 0; k < OL; ++k)
+        if ((ib >> k) & 1u) apply((meta4 >> (8 * k)) & 0xFFu, (int64_t)amt[k], ft[k]);
+    }
+    if (!GENERAL) a.reset();
+    if constexpr (!GENERAL && DMAX <= 8) {
+      if (__ballot(esc)) {  // rare: ops outside the packed view, from the full columns
+        for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
+          if (L.pk_vc[p] != AM_PK_ESC) continue;
+          uint64_t sv[DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+          const uint32_t meta = L.op_meta[p];
+          if (eval_op<DMAX, false>(u, meta, L.commit_time[p], sv, u.allmask, false, p, a))
+            apply(meta, (int64_t)L.p0[p], L.p1[p]);
+        }
+      }
+    } else if constexpr (!GENERAL) {
+      if (__ballot(esc)) {
+        // D > 8: the same, eval_op<DMAX, false> one DC at a time (the clock entry from lane d)
+        // and the included ops' maxima into LDS, so the pass holds no D-wide arrays (it would
+        // set the kernel's register peak)
+        uint64_t vS = 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) vS = (uint32_t)d == lane ? u.S[d] : vS;
+        for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
+          if (L.pk_vc[p] != AM_PK_ESC) continue;
+          const uint32_t meta = L.op_meta[p], dc = meta & 31u;
+          const uint64_t ct = L.commit_time[p];
+          bool incl = true;
+          for (uint32_t d = 0; d < nd; ++d) {
+            if (!((u.spres >> d) & 1u)) {  // logger:error("Could not find DC in SS"); excluded
+              incl = false;
+              a.flags |= AM_FLAG_MISSING_DC_LOGGED;
+              continue;
+            }
+            const uint64_t x = d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p];
+            incl &= x <= lane_u64(vS, d);
+          }
+          if (!incl) {
+            a.min_excl = p < a.min_excl ? p : a.min_excl;
+            continue;
+          }
+          for (uint32_t d = 0; d < nd; ++d) {
+            const uint64_t x = d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p];
+            atomicMax((unsigned long long *)&s.emx[d], (unsigned long long)x);
+          }
+          a.pres |= u.allmask;
+          a.count += 1;
+          if (meta & AM_META_BAD) a.flags |= FLAG_BAD;
+          apply(meta, (int64_t)L.p0[p], L.p1[p]);
+        }
+        wave_sync();
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) a.mx[d] = d < (int)nd ? s.emx[d] : 0;
       }
     }
     pk_fold(ap, pk.K, u.allmask, a);
@@ -202,20 +307,27 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
   }
 }
 
-template <int D>
-int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
+template <int D, bool GENERAL>
+int launch_dg(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
   constexpr size_t smem = sizeof(BcSmem<D>) * NW;
   static int occ = 0;
   if (!occ) {
-    AM_HIP(hipFuncSetAttribute((const void *)k_bc_wave<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bc_wave<D>, BLOCK, smem) != hipSuccess || occ < 1) occ = 1;
+    AM_HIP(hipFuncSetAttribute((const void *)k_bc_wave<D, GENERAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)smem));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bc_wave<D, GENERAL>, BLOCK, smem) != hipSuccess || occ < 1)
+      occ = 1;
   }
   uint64_t blocks = (B->n_reads + NW - 1) / NW, cap = (uint64_t)ctx->n_cu * occ;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
-  hipLaunchKernelGGL((k_bc_wave<D>), dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, *B, *R, S, next);
+  hipLaunchKernelGGL((k_bc_wave<D, GENERAL>), dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, *B, *R, S,
+                     next);
   AM_HIP(hipGetLastError());
   return AM_OK;
+}
+template <int D>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
+  return am_batch_general(L, B) ? launch_dg<D, true>(ctx, L, B, R, S, next) : launch_dg<D, false>(ctx, L, B, R, S, next);
 }
 
 }  // namespace
