@@ -503,13 +503,95 @@ __global__ void __launch_bounds__(BLOCK) k_big_chunk(am_op_log L, am_read_batch 
   }
 }
 
+// ---- LEAN evaluation (packed view, the batch clock: no bases / TxIds / op presence): the clock
+//      is read once per kernel and the chunk loops test the packed entries only; an escaped op
+//      is evaluated from the full columns one DC at a time (lane d's vS holds the clock's entry
+//      d) with its LastOpCt maxima into an LDS array -- the loops hold no D-wide u64 arrays
+//      (D = 16: k_big_gincl 227 -> 155 VGPRs).  eval_op<DMAX, false> semantics. ----
+template <int DMAX>
+__device__ __forceinline__ void lean_clock(const am_read_batch &B, uint32_t nd, uint32_t lane, ReadU<DMAX> &u,
+                                           uint64_t &vS) {
+  u.allmask = nd >= 32 ? 0xFFFFFFFFu : ((1u << nd) - 1u);
+  u.spres = uniform_u32(B.read_pres[0]) & u.allmask;
+  u.base_ignore = true, u.cpres = 0, u.has_txid = false, u.txid = 0;
+  vS = 0;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    u.S[d] = (d < (int)nd && ((u.spres >> d) & 1u)) ? uniform_u64(B.read_vc[d]) : 0;
+    u.C0[d] = 0;
+    vS = (uint32_t)d == lane ? u.S[d] : vS;
+  }
+}
+// the 4 ops [g, g + 4) of a read inside [lo, hi): inclusion bits; packed partials in ap, the
+// escaped ops' count / flags / min in a and their maxima in emx
+template <int DMAX>
+__device__ __forceinline__ uint32_t lean_incl4(const am_op_log &L, uint32_t nd, uint64_t stride, const ReadU<DMAX> &u,
+                                               const PkRead<DMAX> &pk, uint64_t vS, uint64_t g, uint64_t lo,
+                                               uint64_t hi, AccP<DMAX> &ap, Acc<DMAX> &a, unsigned long long *emx) {
+  uint32_t xs[4][DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    u32x4 q = {0, 0, 0, 0};
+    if (d < (int)nd) q = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
+    xs[0][d] = q.x, xs[1][d] = q.y, xs[2][d] = q.z, xs[3][d] = q.w;
+  }
+  const uint64_t tx[4] = {0, 0, 0, 0};
+  bool esc = false;
+  uint32_t ib = pk_tile<DMAX, 4, false>(u, pk, xs, tx, g, lo, hi, ap, esc);
+  if (!esc) return ib;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {  // rare
+    const uint64_t p = g + k;
+    if (p < lo || p >= hi || L.pk_vc[p] != AM_PK_ESC) continue;
+    const uint32_t meta = L.op_meta[p], dc = meta & 31u;
+    const uint64_t ct = L.commit_time[p];
+    bool in = true;
+    for (uint32_t d = 0; d < nd; ++d) {
+      if (!((u.spres >> d) & 1u)) {  // logger:error("Could not find DC in SS"); excluded
+        in = false;
+        a.flags |= AM_FLAG_MISSING_DC_LOGGED;
+        continue;
+      }
+      in &= (d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p]) <= lane_u64(vS, d);
+    }
+    if (!in) {
+      a.min_excl = p < a.min_excl ? p : a.min_excl;
+      continue;
+    }
+    for (uint32_t d = 0; d < nd; ++d)
+      atomicMax(&emx[d], (unsigned long long)(d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p]));
+    a.pres |= u.allmask;
+    a.count += 1;
+    if (meta & AM_META_BAD) a.flags |= FLAG_BAD;
+    ib |= 1u << k;
+  }
+  return ib;
+}
+// a wave's LastOpCt maxima of the read (LEAN: from the packed partials; else from a) and the
+// packed partials folded into a's counts
+template <int DMAX, bool PACKED, bool LEAN>
+__device__ __forceinline__ void wave_partials(AccP<DMAX> &ap, const PkRead<DMAX> &pk, const ReadU<DMAX> &u,
+                                              uint32_t nd, Acc<DMAX> &a, uint64_t (&mx)[DMAX]) {
+  if constexpr (LEAN) {
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? wave_max_u64(ap.count ? pk.K + ap.mx[d] : 0) : 0;
+    a.count += ap.count, a.flags |= ap.flags;
+    if (ap.count) a.pres |= u.allmask;
+    a.min_excl = umin64(a.min_excl, ap.min_excl);
+  } else {
+    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? wave_max_u64(a.mx[d]) : 0;
+  }
+}
+
 // ---- runs of chunks: grouped-mode MV reads and bounded-counter reads.  A workgroup takes a
 //      contiguous run of 1024-op chunks, so a read's partials stay on the workgroup across its
 //      chunks -- the scalar partials in registers, the bounded counter's slot sums in LDS --
 //      and reach the read's accumulators once per read and workgroup (k_big_chunk reduces and
 //      flushes every chunk).  LDS holds only what the type needs: MV the two hash sets, the
 //      bounded counter its slot sums (k_big_chunk's 64 KB allow two workgroups per CU). ----
-template <int DMAX, int TYPE, bool PACKED>
+template <int DMAX, int TYPE, bool PACKED, bool LEAN = false>
 __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
                                                    const BigRead *br, BigAcc *accs, uint32_t *bm, BigSlots SL,
                                                    uint64_t n_gch) {
@@ -522,6 +604,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
   uint32_t *spres = reinterpret_cast<uint32_t *>(lds + (size_t)NS * 16);
   __shared__ uint32_t incl[CHUNK / 32];
   __shared__ uint64_t red[BLOCK / WAVE][DMAX + 4];
+  __shared__ unsigned long long emx[DMAX];  // LEAN: the read's escaped ops' LastOpCt maxima
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
   const uint32_t nbig = uniform_u32(*nbig_p);
   const uint64_t n = B.n_reads;
@@ -537,13 +620,12 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
   AccP<DMAX> ap;
   Acc<DMAX> a;
   // the read's partials -> its accumulators (one LDS round over the waves)
+  uint64_t vS = 0;  // LEAN: lane d holds the clock's entry d
   auto flush = [&]() {
-    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
+    uint64_t mx[DMAX];
+    wave_partials<DMAX, PACKED, LEAN>(ap, pk, u, nd, a, mx);
     const uint32_t cnt = wave_sum_u32(a.count), fl = wave_or_u32(a.flags), pr = wave_or_u32(a.pres);
     const uint64_t mn = wave_min_u64(a.min_excl);
-    uint64_t mx[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? wave_max_u64(a.mx[d]) : 0;
     if (lane == 0) {
       red[wv][0] = cnt, red[wv][1] = fl, red[wv][2] = pr, red[wv][3] = mn;
 #pragma unroll
@@ -556,6 +638,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
         const uint64_t y = red[w][tid];
         v = tid == 0 ? v + y : (tid <= 2 ? (v | y) : tid == 3 ? (v < y ? v : y) : (v > y ? v : y));
       }
+      if (LEAN && tid >= 4) v = v > emx[tid - 4] ? v : emx[tid - 4];
       BigAcc *acc = accs + cur;
       if (tid == 0 && v) atomicAdd(&acc->count, (uint32_t)v);
       if (tid == 1 && v) atomicOr(&acc->flags, (uint32_t)v);
@@ -577,12 +660,22 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     for (uint32_t i = tid; i < SL.ns; i += BLOCK) slo[i] = 0, shi[i] = 0, spres[i] = 0;
     __syncthreads();
   }
+  if constexpr (LEAN) lean_clock<DMAX>(B, nd, lane, u, vS);
   for (uint64_t x = x0; x < x1; ++x) {
     // a workgroup's run mostly stays in one read: search the read list (a chain of dependent
     // loads) only when x leaves the current read's chunks
     const bool same = cur != 0xFFFFFFFFu && x < R0.gchunk0 + ((R0.off1 - (R0.off0 & ~(uint64_t)(OPL - 1)) + CHUNK - 1) / CHUNK);
     const uint32_t b = same ? cur : find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
-    if (b != cur) {
+    if (b != cur && LEAN) {
+      if (cur != 0xFFFFFFFFu) flush();
+      cur = b;
+      R0 = br[b];
+      if (tid < DMAX) emx[tid] = 0;
+      __syncthreads();
+      pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[R0.r])]), pk);
+      ap.reset();
+      a.reset();
+    } else if (b != cur) {
       if (cur != 0xFFFFFFFFu) flush();
       cur = b;
       R0 = br[b];
@@ -609,7 +702,8 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     if (TYPE == AM_BCOUNTER) {  // included ops -> LDS slot sums (orddict:update_counter)
       if (g < hi) {
         const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
-        const uint32_t ib = incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
+        const uint32_t ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, vS, g, R0.off0, hi, ap, a, emx)
+                                 : incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
 #pragma unroll
         for (int k = 0; k < OPL; ++k) {
           if (!((ib >> k) & 1u)) continue;
@@ -631,7 +725,8 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     if (tid < CHUNK / 32) incl[tid] = 0;
     __syncthreads();
     if (g < hi) {
-      const uint32_t ib = incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
+      const uint32_t ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, vS, g, R0.off0, hi, ap, a, emx)
+                               : incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
       if (ib) atomicOr(&incl[(uint32_t)(g - lo) >> 5], ib << ((uint32_t)(g - lo) & 31u));
     }
     __syncthreads();
@@ -647,10 +742,16 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
 //                   read and workgroup -- a streaming kernel with no LDS state
 //      k_big_grec   per chunk: the records against those bits, the chunk's births and kills
 //                   settled in the LDS hash sets (grouped_records), the rest exported ----
-template <int DMAX, bool PACKED>
+//      LEAN (packed view, the batch clock: no bases / TxIds / op presence): the clock is read
+//      once, the chunk loop tests the packed entries only, and an escaped op is evaluated one DC
+//      at a time with its LastOpCt maxima into LDS -- no D-wide u64 arrays in the loop (D = 16:
+//      227 -> fewer VGPRs)
+template <int DMAX, bool PACKED, bool LEAN = false>
 __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
                                                      const BigRead *br, BigAcc *accs, uint32_t *ibm, uint64_t n_gch) {
+  static_assert(!LEAN || PACKED, "the lean pass reads the packed view");
   __shared__ uint64_t red[BLOCK / WAVE][DMAX + 4];
+  __shared__ unsigned long long emx[DMAX];  // LEAN: the read's escaped ops' LastOpCt maxima
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
   const uint32_t nbig = uniform_u32(*nbig_p);
   const uint32_t nd = L.n_dc;
@@ -664,13 +765,12 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
   PkRead<DMAX> pk;
   AccP<DMAX> ap;
   Acc<DMAX> a;
+  uint64_t vS = 0;  // LEAN: lane d holds the clock's entry d
   auto flush = [&]() {
-    if (PACKED) pk_fold(ap, pk.K, u.allmask, a);
+    uint64_t mx[DMAX];
+    wave_partials<DMAX, PACKED, LEAN>(ap, pk, u, nd, a, mx);
     const uint32_t cnt = wave_sum_u32(a.count), fl = wave_or_u32(a.flags), pr = wave_or_u32(a.pres);
     const uint64_t mn = wave_min_u64(a.min_excl);
-    uint64_t mx[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? wave_max_u64(a.mx[d]) : 0;
     if (lane == 0) {
       red[wv][0] = cnt, red[wv][1] = fl, red[wv][2] = pr, red[wv][3] = mn;
 #pragma unroll
@@ -683,6 +783,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
         const uint64_t y = red[w][tid];
         v = tid == 0 ? v + y : (tid <= 2 ? (v | y) : tid == 3 ? (v < y ? v : y) : (v > y ? v : y));
       }
+      if (LEAN && tid >= 4) v = v > emx[tid - 4] ? v : emx[tid - 4];
       BigAcc *acc = accs + cur;
       if (tid == 0 && v) atomicAdd(&acc->count, (uint32_t)v);
       if (tid == 1 && v) atomicOr(&acc->flags, (uint32_t)v);
@@ -692,10 +793,20 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
     }
     __syncthreads();
   };
+  if constexpr (LEAN) lean_clock<DMAX>(B, nd, lane, u, vS);
   for (uint64_t x = x0; x < x1; ++x) {
     const bool same = cur != 0xFFFFFFFFu && x < R0.gchunk0 + ((R0.off1 - (R0.off0 & ~(uint64_t)(OPL - 1)) + CHUNK - 1) / CHUNK);
     const uint32_t b = same ? cur : find_read(br, nbig, x, [](const BigRead &v) { return v.gchunk0; });
-    if (b != cur) {
+    if (b != cur && LEAN) {
+      if (cur != 0xFFFFFFFFu) flush();
+      cur = b;
+      R0 = br[b];
+      if (tid < DMAX) emx[tid] = 0;
+      __syncthreads();
+      pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[R0.r])]), pk);
+      ap.reset();
+      a.reset();
+    } else if (b != cur) {
       if (cur != 0xFFFFFFFFu) flush();
       cur = b;
       R0 = br[b];
@@ -720,7 +831,10 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
     const uint64_t t0 = R0.off0 & ~(uint64_t)(OPL - 1), c = x - R0.gchunk0;
     const uint64_t lo = t0 + c * CHUNK, hi = lo + CHUNK < R0.off1 ? lo + CHUNK : R0.off1;
     const uint64_t g = lo + (uint64_t)tid * OPL;
-    const uint32_t ib = g < hi ? incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a) : 0u;
+    uint32_t ib = 0;
+    if (g < hi)
+      ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, vS, g, R0.off0, hi, ap, a, emx)
+                : incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
     uint32_t word = ib << (OPL * (tid % 8));  // 8 lanes of 4 ops per 32-bit word
     word |= (uint32_t)__shfl_xor((int)word, 1);
     word |= (uint32_t)__shfl_xor((int)word, 2);
@@ -986,7 +1100,10 @@ int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_res
   if constexpr (TYPE == AM_MVREG) if (n_gch) {  // grouped MV reads: inclusion pass, record pass
     const uint64_t gcap = (uint64_t)ctx->n_cu * 8;
     const unsigned g4 = (unsigned)(n_gch < gcap ? n_gch : gcap);
-    if (am_log_packed(L))
+    if (am_log_packed(L) && !am_batch_general(L, B))
+      hipLaunchKernelGGL((k_big_gincl<DMAX, true, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br,
+                         acc, G.ibm, n_gch);
+    else if (am_log_packed(L))
       hipLaunchKernelGGL((k_big_gincl<DMAX, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br, acc,
                          G.ibm, n_gch);
     else
@@ -1000,7 +1117,10 @@ int run_big(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_res
   if constexpr (TYPE == AM_BCOUNTER) if (n_gch) {  // runs of chunks: bounded-counter reads
     const uint64_t gcap = (uint64_t)ctx->n_cu * 8;
     const unsigned g4 = (unsigned)(n_gch < gcap ? n_gch : gcap);
-    if (am_log_packed(L))
+    if (am_log_packed(L) && !am_batch_general(L, B))
+      hipLaunchKernelGGL((k_big_run<DMAX, TYPE, true, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br,
+                         acc, G.bm, SL, n_gch);
+    else if (am_log_packed(L))
       hipLaunchKernelGGL((k_big_run<DMAX, TYPE, true>), dim3(g4), dim3(BLOCK), 0, ctx->stream, *L, *B, nbig_d, br, acc,
                          G.bm, SL, n_gch);
     else
