@@ -25,7 +25,6 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int NW = BLOCK / WAVE;
 constexpr int OPL = 4;
-constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
 constexpr uint64_t BCW_OPS = 4096;  // longer logs: the chunked big-read tier (a wave streaming 32768 ops
                                       // alone was the tail of C5 at the 32768 limit)
 
