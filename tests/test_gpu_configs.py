@@ -104,3 +104,46 @@ def test_config_mixed_batch_parity(mat, name):
                int(h["flags"][i]))
         assert got == ref.result(j), (name, int(i), int(ktypes[i]), got, ref.result(j))
     st.close()
+
+
+def test_config_mixed_batch_foreign_types(mat):
+    """A mixed batch over an MV + bounded-counter log whose reads also name types the log has no
+    keys of (AW set, PN, LWW) or the other present type: every such read of a key with ops gets
+    corrupted_ops_cache (src/clocksi_materializer.erl:190-191) -- the planner skips the chains of
+    absent set types, so those statuses must come from the lane tier -- and the rest stay exact."""
+    p = synth.params(**SHAPES["c5_mv_bc_zipf"])
+    st = mat.synth_store(p)
+    dlog = st.device_log()
+    hlog = synth.host_log(p, 0, p.n_keys)
+    ktypes = hlog.key_type[:p.n_keys].copy()
+    lens = np.diff(hlog.key_off.astype(np.int64))[:p.n_keys]
+    rtypes = ktypes.copy()
+    idx = np.arange(p.n_keys)
+    rtypes[idx % 7 == 3] = abi.AM_AWSET
+    rtypes[idx % 11 == 5] = abi.AM_PN
+    rtypes[idx % 13 == 6] = abi.AM_LWW
+    swap = idx % 17 == 8  # the other present type
+    rtypes[swap] = np.where(ktypes[swap] == abi.AM_MVREG, abi.AM_BCOUNTER, abi.AM_MVREG)
+    clock = synth.read_clock(p, 0.75)
+    dr = DeviceReads(p.n_keys, p.n_dc, 0, clock, set_cap=128, types=torch.from_numpy(rtypes).cuda())
+    torch.cuda.synchronize()
+    materialize(mat, dlog, dr)
+    mat.sync()
+    h = dr.host()
+    foreign = (rtypes != ktypes) & (lens > 0)
+    assert foreign.sum() > 0
+    assert (h["status"][foreign] == abi.AM_ERR_CORRUPTED_OPS_CACHE).all(), \
+        np.unique(h["status"][foreign], return_counts=True)
+    assert (h["status"][~foreign] == 0).all(), np.unique(h["status"][~foreign], return_counts=True)
+    rng = np.random.default_rng(9)
+    sample = np.sort(rng.choice(np.flatnonzero(~foreign), 200, replace=False))
+    reads = [Read(int(k), int(ktypes[k]), {d: clock[d] for d in range(p.n_dc)}) for k in sample]
+    ref = amo.materialize(hlog, HostBatch(p.n_dc, reads, randlog.caps_for(reads, p.n_dc, 128)))
+    vals = dr.values(sample)
+    for j, i in enumerate(sample):
+        ct = None if h["last_ct_ignore"][i] else {d: int(h["last_ct"][d, i]) for d in range(p.n_dc)
+                                                  if (int(h["last_ct_pres"][i]) >> d) & 1}
+        got = ("ok", vals[j], int(h["new_last_op"][i]), ct, bool(h["is_new_ss"][i]), int(h["count"][i]),
+               int(h["flags"][i]))
+        assert got == ref.result(j), (int(i), got, ref.result(j))
+    st.close()
