@@ -433,12 +433,8 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   uint32_t *range = nullptr, *idx = nullptr;
   rc = plan(ctx, AM_SCR_PLAN, in, n_in, true, mv_early, &range, &idx);
   if (!rc && hipEventRecord(ctx->ev_fork, ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
-  // a set type the lane tier takes, without keys in the log, has no hand-offs after the lane
-  // tier (its reads of other types' keys got their error status there): its chain is not
-  // launched (on C5 the AW chain's empty tiers still took CU slots from the others)
   for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t)
-    if ((t != AM_BCOUNTER || !bc_early) && (!((lanes >> t) & 1u) || ((types >> t) & 1u)))
-      rc = start_chain(t, idx, range, false);
+    if (t != AM_BCOUNTER || !bc_early) rc = start_chain(t, idx, range, false);
   for (uint32_t t = AM_PN; t <= AM_LWW && !rc; ++t) {
     am_sel S;
     S.idx = idx;
