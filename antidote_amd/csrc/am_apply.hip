@@ -370,7 +370,22 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   const am_op_log &S = sub->dev;
   bool cols = !(S.snap_pres && !L.snap_pres) && !(S.var_off && !L.var_off) && !(L.pk_vc && !S.pk_vc) &&
               !(S.rec_key_off && !L.rec_key_off) && !(S.gmask && !L.gmask);
-  if (cols && ((S.op_id && !L.op_id) || (S.op_txid && !L.op_txid))) {  // turn the column on (O(store), once)
+  uint64_t fit = 0;
+  if (cols || check_keys) {
+    if (cols) hipLaunchKernelGGL(k_fit, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, S, d_keys, m, nofit);
+    if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
+    uint64_t w = 0;
+    if (!rc) rc = am_ctx_fetch(c, nofit, 1, &w);
+    if (!rc && (w & (AM_BADKEY_RANGE | AM_BADKEY_DUP))) {
+      am_set_error("am_store_apply: %s", (w & AM_BADKEY_RANGE) ? "a touched key is outside the store's key space"
+                                                               : "a touched key appears twice in the list");
+      rc = AM_ERR_INVALID;
+    }
+    fit = cols && (w & 0xFFFFFFFFull) == 0;
+  }
+  // a column the store lacks (its first gap in op ids, its first TxId) is turned on only once the
+  // key check and the fit have passed: a failing call writes nothing into the store
+  if (!rc && fit && ((S.op_id && !L.op_id) || (S.op_txid && !L.op_txid))) {  // turn the column on (O(store), once)
     const size_t na = L.snap_stride ? L.snap_stride : L.n_ops;
     void *ids = nullptr, *tx = nullptr;
     if (S.op_id && !L.op_id && !rc) rc = am_dev_alloc(c, na * 8 + 8, &ids);
@@ -387,19 +402,6 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
     }
     if (ids) st->allocs.push_back(ids), L.op_id = (const uint64_t *)ids;
     if (tx) st->allocs.push_back(tx), L.op_txid = (const uint64_t *)tx;
-  }
-  uint64_t fit = 0;
-  if (cols || check_keys) {
-    if (cols) hipLaunchKernelGGL(k_fit, dim3(grid_threads(m)), dim3(256), 0, c->stream, L, S, d_keys, m, nofit);
-    if (hipGetLastError() != hipSuccess) rc = AM_ERR_HIP;
-    uint64_t w = 0;
-    if (!rc) rc = am_ctx_fetch(c, nofit, 1, &w);
-    if (!rc && (w & (AM_BADKEY_RANGE | AM_BADKEY_DUP))) {
-      am_set_error("am_store_apply: %s", (w & AM_BADKEY_RANGE) ? "a touched key is outside the store's key space"
-                                                               : "a touched key appears twice in the list");
-      rc = AM_ERR_INVALID;
-    }
-    fit = cols && (w & 0xFFFFFFFFull) == 0;
   }
   if (!rc && fit) {
     hipLaunchKernelGGL(k_writeback, dim3(grid_waves(m)), dim3(256), 0, c->stream, L, S,

@@ -445,7 +445,11 @@ __device__ __forceinline__ QMeta q_meta(const am_op_log &L, const am_read_result
   m.ok = p.ok && p.key < L.n_keys;
   const uint64_t k = m.ok ? p.key : 0;
   const uint64_t *ke = L.key_end ? L.key_end : L.key_off + 1;
-  const uint64_t *rke = L.rec_key_end ? L.rec_key_end : L.rec_key_off + 1;
+  // a log without the token-group view (no set read is taken then: am_lane_accept) reads
+  // dummies from key_off
+  const uint64_t *rko = L.rec_key_off ? L.rec_key_off : L.key_off;
+  const uint64_t *rke = L.rec_key_end ? L.rec_key_end : rko + 1;
+  const uint32_t *kng = L.key_ngrp ? L.key_ngrp : (const uint32_t *)L.key_off;
   m.off0 = L.key_off[k];
   m.off1 = ke[k];
   m.kt = L.key_type[k];
@@ -454,8 +458,8 @@ __device__ __forceinline__ QMeta q_meta(const am_op_log &L, const am_read_result
   m.idb = (L.key_id_base ? L.key_id_base : L.key_off)[k];  // (key_off: a dummy, unused)
   // set fields for every read: the block's reads cover one span of each column, so the
   // lines are fetched whatever the types
-  m.G = L.key_ngrp[k];
-  m.rk0 = L.rec_key_off[k];
+  m.G = kng[k];
+  m.rk0 = rko[k];
   m.rk1 = rke[k];
   const uint64_t *so = R.value.set_off ? R.value.set_off : L.key_off;  // (key_off: a dummy)
   m.ooff = so[m.r];

@@ -21,8 +21,6 @@
 // big-read path, which sizes its scratch on the host (one synchronization).  In a mixed
 // batch every set type's chain runs on a stream of its own (am_ctx::sub), joined back
 // before the call returns: a type's latency-bound tiers overlap the other types' tiers.
-#include <sched.h>
-
 #include "am_wave.h"
 
 using namespace amk;
@@ -46,7 +44,9 @@ __device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read
     if (write_status) R.status[r] = AM_ERR_INVALID;
     return CLS_DONE;
   }
-  if (mvbig && t == AM_MVREG && L.key_type[key] == AM_MVREG && am_ngrp_big(L.key_ngrp[key])) return CLS_MVBIG;
+  // (mvbig comes from a per-log cache that may be stale: the log itself must have the view)
+  if (mvbig && t == AM_MVREG && L.key_type[key] == AM_MVREG && L.key_ngrp && L.rec_g && am_ngrp_big(L.key_ngrp[key]))
+    return CLS_MVBIG;
   return t;
 }
 
@@ -248,7 +248,8 @@ int run_sets(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
 // The set chains' big tiers, each launched once its chain's front has drained (its hand-off
 // count is read back to size the big tier): in the order the chains finish, not in type order
 // -- a host readback that waits on a slow chain would hold back a finished one's big tier
-// (C5: the bounded-counter chain drains ~1 ms before the MV chain).
+// (C5: the bounded-counter chain drains ~1 ms before the MV chain).  Between polls the host
+// blocks on one chain's event instead of spinning.
 int launch_bigs_when_ready(am_ctx *const sub[3], const am_op_log *L, const am_read_batch *B, am_read_result *R,
                            const am_retry retry[3]) {
   bool pend[3];
@@ -266,7 +267,14 @@ int launch_bigs_when_ready(am_ctx *const sub[3], const am_op_log *L, const am_re
       pend[i] = false, --left, ++done;
       if (int rc = am_launch_big(sub[i], L, B, R, AM_AWSET + (uint32_t)i, retry[i])) return rc;
     }
-    if (left && !done) sched_yield();
+    if (left && !done) {  // block on the chain expected to drain first (bounded counter, then AW, MV)
+      // rather than spin a host core beside the RCCL / read-server threads
+      for (int i : {2, 0, 1})
+        if (pend[i]) {
+          AM_HIP(hipEventSynchronize(sub[i]->ev1));
+          break;
+        }
+    }
   }
   return AM_OK;
 }

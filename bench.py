@@ -297,15 +297,31 @@ def cpu_baseline(cfg, p, budget_s=10.0, cached=False):
                       f"C restatement of clocksi_materializer (oracle/am_oracle.c), not BEAM"}
 
 
+def src_sha16() -> str:
+    """Hash of the library's kernel and ABI sources (antidote_amd/csrc, include/antidote_mat.h):
+    stamps a PMC traffic record with the code it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(HERE, "antidote_amd", "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".h")))
+    for f in files + [os.path.join(HERE, "include", "antidote_mat.h")]:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(config: str, workload: str, zone_index: str = "none"):
     """HBM bytes per materialize launch from the committed PMC summary, if it matches the
-    workload and the store's zone index."""
+    workload, the store's zone index AND the library sources this run uses (src_sha16): a
+    record taken on other kernels is not reported (traffic null)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(config, d)
-        if e.get("workload") == workload and e.get("zone_index", "") == zone_index:
+        if (e.get("workload") == workload and e.get("zone_index", "") == zone_index
+                and e.get("src_sha16") == src_sha16()):
             return e.get("calibrated_bytes_per_launch", e.get("bytes_per_launch"))
     except Exception:
         pass
@@ -524,7 +540,8 @@ def main():
                     help="zone index of the headline store (am_store_index); the headline streams every op "
                          "(none) unless asked otherwise")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the secondary lines (c3: cached c3, the indexed reads and c4; single GPU only)")
+                    help="skip the secondary lines (c3: cached c3, the indexed reads, c4, c5 and c2; single GPU "
+                         "only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -607,7 +624,7 @@ def main():
                            "q=0.5, materialize/4, write-back); cache rebuilt between steps, untimed; HIP-event "
                            "timing of each step",
                    "base": args.base, "zone_index": INDEX_NAMES[level],
-                   "store_build_s": st.build_s},
+                   "store_build_s": st.build_s, "src_sha16": src_sha16()},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
@@ -656,10 +673,13 @@ def main():
         st.close()
         st = None
         # the north-star mix (BASELINE.json configs[3] per GPU)
-        s4 = Step(mat, comm, CONFIGS["c4"], rank, world, abi.AM_INDEX_NONE)
-        m4 = measure(s4, "fresh", ksteps, 2, barrier, pg)
-        sec["c4"] = summary(s4, m4, world, "c4: " + CONFIGS["c4"]["desc"])
-        s4.close()
+        # the other BASELINE.json configs, each on its own store (C4: the north-star mix)
+        for c in ("c4", "c5", "c2"):
+            sx = Step(mat, comm, CONFIGS[c], rank, world, abi.AM_INDEX_NONE)
+            mx = measure(sx, "fresh", ksteps, 2, barrier, pg)
+            sec[c] = summary(sx, mx, world, f"{c}: " + CONFIGS[c]["desc"])
+            sec[c]["traffic"] = load_traffic(c, f"{c}: " + CONFIGS[c]["desc"], "none")
+            sx.close()
         out["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         p = st.p if st is not None else synth_params(cfg, rank, world)

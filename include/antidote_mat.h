@@ -360,7 +360,9 @@ int am_store_destroy(am_store *st);
  * AM_INDEX_ZONES keeps the per-block upper bounds only (base-snapshot reads skip the blocks
  * inside their base; no exact marks), AM_INDEX_EXACT adds the exact marks (fresh reads take an
  * exact block inside their clock whole), AM_INDEX_SUMMARIES adds the group summaries (the
- * default every store builder leaves).  Rebuilds from the op columns; blocks until done. */
+ * default every store builder leaves).  Rebuilds from the op columns; blocks until done.
+ * It frees and replaces the store's zone_vc / zone_gsum buffers: an am_op_log obtained from
+ * am_store_log before the call holds stale pointers and must be fetched again. */
 #define AM_INDEX_NONE 0
 #define AM_INDEX_ZONES 1
 #define AM_INDEX_EXACT 2
@@ -513,7 +515,9 @@ int am_store_update(am_ctx *ctx, const am_store *st, const am_op_log *dev_new, c
  * NULL) receives AM_GC_*.  Cost O(the touched keys' ops).  *applied = 0 when some touched key
  * would outgrow its room (or the store has none): nothing is written, and the caller rebuilds
  * with am_store_update (+ am_store_reserve).  Readers of the store must not run concurrently
- * (the context lock serializes library calls).  Blocks. */
+ * (the context lock serializes library calls).  Blocks.  A call that fails (AM_ERR_INVALID: a
+ * touched key outside the store or repeated) writes nothing into the store; gc_flags is then
+ * unspecified. */
 int am_store_reserve(am_ctx *ctx, const am_store *st, am_store **out);
 int am_store_apply(am_ctx *ctx, am_store *st, uint64_t n_touched, const uint64_t *keys, const am_op_log *dev_new,
                    const uint8_t *prune_mask, const uint64_t *thr_vc, const uint32_t *thr_pres, uint8_t *gc_flags,

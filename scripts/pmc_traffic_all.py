@@ -46,6 +46,10 @@ def main():
         allc = json.load(open(out))
     except Exception:
         allc = {}
+    # the sources the passes ran (bench.py reports traffic only for a record of its own sources)
+    sys.path.insert(0, ".")
+    from bench import src_sha16
+    d["src_sha16"] = src_sha16()
     allc[cfg] = d
     json.dump(allc, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in d.items() if not k.startswith("per_kernel")}))

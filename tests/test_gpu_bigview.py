@@ -121,3 +121,47 @@ def test_gpu_chunked_view_token_born_twice(mat):
     hi = ops[-1].commit_time
     _, ng = _compare(mat, log, [Read(0, abi.AM_MVREG, {d: hi for d in range(3)})], cap=64)
     assert int(ng[0]) == NGRP_NONE
+
+
+def test_gpu_stale_type_cache_log_without_groups(mat):
+    """The per-log type mask is cached on the context by the key_type pointer (am_plan.hip
+    log_types) and may be stale: a log that shares key_type with a big-MV store but has no
+    token-group view (key_ngrp / rec_g / gmask absent) must still read correctly -- the early
+    big-MV class and the lane tier's metadata loads guard on the log itself."""
+    import ctypes
+
+    import torch
+
+    from antidote_amd.devbatch import DeviceReads, materialize
+    rng = random.Random(11)
+    n_dc = 3
+    keys = [_chain(n_dc, 2000)] + [randlog.rand_key_ops(rng, abi.AM_PN, n_dc, rng.choice([0, 5, 16])) for _ in range(40)]
+    keys += [_chain(n_dc, 7)]
+    types = [abi.AM_MVREG] + [abi.AM_PN] * 40 + [abi.AM_MVREG]
+    log = HostLog(n_dc, keys, key_types=types)
+    st = mat.store(log)
+    try:
+        full = st.device_log()
+        bare = abi.am_op_log()
+        ctypes.pointer(bare)[0] = full
+        for f in ("key_ngrp", "rec_key_off", "rec_key_end", "rec_g", "grp", "gmask", "zone_vc", "zone_gsum"):
+            setattr(bare, f, None)
+        bare.n_rec = 0
+        clock = [10 ** 6] * n_dc
+        tt = torch.tensor(types, dtype=torch.uint8, device="cuda")
+        for L in (full, bare, full, bare):  # the mask is cached from the first (full) log
+            dr = DeviceReads(len(keys), n_dc, 0, clock, set_cap=64, types=tt)
+            materialize(mat, L, dr)
+            mat.sync()
+            reads = [Read(k, types[k], {d: clock[d] for d in range(n_dc)}) for k in range(len(keys))]
+            ref = amo.materialize(log, HostBatch(n_dc, reads, [64] * len(keys)))
+            h = dr.host()
+            vals = dr.values(range(len(keys)))
+            for i in range(len(keys)):
+                ct = None if h["last_ct_ignore"][i] else {d: int(h["last_ct"][d, i]) for d in range(n_dc)
+                                                          if (int(h["last_ct_pres"][i]) >> d) & 1}
+                got = ("ok", vals[i], int(h["new_last_op"][i]), ct, bool(h["is_new_ss"][i]), int(h["count"][i]),
+                       int(h["flags"][i])) if h["status"][i] == 0 else ("error", int(h["status"][i]))
+                assert got == ref.result(i), (i, got, ref.result(i))
+    finally:
+        st.close()
