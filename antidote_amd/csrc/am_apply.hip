@@ -213,6 +213,13 @@ __global__ void __launch_bounds__(256) k_writeback(am_op_log L, am_op_log S, con
         ng = S.key_ngrp[i];
         uint32_t *rg = const_cast<uint32_t *>(L.rec_g);
         for (uint64_t r = lane; r < nr; r += WAVE_SZ) rg[r0 + r] = S.rec_g[sr0 + r];
+        if (L.prec && S.prec) {  // the birth-ordered pairs travel with their records
+          uint64_t *pr = const_cast<uint64_t *>(L.prec);
+          for (uint64_t r = lane; r < nr; r += WAVE_SZ) {
+            pr[2 * (r0 + r)] = S.prec[2 * (sr0 + r)];
+            pr[2 * (r0 + r) + 1] = S.prec[2 * (sr0 + r) + 1];
+          }
+        }
         uint64_t *gp = const_cast<uint64_t *>(L.grp);
         const uint32_t ngc = am_ngrp_count(ng);
         for (uint32_t g = lane; g < ngc; g += WAVE_SZ) {
@@ -355,7 +362,7 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   view.n_keys = m;
   view.key_off = V.off, view.key_end = V.end, view.key_id_base = V.idb, view.key_type = V.type, view.key_flags = V.flags;
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
-  view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr;
+  view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr, view.prec = nullptr;
   am_store *sub = nullptr;
   int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
                               false, nullptr, &sub);
@@ -496,7 +503,7 @@ int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint
   view.key_off = (uint64_t *)b, view.key_end = (uint64_t *)(b + o_end), view.key_id_base = (uint64_t *)(b + o_idb);
   view.key_type = (uint8_t *)(b + o_type), view.key_flags = (uint8_t *)(b + o_flags);
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
-  view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr;
+  view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr, view.prec = nullptr;
   hipLaunchKernelGGL(k_grow_view, dim3(grid_threads(n_new + 1)), dim3(256), 0, c->stream, L,
                      (const uint64_t *)st->counter, n_new, (uint64_t *)view.key_off, (uint64_t *)view.key_end,
                      (uint64_t *)view.key_id_base, (uint64_t *)(b + o_ctr), (uint8_t *)view.key_type,

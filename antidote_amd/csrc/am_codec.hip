@@ -516,6 +516,15 @@ __global__ void k_store_relabel(am_op_log L, uint64_t *p0, uint64_t *p1, uint64_
         relabel_word(grp + 2 * (r0 + j), old, nw, n);
         relabel_word(grp + 2 * (r0 + j) + 1, old, nw, n);
       }
+      if (L.prec && L.rec_g && !am_ngrp_big(L.key_ngrp[k])) {  // the birth-ordered pairs of its births
+        uint64_t *pr = const_cast<uint64_t *>(L.prec);
+        for (uint64_t r = r0 + lane; r < am_rkend(L, k); r += 64) {
+          const uint32_t x = L.rec_g[r];
+          if (x == 0xFFFFFFFFu || (x & AM_REC_KILL)) continue;
+          relabel_word(pr + 2 * r, old, nw, n);
+          relabel_word(pr + 2 * r + 1, old, nw, n);
+        }
+      }
     }
   }
 }

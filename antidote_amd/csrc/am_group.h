@@ -1392,7 +1392,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
 // first two record chunks in flight while it applies this read's records and gathers its
 // survivors; LDS per wave is a few KB (survivor list in rounds), so ~5 waves per SIMD.
 constexpr uint32_t RCH = 512;    // records per chunk: two 16-byte loads per lane
-constexpr uint32_t RLIST = 512;  // survivor-list entries per gather round
+constexpr uint32_t RLIST = 256;  // survivor-list entries per gather round
 struct RSlot {
   uint64_t off0, rk0, ooff;
   uint32_t r, nops, nrec, G, ocap, ok;
@@ -1401,6 +1401,7 @@ struct RSmem {
   uint32_t born[VG / 32], killed[VG / 32];
   uint32_t incl[VWORDS];
   uint16_t list[RLIST];
+  uint16_t bri[VG];  // per group: its birth record (from the read's rk0), set with its born bit
   RSlot slot[IWB];
 };
 struct RPre {  // a read's prefetched inputs: one bitmap word and two record chunks per lane
@@ -1418,6 +1419,7 @@ __global__ void __launch_bounds__(BLOCK, 5) k_grp_recs(am_op_log L, am_read_batc
   const uint64_t nsel = S.idx ? (uint64_t)(uniform_u32(S.range[1]) - sel0) : B.n_reads;
   const uint64_t W = (uint64_t)gridDim.x * NW;
   const uint64_t gw = (uint64_t)blockIdx.x * NW + uniform_u32(threadIdx.x >> 6);
+  const uint64_t *const pairs = L.prec ? L.prec : L.grp;
 
   // prefetch read j of the slot table: bitmap words [t0 / 32, ...) (lane i: word i, the first
   // 64), records [rk0 & ~3, + 2 RCH)
@@ -1443,7 +1445,9 @@ __global__ void __launch_bounds__(BLOCK, 5) k_grp_recs(am_op_log L, am_read_batc
       if (x == 0xFFFFFFFFu || q + k < rk0 || q + k >= rk1) continue;
       const uint32_t bit = AM_REC_OP(x) + sh;
       if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
-      atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
+      const uint32_t g = AM_REC_GRP(x);
+      atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (g >> 5), 1u << (g & 31));
+      if (!(x & AM_REC_KILL)) s.bri[g] = (uint16_t)(q + k - rk0);  // a group's one birth
     }
   };
 
@@ -1519,8 +1523,10 @@ __global__ void __launch_bounds__(BLOCK, 5) k_grp_recs(am_op_log L, am_read_batc
         for (uint32_t j0 = 0; j0 < end; j0 += 2 * WAVE) {
           const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
           u64x2 p1 = {0, 0}, p2 = {0, 0};
-          if (j1 < end) p1 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j1]));
-          if (j2 < end) p2 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j2]));
+          // a survivor's pair through its birth record (prec: births close together in op
+          // order) rather than its group slot (grp: one group run apart in output order)
+          if (j1 < end) p1 = *(const u64x2 *)(pairs + 2 * (rk0 + (L.prec ? s.bri[s.list[j1]] : s.list[j1])));
+          if (j2 < end) p2 = *(const u64x2 *)(pairs + 2 * (rk0 + (L.prec ? s.bri[s.list[j2]] : s.list[j2])));
           if (j1 < end) R.value.set_a[ooff + base + j1] = p1.x, R.value.set_b[ooff + base + j1] = p1.y;
           if (j2 < end) R.value.set_a[ooff + base + j2] = p2.x, R.value.set_b[ooff + base + j2] = p2.y;
         }

@@ -106,7 +106,7 @@ __device__ uint32_t raw_groups(BuildSmem &s, uint32_t n) {
 template <int TYPE>
 __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t off0, uint64_t off1, uint64_t r0,
                           uint32_t n, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
-                          uint32_t *ngrp) {
+                          uint32_t *ngrp, uint64_t *prec) {
   const uint32_t tid = threadIdx.x;
   // 1. the key's births / kills into LDS (record order = op order, effect order within an op)
   for (uint64_t p = off0 + tid; p < off1; p += BLOCK) {
@@ -180,13 +180,17 @@ __device__ void build_key(const am_op_log &L, BuildSmem &s, uint64_t k, uint64_t
     const bool kill = (s.info[r] & KILL31) != 0;
     const bool keep = !kill || b == 0xFFFFFFFFu || op > (s.info[b] & 0xFFFFu);
     rec_g[r0 + r] = keep ? (op | ((kill ? 1u : 0u) << 16) | (s.fin[g] << 17)) : 0xFFFFFFFFu;
+    if (prec && !kill) {  // a birth's (elem | value, token) is its group's pair
+      prec[2 * (r0 + r)] = s.val[r];
+      prec[2 * (r0 + r) + 1] = s.tok[r];
+    }
   }
   if (tid == 0) ngrp[k] = G;
   __syncthreads();
 }
 
 __global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
-                                                     uint32_t *ngrp) {
+                                                     uint32_t *ngrp, uint64_t *prec) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   BuildSmem &s = *reinterpret_cast<BuildSmem *>(smem_raw);
   for (uint64_t k = blockIdx.x; k < L.n_keys; k += gridDim.x) {
@@ -200,8 +204,8 @@ __global__ void __launch_bounds__(BLOCK) k_grp_build(am_op_log L, const uint64_t
       if (threadIdx.x == 0) ngrp[k] = AM_NGRP_NONE;
       continue;
     }
-    if (type == AM_AWSET) build_key<AM_AWSET>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp, ngrp);
-    else build_key<AM_MVREG>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp, ngrp);
+    if (type == AM_AWSET) build_key<AM_AWSET>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp, ngrp, prec);
+    else build_key<AM_MVREG>(L, s, k, off0, off1, r0, (uint32_t)n, rcnt, rec_g, grp, ngrp, prec);
   }
 }
 
@@ -225,7 +229,7 @@ int am_launch_group(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_
 }
 
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
-                          uint32_t *key_ngrp) {
+                          uint32_t *key_ngrp, uint64_t *prec) {
   if (L->n_keys == 0) return AM_OK;
   constexpr size_t smem = sizeof(BuildSmem);
   static bool attr = false;
@@ -235,7 +239,7 @@ int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt,
   }
   const uint64_t blocks = L->n_keys < (uint64_t)ctx->n_cu * 8 ? L->n_keys : (uint64_t)ctx->n_cu * 8;
   hipLaunchKernelGGL(k_grp_build, dim3((unsigned)blocks), dim3(BLOCK), smem, ctx->stream, *L, rcnt, rec_g, grp,
-                     key_ngrp);
+                     key_ngrp, prec);
   AM_HIP(hipGetLastError());
   return AM_OK;
 }

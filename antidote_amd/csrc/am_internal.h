@@ -13,7 +13,7 @@
 
 #include "../../include/antidote_mat.h"
 
-enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_SCR_MISC = 9, AM_SCR_INCL = 10, AM_N_SCR = 11 };
+enum { AM_SCR_PLAN = 0, AM_SCR_BIGMETA = 1, AM_SCR_BIGREC = 2, AM_SCR_ROWS = 3, AM_SCR_GRP = 4, AM_SCR_SPARE = 5, AM_SCR_SNAP = 6, AM_SCR_GC = 7, AM_SCR_SIZES = 8, AM_SCR_MISC = 9, AM_SCR_INCL = 10, AM_SCR_LGATHER = 11, AM_N_SCR = 12 };
 
 struct am_ctx {
   int device = 0;
@@ -169,7 +169,7 @@ int am_launch_bcwave(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am
                      am_retry next);
 // the token-group view of a store (per-op record offsets rcnt [n_ops+1], rec_key_off set in L)
 int am_launch_group_build(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
-                          uint32_t *key_ngrp);
+                          uint32_t *key_ngrp, uint64_t *prec);
 // the chunked token-group view of the hot MV keys (am_grpbig.hip), after am_launch_group_build
 int am_launch_group_build_big(am_ctx *ctx, const am_op_log *L, const uint64_t *rcnt, uint32_t *rec_g, uint64_t *grp,
                               uint32_t *key_ngrp);

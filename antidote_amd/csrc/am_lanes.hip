@@ -611,6 +611,8 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
   QOwn own = q_publish<DMAX>(L, R, u, nd, q_meta(L, R, q_pre<SEL>(B, S, sel0, nsel, first + lane)),
                              first + lane < nsel, accept, next, slot, lane, any);
   wave_sync();
+  PH_DECL();
+  PH_BEGIN();
   for (uint64_t b0 = first; b0 < nsel; b0 += step) {
     QMeta m;
     if (!any) {
@@ -618,6 +620,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
       pn = q_pre<SEL>(B, S, sel0, nsel, b0 + 2 * step + lane);
       own = q_publish<DMAX>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
       wave_sync();
+      PH(5);
       continue;
     }
     const QOwn me = own;
@@ -737,11 +740,13 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
         }
       }
     }
+    PH(0);
     // the next block's reads: statuses, hand-offs, positions (its metadata has arrived by now;
     // the slots are free once scanned)
     wave_sync();
     own = q_publish<DMAX>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
     wave_sync();
+    PH(1);
 
     // ---- the lane's own read: its quad's results, or (a longer read) its own scan ----
     const uint32_t tk = me.tk, t = tk & 0xFFu;
@@ -825,7 +830,9 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
       else galive = alive;
     }
     const uint64_t r = me.r, idb = me.idb;
+    PH(2);
     q_gather<DMAX>(L, R, sm, galive, rk0, ooff, me.pos, lane);
+    PH(3);
 
     if (tk_take) {
       uint64_t v0 = 0, v1 = 0;
@@ -841,7 +848,9 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
       write_lane(L, R, u, nd, n, r, idb, off0, off1, t, status, a, v0, v1, vflag, ns);
     }
     wave_sync();  // the LDS area is rewritten by the next block
+    PH(4);
   }
+  PH_END();
 }
 
 template <int D>
@@ -882,6 +891,17 @@ int launch_g(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
 }
 
 }  // namespace
+
+#ifdef AMK_PHASE_PROF
+// experiments only: read and clear the batch-clock lane kernel's phase cycle sums
+extern "C" int am_debug_lane_phase_cycles(uint64_t *out) {
+  unsigned long long h[8] = {0};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(amk_grp::amk_phase_cycles), sizeof(h)) != hipSuccess) return AM_ERR_HIP;
+  for (int i = 0; i < 8; ++i) out[i] = h[i];
+  const unsigned long long z[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(amk_grp::amk_phase_cycles), z, sizeof(z)) == hipSuccess ? AM_OK : AM_ERR_HIP;
+}
+#endif
 
 uint32_t am_lane_accept(const am_op_log *L, const am_read_result *R, uint32_t types) {
   if (!am_log_packed(L)) return 0;

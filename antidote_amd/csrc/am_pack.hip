@@ -222,7 +222,7 @@ int build_records(am_store *st) {
     return AM_ERR_HIP;
   }
   rc = AM_OK;
-  void *rko = nullptr, *rke = nullptr, *rg = nullptr, *gp = nullptr, *ng = nullptr;
+  void *rko = nullptr, *rke = nullptr, *rg = nullptr, *gp = nullptr, *ng = nullptr, *pr = nullptr;
   rc = am_dev_alloc(c, (d.n_keys + 1) * 8, &rko);
   if (!rc) st->allocs.push_back(rko);
   if (!rc && d.key_end) {
@@ -232,14 +232,15 @@ int build_records(am_store *st) {
   if (!rc) rc = am_dev_alloc(c, (n_rec + 4) * 4, &rg);
   if (!rc) st->allocs.push_back(rg), rc = am_dev_alloc(c, (n_rec + 4) * 16, &gp);
   if (!rc) st->allocs.push_back(gp), rc = am_dev_alloc(c, (d.n_keys + 1) * 4, &ng);
-  if (!rc) st->allocs.push_back(ng);
+  if (!rc) st->allocs.push_back(ng), rc = am_dev_alloc(c, (n_rec + 4) * 16, &pr);
+  if (!rc) st->allocs.push_back(pr);
   if (!rc) {
     hipLaunchKernelGGL(k_rec_key_off, dim3(grid_of(d.n_keys + 1)), dim3(256), 0, c->stream, d.key_off, d.key_end,
                        d.n_keys, cnt, (uint64_t *)rko, (uint64_t *)rke);
     am_op_log v = d;
     v.rec_key_off = (const uint64_t *)rko;
     v.rec_key_end = (const uint64_t *)rke;
-    rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng);
+    rc = am_launch_group_build(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng, (uint64_t *)pr);
     if (!rc) rc = am_launch_group_build_big(c, &v, cnt, (uint32_t *)rg, (uint64_t *)gp, (uint32_t *)ng);
     if (!rc && (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)) {
       am_set_error("token-group view: build pass failed");
@@ -271,6 +272,7 @@ int build_records(am_store *st) {
   d.rec_g = (const uint32_t *)rg;
   d.grp = (const uint64_t *)gp;
   d.key_ngrp = (const uint32_t *)ng;
+  d.prec = (const uint64_t *)pr;
   d.gmask = (const uint64_t *)gmk;
   return AM_OK;
 }

@@ -44,9 +44,7 @@ __device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read
     if (write_status) R.status[r] = AM_ERR_INVALID;
     return CLS_DONE;
   }
-  // (mvbig comes from a per-log cache that may be stale: the log itself must have the view)
-  if (mvbig && t == AM_MVREG && L.key_type[key] == AM_MVREG && L.key_ngrp && L.rec_g && am_ngrp_big(L.key_ngrp[key]))
-    return CLS_MVBIG;
+  if (mvbig && t == AM_MVREG && L.key_type[key] == AM_MVREG && am_ngrp_big(L.key_ngrp[key])) return CLS_MVBIG;
   return t;
 }
 
@@ -388,7 +386,8 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   // beside the lane tier: the bounded-counter chain, and the MV reads of keys in the chunked
   // big view (straight to the big-read tier; the later planner leaves them out)
   const bool bc_early = lanes && ((types >> AM_BCOUNTER) & 1u);
-  const bool mv_early = lanes && (types & TYPES_MVBIG);
+  // (the type mask is a per-log cache that may be stale: the log itself must hold the view)
+  const bool mv_early = lanes && (types & TYPES_MVBIG) && L->key_ngrp && L->rec_g;
   uint32_t *erange = nullptr, *eidx = nullptr;
   if (lanes) {
     void *lscr = nullptr;

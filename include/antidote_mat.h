@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 9
+#define AM_ABI_VERSION 10
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -234,6 +234,13 @@ typedef struct am_op_log {
    * ceil(G/32) killed words over the key's G groups -- the OR of its ops' token-group records,
    * so a read including the whole block sets those bits without streaming its records. */
   const uint32_t *zone_gsum;
+  /* Birth-ordered pairs (device stores with the token-group view, or NULL): for a birth
+   * record rec_g[i] of a grouped key, prec[2 i + {0, 1}] = its group's pair (grp above); other
+   * slots unspecified.  Records are in op order, so the groups that survive a read -- in an
+   * add-wins set the newest add of each element, in an MV register the newest assigns --
+   * have their births close together here, while in grp (output order) they lie a group run
+   * apart: the record pass gathers a survivor's pair through its birth record. */
+  const uint64_t *prec;        /* [n_rec][2] or NULL                                 */
 } am_op_log;
 #define AM_ZONE_OPS 256u
 #define AM_GMASK_MAX_GRP 32u
