@@ -92,6 +92,7 @@ class am_synth_params(ctypes.Structure):
         ("seed", c_uint64), ("n_keys", c_uint64), ("ops_per_key", c_uint32), ("n_dc", c_uint32),
         ("type", c_uint32), ("key_base", c_uint32), ("max_lag", c_uint32), ("zipf_milli", c_uint32),
         ("total_ops", c_uint64), ("hot_cap", c_uint32), ("universe", c_uint32), ("part_mask", c_uint64),
+        ("esc_ppm", c_uint32), ("_pad2", c_uint32),
     ]
 
 

@@ -25,8 +25,7 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int NW = BLOCK / WAVE;
 constexpr int OPL = 4;
-constexpr uint64_t BCW_OPS = 4096;  // longer logs: the chunked big-read tier (a wave streaming 32768 ops
-                                      // alone was the tail of C5 at the 32768 limit)
+constexpr uint64_t BCW_OPS = AM_BCWAVE_OPS;  // longer logs: the chunked big-read tier
 
 template <int DMAX>
 struct BcSmem {

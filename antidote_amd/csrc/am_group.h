@@ -567,10 +567,12 @@ struct WSlot {
 // base-snapshot reads (cached AW / MV bases): at most KB base pairs and KB new survivors,
 // merged in LDS (the survivor list area; see k_grp_wave step 4b)
 constexpr uint32_t KB = 120;
+constexpr uint32_t VGB = VG / 2;  // groups of a read whose survivors come through their births
 struct WaveSmem {
   uint32_t born[VG / 32], killed[VG / 32];
   uint32_t incl[VWORDS];
   uint16_t list[VG];  // surviving groups in order
+  uint16_t bri[VGB];  // per group (G <= VGB, every record streamed): its birth record from rk0
   WSlot slot[WB];
 };
 // ops per lane of a wave-kernel tile: the packed view's u32 entries fill 32-64 VGPRs; the
@@ -688,7 +690,7 @@ __device__ __forceinline__ uint32_t hinted_group(const am_op_log &L, uint64_t rk
 template <int TYPE>
 __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_result &R, GrpHint H, WaveSmem &s,
                            uint64_t rk0, uint32_t G, uint32_t nb, uint64_t boff, uint64_t ooff, uint32_t ocap,
-                           uint32_t lane, uint32_t &nout, int32_t &status) {
+                           uint32_t lane, uint32_t &nout, int32_t &status, bool by_birth) {
   const uint32_t nwd = (G + 31) / 32;
   const uint32_t aw = lane < nwd ? (s.born[lane] & ~s.killed[lane]) : 0u;
   const uint32_t c = (uint32_t)__popc(aw);
@@ -711,7 +713,8 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
   for (int h = 0; h < 2; ++h) {
     const uint32_t i = lane + 64u * h;
     if (i < ns) {
-      np[h] = *(const u64x2 *)(L.grp + 2 * (rk0 + list[i]));
+      np[h] = by_birth ? *(const u64x2 *)(L.prec + 2 * (rk0 + s.bri[list[i]]))  // through its birth record
+                 : *(const u64x2 *)(L.grp + 2 * (rk0 + list[i]));
       nka[i] = np[h].x, nkb[i] = np[h].y;
     }
   }
@@ -972,6 +975,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           zrows = 0;
         }
       }
+      // survivors' pairs through their birth records (prec, births in op order: the survivors'
+      // lie close together) when every record is streamed and the groups fit bri
+      const bool by_birth = L.prec != nullptr && G <= VGB && !(qe > qs);
       if (qe > qs) {  // records not streamed; a leading range moves the stream's start
         n_rskip += qe - qs;
         if (qs <= rk0) qa = qe & ~3ull, qs = ~0ull;
@@ -1057,6 +1063,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
             const uint32_t op = AM_REC_OP(x), bit = op + sh;
             if (!((s.incl[bit >> 5] >> (bit & 31)) & 1u)) continue;
             atomicOr(((x & AM_REC_KILL) ? s.killed : s.born) + (AM_REC_GRP(x) >> 5), 1u << (AM_REC_GRP(x) & 31));
+            if (by_birth && !(x & AM_REC_KILL)) s.bri[AM_REC_GRP(x)] = (uint16_t)(q + k - rk0);  // a group's one birth
           }
         }
         if (q1 >= rk1) break;
@@ -1094,7 +1101,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         //     included candidate with the new survivors (base_merge); a read that outgrows the
         //     LDS lists goes to the next tier untouched
         if (!base_merge<TYPE>(L, B, R, H, s, rk0, G, nb, uniform_u64(s.slot[j].boff), uniform_u64(s.slot[j].ooff),
-                              uniform_u32(s.slot[j].ocap), lane, ns, status)) {
+                              uniform_u32(s.slot[j].ocap), lane, ns, status, by_birth)) {
           if (lane == 0) next.list[atomicAdd(next.count, 1u)] = (uint32_t)r;
           wave_sync();
           continue;
@@ -1114,8 +1121,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         for (uint32_t j0 = 0; j0 < nput; j0 += 2 * WAVE) {
           const uint32_t j1 = j0 + lane, j2 = j1 + WAVE;
           u64x2 p1 = {0, 0}, p2 = {0, 0};
-          if (j1 < nput) p1 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j1]));
-          if (j2 < nput) p2 = *(const u64x2 *)(L.grp + 2 * (rk0 + s.list[j2]));
+          const uint64_t *src = by_birth ? L.prec : L.grp;
+          if (j1 < nput) p1 = *(const u64x2 *)(src + 2 * (rk0 + (by_birth ? s.bri[s.list[j1]] : s.list[j1])));
+          if (j2 < nput) p2 = *(const u64x2 *)(src + 2 * (rk0 + (by_birth ? s.bri[s.list[j2]] : s.list[j2])));
           if (j1 < nput) R.value.set_a[ooff + j1] = p1.x, R.value.set_b[ooff + j1] = p1.y;
           if (j2 < nput) R.value.set_a[ooff + j2] = p2.x, R.value.set_b[ooff + j2] = p2.y;
           if (j1 < nput) H.put(ooff + j1, p1.x, p1.y, s.list[j1]);

@@ -97,6 +97,10 @@ int check_params(const am_synth_params *p) {
     am_set_error("synth: unknown type %u", p->type);
     return AM_ERR_INVALID;
   }
+  if (p->esc_ppm > 1000000u) {
+    am_set_error("synth: esc_ppm %u above 10^6", p->esc_ppm);
+    return AM_ERR_INVALID;
+  }
   return AM_OK;
 }
 
@@ -136,7 +140,7 @@ __global__ void k_gen_ops(am_synth_params p, const uint64_t *key_off, uint64_t s
       ct[q] = o.ct;
       p0[q] = o.p0;
       if (p1) p1[q] = o.p1;
-      for (uint32_t d = 0; d < p.n_dc; ++d) snap[(uint64_t)d * stride + q] = am_syn_snap(p.seed, key, i, d, p.max_lag);
+      for (uint32_t d = 0; d < p.n_dc; ++d) snap[(uint64_t)d * stride + q] = am_syn_snap_e(p.seed, key, i, d, p.max_lag, p.n_dc, p.esc_ppm);
       if (vlen) vlen[q] = var_words(p, key, i, kt);
     }
   }
@@ -329,7 +333,7 @@ int am_synth_host(const am_synth_params *p, uint64_t k0, uint64_t nk, am_op_log 
       ct[q] = op.ct;
       p0[q] = op.p0;
       if (p1) p1[q] = op.p1;
-      for (uint32_t d = 0; d < p->n_dc; ++d) snap[(uint64_t)d * stride + q] = am_syn_snap(p->seed, key, i, d, p->max_lag);
+      for (uint32_t d = 0; d < p->n_dc; ++d) snap[(uint64_t)d * stride + q] = am_syn_snap_e(p->seed, key, i, d, p->max_lag, p->n_dc, p->esc_ppm);
       if (var_off) {
         var_off[q] = w;
         if (var_data) var_write(*p, key, i, kt, var_data + w);

@@ -13,6 +13,7 @@
 //   snap_vc(i)[d] = g(i - lag_d), lag_d = 1 + h(k,i,2+d) mod max_lag   (causally earlier;
 //                   snap_vc[commit_dc] < commit_time as ClockSI guarantees)
 //   read clock(q) = BASE + floor(q * N) * STEP + d * STEP/2   per DC d
+//   (esc_ppm > 0: a fraction of ops carry one remote DC's entry 2^33 us behind, am_syn_snap_e)
 // Payloads:
 //   PN   delta uniform in [-1000, 1000]
 //   LWW  ts = BASE + perm_k(i) * STEP + jitter  (perm_k a bijection of [0, 2^ceil(log2 N)),
@@ -53,6 +54,22 @@ AM_HD uint32_t am_syn_dc(uint64_t seed, uint64_t key, uint64_t i, uint32_t n_dc)
 AM_HD uint64_t am_syn_snap(uint64_t seed, uint64_t key, uint64_t i, uint32_t d, uint32_t max_lag) {
   uint64_t lag = 1 + am_syn_h(seed, key, i, 2 + d) % (max_lag ? max_lag : 1);
   return am_syn_g(seed, key, (int64_t)i - (int64_t)lag);
+}
+
+// A lagging DC (the packed view's escape path): with probability esc_ppm / 10^6 an op's
+// snapshot entry of one remote DC -- never its commit DC, whose entry the commit time replaces
+// in the inclusion test -- lags by AM_SYN_ESC_LAG us (2.4 h), outside the 2^32-us window of the
+// packed view around the key's time base.  snapshot_time is a full vectorclock
+// (include/antidote.hrl:197-204); a partitioned DC's entry stays where the partition left it
+// (src/inter_dc_dep_vnode.erl:206-232), so such entries are real, and the view escapes the op.
+#define AM_SYN_ESC_LAG (1ull << 33)
+AM_HD uint64_t am_syn_snap_e(uint64_t seed, uint64_t key, uint64_t i, uint32_t d, uint32_t max_lag, uint32_t n_dc,
+                             uint32_t esc_ppm) {
+  const uint64_t s = am_syn_snap(seed, key, i, d, max_lag);
+  if (!esc_ppm || n_dc < 2 || am_syn_h(seed, key, i, 60) % 1000000u >= esc_ppm) return s;
+  const uint32_t cdc = (uint32_t)(am_syn_h(seed, key, i, 1) % n_dc);  // am_syn_dc
+  const uint32_t ed = (cdc + 1u + (uint32_t)(am_syn_h(seed, key, i, 61) % (n_dc - 1))) % n_dc;
+  return d == ed ? s - AM_SYN_ESC_LAG : s;
 }
 
 AM_HD uint64_t am_syn_read_clock(uint64_t n_ops_per_key, double q, uint32_t d) {

@@ -13,11 +13,12 @@ SEED = 0x5EED
 
 
 def params(n_keys, n_dc, type_, ops_per_key=0, seed=SEED + 2, key_base=0, max_lag=8, zipf=0.0, total_ops=0,
-           hot_cap=0, universe=64) -> abi.am_synth_params:
+           hot_cap=0, universe=64, esc_ppm=0) -> abi.am_synth_params:
     p = abi.am_synth_params()
     p.seed, p.n_keys, p.ops_per_key, p.n_dc, p.type = seed, n_keys, ops_per_key, n_dc, type_
     p.key_base, p.max_lag, p.zipf_milli = key_base, max_lag, int(round(zipf * 1000))
     p.total_ops, p.hot_cap, p.universe = total_ops, hot_cap, universe
+    p.esc_ppm = esc_ppm  # ops with one remote DC's entry outside the packed view (synth.h am_syn_snap_e)
     return p
 
 

@@ -118,7 +118,8 @@ def synth_params(cfg, rank=0, world=1):
     (= key mod 64, src/log_utilities.erl:60-79) this rank owns -- local key k is the k-th
     of them (am_synth_params.part_mask).  Per-GPU work is fixed (weak scaling)."""
     p = synth.params(cfg["n_keys"], cfg["n_dc"], cfg["type"], ops_per_key=cfg.get("ops", 0),
-                     zipf=cfg.get("zipf", 0.0), total_ops=cfg.get("total_ops", 0), hot_cap=cfg.get("hot_cap", 0))
+                     zipf=cfg.get("zipf", 0.0), total_ops=cfg.get("total_ops", 0), hot_cap=cfg.get("hot_cap", 0),
+                     esc_ppm=int(round(cfg.get("escape", 0.0) * 1e6)))
     p.part_mask = owned_partitions_mask(rank, world)
     return p
 
@@ -539,6 +540,9 @@ def main():
     ap.add_argument("--index", default="none", choices=["none", "zones", "exact", "summaries"],
                     help="zone index of the headline store (am_store_index); the headline streams every op "
                          "(none) unless asked otherwise")
+    ap.add_argument("--escape", type=float, default=0.0,
+                    help="fraction of ops whose snapshot_time holds one remote DC's entry 2^33 us behind (a "
+                         "partitioned DC): outside the packed view's window, read from the full columns")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary lines (c3: cached c3, the indexed reads, c4, c5 and c2; single GPU "
                          "only)")
@@ -556,7 +560,10 @@ def main():
         pg = dist
     torch.cuda.set_device(local_rank)
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.escape:
+        cfg["escape"] = args.escape
+        cfg["desc"] += f", {args.escape:.0%} of ops with a lagging-DC entry (escaped from the packed view)"
     mat = Materializer(local_rank)
 
     # ---- RCCL communicator for the GST all-reduce (the only data-path collective) ----

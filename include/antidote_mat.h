@@ -664,6 +664,9 @@ typedef struct am_synth_params {
                             riak_core partitions (of 64) this GPU owns: local key
                             k is the k-th integer key >= key_base whose partition
                             am_key_partition(key, 64) = key mod 64 is in the mask */
+  uint32_t esc_ppm;      /* ops (per 10^6) whose snapshot_time holds one remote DC's entry
+                            2^33 us behind: outside the packed view's window (escaped ops) */
+  uint32_t _pad2;
 } am_synth_params;
 #define AM_SYNTH_MV_BC 6
 /* Device log owned by the returned store. */

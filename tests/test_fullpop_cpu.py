@@ -26,9 +26,10 @@ def _as_dev(ref, kt, nk):
     return dev
 
 
-@pytest.mark.parametrize("cfg_name", ["c2", "c3", "c4", "c5"])
-def test_oracle_chunk_matches_hostbatch(cfg_name):
+@pytest.mark.parametrize("cfg_name,esc", [("c2", 0), ("c3", 0), ("c4", 0), ("c5", 0), ("c4", 100000)])
+def test_oracle_chunk_matches_hostbatch(cfg_name, esc):
     cfg, p = _small(cfg_name, 96 if cfg_name != "c3" else 24)
+    p.esc_ppm = esc
     clock = synth.read_clock(p, bench.Q)
     cap = max(cfg["set_cap"], 1)
     k0, nk = 5, 17
@@ -85,3 +86,22 @@ def test_chunks_cover_every_key_once():
         assert nk >= 1 and (nk == 1 or lens[k0:k0 + nk].sum() <= 1 << 16) and nk <= 64
         seen[k0:k0 + nk] += 1
     assert (seen == 1).all()
+
+
+def test_escape_knob_rate_and_shape():
+    """bench.py --escape: about esc_ppm / 10^6 of the ops carry exactly one entry 2^33 us below
+    the op's own timeline, never at the commit DC; esc_ppm = 0 leaves the log unchanged."""
+    cfg, p = _small("c4", 4000)
+    base = synth.host_log(p, 0, 4000)
+    p.esc_ppm = 100000
+    log = synth.host_log(p, 0, 4000)
+    assert (log.commit_time == base.commit_time).all() and (log.p0 == base.p0).all()
+    low = log.snap_vc < base.snap_vc  # [n_dc][n_ops]
+    per_op = low.sum(axis=0)
+    assert set(np.unique(per_op).tolist()) <= {0, 1}
+    rate = per_op.mean()
+    assert 0.08 < rate < 0.12, rate
+    d = np.argmax(low, axis=0)[per_op == 1]
+    cdc = (log.op_meta[:log.n_ops][per_op == 1] & 0x1F)
+    assert (d != cdc).all()
+    assert (base.snap_vc[low] - log.snap_vc[low] == 1 << 33).all()

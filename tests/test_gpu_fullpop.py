@@ -40,9 +40,13 @@ def _device_read(mat, dlog, p, kt, cfg, clock):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cfg_name", ["c2", "c3", "c4", "c5"])
-def test_fullpop_config(mat, cfg_name):
-    cfg = bench.CONFIGS[cfg_name]
+@pytest.mark.parametrize("cfg_name,escape", [("c2", 0.0), ("c3", 0.0), ("c4", 0.0), ("c5", 0.0), ("c2", 0.1),
+                                             ("c3", 0.1), ("c4", 0.1), ("c5", 0.1)],
+                         ids=["c2", "c3", "c4", "c5", "c2-esc10", "c3-esc10", "c4-esc10", "c5-esc10"])
+def test_fullpop_config(mat, cfg_name, escape):
+    """escape: the fraction of ops with one remote DC's snapshot entry 2^33 us behind (bench.py
+    --escape), which the packed view escapes: their inclusion comes from the full columns."""
+    cfg = dict(bench.CONFIGS[cfg_name], escape=escape)
     p = bench.synth_params(cfg)
     st = mat.synth_store(p)
     try:
@@ -57,9 +61,9 @@ def test_fullpop_config(mat, cfg_name):
         n, ops, bad = fullpop.full_parity(p, clock, cap, dev, lens)
         assert n == p.n_keys and ops == int(ko[-1])
         assert len(bad) == 0, (cfg_name, len(bad), bad[:16].tolist())
-        print(f"{cfg_name}: {n} reads / {ops} ops bit-exact")
+        print(f"{cfg_name} escape {escape}: {n} reads / {ops} ops bit-exact")
 
-        if cfg_name == "c4":
+        if cfg_name == "c4" and not escape:
             # a planted one-op change: the oldest op of a PN key leaves the snapshot (its DC-0
             # packed entry above every threshold); the comparator must flag that key alone
             k = int(np.nonzero((kt == abi.AM_PN) & (dev["count"] > 0) & (lens > 0))[0][1000])
