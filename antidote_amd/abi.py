@@ -58,7 +58,8 @@ class am_op_log(ctypes.Structure):
         ("key_tbase", c_void_p), ("pk_vc", c_void_p),
         ("n_rec", c_uint64), ("rec_key_off", c_void_p), ("rec_g", c_void_p), ("grp", c_void_p),
         ("key_ngrp", c_void_p), ("key_end", c_void_p), ("rec_key_end", c_void_p), ("gmask", c_void_p),
-        ("zone_vc", c_void_p), ("zone_gsum", c_void_p), ("prec", c_void_p),
+        ("zone_vc", c_void_p), ("zone_gsum", c_void_p), ("prec", c_void_p), ("esc_rows", c_void_p),
+        ("lag_ct", c_void_p), ("lag", c_void_p), ("key_lag", c_void_p),
     ]
 
 
@@ -220,7 +221,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.am_abi_version() != 10:
+        if L.am_abi_version() != 12:
             raise AmError("ABI version mismatch")
         _lib = L
     return _lib

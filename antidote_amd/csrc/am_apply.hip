@@ -175,9 +175,18 @@ __global__ void __launch_bounds__(256) k_writeback(am_op_log L, am_op_log S, con
       if (L.op_id) const_cast<uint64_t *>(L.op_id)[q] = S.op_id ? S.op_id[p] : idb + j;
       p0[q] = S.p0[p];
       p1[q] = S.p1 ? S.p1[p] : 0;
-      if (L.pk_vc && S.pk_vc)
+      if (L.pk_vc && S.pk_vc) {
         for (uint32_t d = 0; d < L.n_dc; ++d)
           const_cast<uint32_t *>(L.pk_vc)[(uint64_t)d * ls + q] = S.pk_vc[(uint64_t)d * ss + p];
+        // an escaped op written here reads the columns (its row index is S's, not the store's)
+        if (L.n_dc >= 2 && S.pk_vc[p] == AM_PK_ESC) const_cast<uint32_t *>(L.pk_vc)[ls + q] = 0;
+      }
+      if (L.lag_ct) {  // the lag view under the key's new lag bases (S's; escaped without them)
+        const bool lv = S.lag_ct && S.lag && S.key_lag;
+        const_cast<uint32_t *>(L.lag_ct)[q] = lv ? S.lag_ct[p] : AM_PK_ESC;
+        for (uint32_t d = 0; d < L.n_dc; ++d)
+          const_cast<uint16_t *>(L.lag)[(uint64_t)d * ls + q] = lv ? S.lag[(uint64_t)d * ss + p] : 0;
+      }
       if (L.var_off) const_cast<uint64_t *>(L.var_off)[q] = vb + (S.var_off ? S.var_off[p] - sv0 : 0);
       if (L.gmask) const_cast<uint64_t *>(L.gmask)[q] = S.gmask ? S.gmask[p] : 0;
       const uint64_t zq = q / AM_ZONE_OPS;
@@ -193,6 +202,9 @@ __global__ void __launch_bounds__(256) k_writeback(am_op_log L, am_op_log S, con
       }
     }
     for (uint64_t q = d0 + n + lane; L.gmask && q < cap_end; q += WAVE_SZ) const_cast<uint64_t *>(L.gmask)[q] = 0;
+    if (L.key_lag)
+      for (uint32_t d = lane; d < L.n_dc; d += WAVE_SZ)
+        const_cast<int32_t *>(L.key_lag)[k * L.n_dc + d] = (S.key_lag && S.lag_ct) ? S.key_lag[i * S.n_dc + d] : 0;
     if (L.zone_vc)  // the blocks inside the key: maxima, marks and summaries recomputed
       zone_rewrite(L, S, i, d0, n, cap_end, L.rec_key_off ? L.rec_key_off[k] : 0, zlevel, lane,
                    zbits[threadIdx.x / WAVE_SZ]);
@@ -363,6 +375,7 @@ int am_store_apply_ex(am_ctx *c, am_store *st, uint64_t m, const uint64_t *d_key
   view.key_off = V.off, view.key_end = V.end, view.key_id_base = V.idb, view.key_type = V.type, view.key_flags = V.flags;
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
   view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr, view.prec = nullptr;
+  view.esc_rows = nullptr, view.lag_ct = nullptr, view.lag = nullptr, view.key_lag = nullptr;
   am_store *sub = nullptr;
   int rc = am_store_update_ex(c, view, V.ctr, dev_new, mask, mask ? tvc : nullptr, mask ? tpres : nullptr, d_gc_flags,
                               false, nullptr, &sub);
@@ -504,6 +517,7 @@ int am_store_grow_keys(am_ctx *c, const am_store *st, uint64_t n_new, const uint
   view.key_type = (uint8_t *)(b + o_type), view.key_flags = (uint8_t *)(b + o_flags);
   view.key_tbase = nullptr, view.rec_key_off = nullptr, view.rec_key_end = nullptr, view.key_ngrp = nullptr;
   view.gmask = nullptr, view.zone_vc = nullptr, view.zone_gsum = nullptr, view.prec = nullptr;
+  view.esc_rows = nullptr, view.lag_ct = nullptr, view.lag = nullptr, view.key_lag = nullptr;
   hipLaunchKernelGGL(k_grow_view, dim3(grid_threads(n_new + 1)), dim3(256), 0, c->stream, L,
                      (const uint64_t *)st->counter, n_new, (uint64_t *)view.key_off, (uint64_t *)view.key_end,
                      (uint64_t *)view.key_id_base, (uint64_t *)(b + o_ctr), (uint8_t *)view.key_type,

@@ -222,9 +222,10 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
         for (uint32_t tb = shfl_u32(esc, row * RG + owner); tb; tb &= tb - 1) {
           const uint32_t t = (uint32_t)__builtin_ctz(tb), q = RG * t + owner;
           const uint64_t p = in.off0 + q;
-          const uint32_t meta = L.op_meta[p], dc = meta & 31u;
+          const uint64_t *w = esc_row(L, stride, p);  // its escape row, or the columns
+          const uint32_t meta = w ? (uint32_t)w[1] : L.op_meta[p], dc = meta & 31u;
           uint64_t xd = 0, sd = 0;
-          if (sl < nd) xd = sl == dc ? L.commit_time[p] : L.snap_vc[(uint64_t)sl * stride + p];
+          if (sl < nd) xd = sl == dc ? (w ? w[0] : L.commit_time[p]) : (w ? w[2 + sl] : L.snap_vc[(uint64_t)sl * stride + p]);
 #pragma unroll
           for (int d = 0; d < DMAX; ++d)
             if ((uint32_t)d == sl) sd = u.S[d];

@@ -184,11 +184,10 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
       if (__ballot(esc)) {  // rare: ops outside the packed view, from the full columns
         for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
           if (L.pk_vc[p] != AM_PK_ESC) continue;
-          uint64_t sv[DMAX];
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-          const uint32_t meta = L.op_meta[p];
-          if (eval_op<DMAX, false>(u, meta, L.commit_time[p], sv, u.allmask, false, p, a))
+          uint64_t sv[DMAX], ct;
+          uint32_t meta;
+          esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
+          if (eval_op<DMAX, false>(u, meta, ct, sv, u.allmask, false, p, a))
             apply(meta, (int64_t)L.p0[p], L.p1[p]);
         }
       }
@@ -202,8 +201,9 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
         for (int d = 0; d < DMAX; ++d) vS = (uint32_t)d == lane ? u.S[d] : vS;
         for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
           if (L.pk_vc[p] != AM_PK_ESC) continue;
-          const uint32_t meta = L.op_meta[p], dc = meta & 31u;
-          const uint64_t ct = L.commit_time[p];
+          const uint64_t *w = esc_row(L, stride, p);  // its escape row, or the columns
+          const uint32_t meta = w ? (uint32_t)w[1] : L.op_meta[p], dc = meta & 31u;
+          const uint64_t ct = w ? w[0] : L.commit_time[p];
           bool incl = true;
           for (uint32_t d = 0; d < nd; ++d) {
             if (!((u.spres >> d) & 1u)) {  // logger:error("Could not find DC in SS"); excluded
@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
               a.flags |= AM_FLAG_MISSING_DC_LOGGED;
               continue;
             }
-            const uint64_t x = d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p];
+            const uint64_t x = d == dc ? ct : (w ? w[2 + d] : L.snap_vc[(uint64_t)d * stride + p]);
             incl &= x <= lane_u64(vS, d);
           }
           if (!incl) {
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
             continue;
           }
           for (uint32_t d = 0; d < nd; ++d) {
-            const uint64_t x = d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p];
+            const uint64_t x = d == dc ? ct : (w ? w[2 + d] : L.snap_vc[(uint64_t)d * stride + p]);
             atomicMax((unsigned long long *)&s.emx[d], (unsigned long long)x);
           }
           a.pres |= u.allmask;

@@ -543,8 +543,9 @@ __device__ __forceinline__ uint32_t lean_incl4(const am_op_log &L, uint32_t nd, 
   for (int k = 0; k < 4; ++k) {  // rare
     const uint64_t p = g + k;
     if (p < lo || p >= hi || L.pk_vc[p] != AM_PK_ESC) continue;
-    const uint32_t meta = L.op_meta[p], dc = meta & 31u;
-    const uint64_t ct = L.commit_time[p];
+    const uint64_t *w = esc_row(L, stride, p);  // its escape row, or the columns
+    const uint32_t meta = w ? (uint32_t)w[1] : L.op_meta[p], dc = meta & 31u;
+    const uint64_t ct = w ? w[0] : L.commit_time[p];
     bool in = true;
     for (uint32_t d = 0; d < nd; ++d) {
       if (!((u.spres >> d) & 1u)) {  // logger:error("Could not find DC in SS"); excluded
@@ -552,14 +553,14 @@ __device__ __forceinline__ uint32_t lean_incl4(const am_op_log &L, uint32_t nd, 
         a.flags |= AM_FLAG_MISSING_DC_LOGGED;
         continue;
       }
-      in &= (d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p]) <= lane_u64(vS, d);
+      in &= (d == dc ? ct : (w ? w[2 + d] : L.snap_vc[(uint64_t)d * stride + p])) <= lane_u64(vS, d);
     }
     if (!in) {
       a.min_excl = p < a.min_excl ? p : a.min_excl;
       continue;
     }
     for (uint32_t d = 0; d < nd; ++d)
-      atomicMax(&emx[d], (unsigned long long)(d == dc ? ct : L.snap_vc[(uint64_t)d * stride + p]));
+      atomicMax(&emx[d], (unsigned long long)(d == dc ? ct : (w ? w[2 + d] : L.snap_vc[(uint64_t)d * stride + p])));
     a.pres |= u.allmask;
     a.count += 1;
     if (meta & AM_META_BAD) a.flags |= FLAG_BAD;

@@ -208,16 +208,34 @@ __device__ __forceinline__ void ld_n32(const uint32_t *p, uint32_t *o) {
 // the OPL ops [g, g + OPL) of a read's [off0, off1): inclusion bits (is_op_in_snapshot/7).
 // Packed view: u32 entries relative to the key's time base (am_wave.h pk_eval), partials in
 // ap; an escaped op (pk_vc[0] == AM_PK_ESC) is not evaluated here: esc is set and the
-// caller's escape pass (esc_pass) evaluates it from the full columns, off the hot loop.
+// caller's escape pass (esc_pass) evaluates it from the full columns, off the hot loop.  With
+// the lag view (lr.on) the same from 4 + 2 D bytes per op (escapes: lag_ct == AM_PK_ESC).
 // Full view: eval_op on the u64 columns, partials in a.
 template <int DMAX, int OPL, bool GENERAL, bool PACKED>
 __device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u,
-                                              const PkRead<DMAX> &pk, uint64_t g, uint64_t off0, uint64_t off1,
-                                              uint64_t stride, AccP<DMAX> &ap, Acc<DMAX> &a, bool &esc) {
+                                              const PkRead<DMAX> &pk, const LagRead<DMAX> &lr, uint64_t g,
+                                              uint64_t off0, uint64_t off1, uint64_t stride, AccP<DMAX> &ap,
+                                              Acc<DMAX> &a, bool &esc) {
   uint32_t ib = 0;
   uint64_t tx[OPL] = {};
   if (GENERAL && u.has_txid) ld_n64<OPL>(L.op_txid + g, tx);
-  if (PACKED) {
+  if (PACKED && lr.on) {
+    uint32_t c[OPL] = {}, lw[DMAX][(OPL + 1) / 2];
+    ld_n32<OPL>(L.lag_ct + g, c);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      const uint16_t *lp = L.lag + (uint64_t)d * stride + g;
+      if constexpr (OPL == 4) {
+        const uint2 v = d < (int)nd ? *(const uint2 *)lp : uint2{0, 0};
+        lw[d][0] = v.x, lw[d][1] = v.y;
+      } else if constexpr (OPL == 2) {
+        lw[d][0] = d < (int)nd ? *(const uint32_t *)lp : 0u;
+      } else {
+        lw[d][0] = d < (int)nd ? (uint32_t)*lp : 0u;
+      }
+    }
+    ib = pk_tile_lag<DMAX, OPL, GENERAL>(u, pk, lr, c, lw, tx, g, off0, off1, ap, esc);
+  } else if (PACKED) {
     uint32_t x[OPL][DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
@@ -260,31 +278,30 @@ __device__ __forceinline__ uint32_t eval_tile(const am_op_log &L, uint32_t nd, c
 template <int DMAX, bool GENERAL>
 __device__ __forceinline__ void esc_pass(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t off0,
                                       uint64_t off1, uint64_t t0, uint64_t stride, uint32_t lane0, uint32_t nl,
-                                      uint32_t *incl, Acc<DMAX> &a) {
+                                      uint32_t *incl, Acc<DMAX> &a, const uint32_t *escv) {
   for (uint64_t p = off0 + lane0; p < off1; p += nl) {
-    if (L.pk_vc[p] != AM_PK_ESC) continue;
-    uint64_t sv[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-    const uint32_t meta = L.op_meta[p];
+    if (escv[p] != AM_PK_ESC) continue;
+    uint64_t sv[DMAX], ct;
+    uint32_t meta;
+    esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
     const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
     const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
-    if (eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], sv, sp, txm, p, a) && !(meta & AM_META_BAD))
+    if (eval_op<DMAX, GENERAL>(u, meta, ct, sv, sp, txm, p, a) && !(meta & AM_META_BAD))
       atomicOr(&incl[(uint32_t)((p - t0) >> 5)], 1u << ((p - t0) & 31));
   }
 }
 
-// the same for a fresh read whose bits live in the global bitmap gbm (bit = op slot)
+// the same for a fresh read whose bits live in the global bitmap gbm (bit = op slot); escv: the
+// view the read streamed (pk_vc, or the lag view's lag_ct), whose AM_PK_ESC marks the escapes
 template <int DMAX>
 __device__ void esc_pass_g(const am_op_log &L, uint32_t nd, const ReadU<DMAX> &u, uint64_t off0, uint64_t off1,
-                           uint64_t stride, uint32_t lane, uint32_t *gbm, Acc<DMAX> &a) {
+                           uint64_t stride, uint32_t lane, uint32_t *gbm, Acc<DMAX> &a, const uint32_t *escv) {
   for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
-    if (L.pk_vc[p] != AM_PK_ESC) continue;
-    uint64_t sv[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-    const uint32_t meta = L.op_meta[p];
-    if (eval_op<DMAX, false>(u, meta, L.commit_time[p], sv, u.allmask, false, p, a) && !(meta & AM_META_BAD))
+    if (escv[p] != AM_PK_ESC) continue;
+    uint64_t sv[DMAX], ct;
+    uint32_t meta;
+    esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
+    if (eval_op<DMAX, false>(u, meta, ct, sv, u.allmask, false, p, a) && !(meta & AM_META_BAD))
       atomicOr(&gbm[p >> 5], 1u << (p & 31));
   }
 }
@@ -429,6 +446,8 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
     // ---- 1. inclusion per op -> bitmap + scalar partials ----
     PkRead<DMAX> pk;
     if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[m.key]), pk);
+    LagRead<DMAX> lr;  // (the packed view)
+    lag_setup(L, nd, m.key, false, lr);
     AccP<DMAX> ap;
     Acc<DMAX> a;
     ap.reset();
@@ -437,7 +456,8 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
     for (uint64_t t = t0; t < m.off1; t += TILE) {
       const uint64_t g = t + (uint64_t)tid * OPL;
       const uint32_t ib =
-          g < m.off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, m.off0, m.off1, stride, ap, a, esc) : 0u;
+          g < m.off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, lr, g, m.off0, m.off1, stride, ap, a, esc)
+                     : 0u;
       // 32 / OPL lanes -> one bitmap word
       constexpr uint32_t LPW = 32 / OPL;
       uint32_t word = ib << (OPL * (lane % LPW));
@@ -447,7 +467,7 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
     }
     const bool full = !PACKED || __syncthreads_or(esc);
     if (PACKED && full)  // rare: ops outside the packed view, from the full columns
-      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, tid, WBLOCK, s.incl, a);
+      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, tid, WBLOCK, s.incl, a, L.pk_vc);
     {  // wave partials of the scalar outputs (VGPR reductions: the scalar file is full)
       uint32_t cnt, fl, pr;
       uint64_t mn, mxl;
@@ -561,7 +581,7 @@ constexpr int VRPT = 8;                    // records per lane per chunk (512 pe
 // starts with no dependent global load (key -> key_off / records / time base / output range)
 constexpr uint32_t WB = 32;
 struct WSlot {
-  uint64_t off0, rk0, ooff, K, idb, boff;
+  uint64_t off0, rk0, ooff, K, idb, boff, key;
   uint32_t r, nops, nrec, G, ocap, nb;
 };
 // base-snapshot reads (cached AW / MV bases): at most KB base pairs and KB new survivors,
@@ -830,6 +850,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
         const uint64_t o0 = R.value.set_off[mm.r], o1 = R.value.set_off[mm.r + 1];
         w.off0 = mm.off0, w.rk0 = mm.rk0, w.ooff = o0;
         w.K = PACKED ? L.key_tbase[mm.key] : 0;
+        w.key = mm.key;
         w.idb = L.key_id_base ? L.key_id_base[mm.key] : 1;
         w.r = (uint32_t)mm.r, w.nops = (uint32_t)(mm.off1 - mm.off0), w.nrec = (uint32_t)(mm.rk1 - mm.rk0);
         w.G = mm.G, w.ocap = o1 - o0 < 0xFFFFFFFFull ? (uint32_t)(o1 - o0) : 0xFFFFFFFFu;
@@ -882,6 +903,8 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
       PkRead<DMAX> pk;
       if (PACKED) pk_setup(u, nd, uniform_u64(s.slot[j].K), pk);
+      LagRead<DMAX> lr;  // the lag view: 4 + 2 D bytes per op instead of 4 D
+      lag_setup(L, nd, uniform_u64(s.slot[j].key), PACKED && L.lag_ct != nullptr, lr);
       AccP<DMAX> ap;
       Acc<DMAX> a;
       ap.reset();
@@ -1027,7 +1050,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
           }
         }
         const uint32_t ib =
-            g < off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, g, off0, off1, stride, ap, a, esc) : 0u;
+            g < off1 ? eval_tile<DMAX, OPL, GENERAL, PACKED>(L, nd, u, pk, lr, g, off0, off1, stride, ap, a, esc) : 0u;
         uint32_t word = ib << (OPL * (lane % LPW));
 #pragma unroll
         for (uint32_t x = 1; x < LPW; x <<= 1) word |= (uint32_t)__shfl_xor((int)word, (int)x);
@@ -1036,7 +1059,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       wave_sync();
       const bool full = !BM && (!PACKED || __ballot(esc));
       if (PACKED && full) {  // rare: ops outside the packed view, from the full columns
-        esc_pass<DMAX, GENERAL>(L, nd, u, off0, off1, t0, stride, lane, WAVE, s.incl, a);
+        esc_pass<DMAX, GENERAL>(L, nd, u, off0, off1, t0, stride, lane, WAVE, s.incl, a, lr.on ? L.lag_ct : L.pk_vc);
         wave_sync();
       }
 
@@ -1183,7 +1206,7 @@ __device__ __forceinline__ uint32_t wave_min_u32_v(uint32_t v) {
   return min(v, (uint32_t)__shfl_xor((int)v, 32, WAVE));
 }
 struct ISlot {
-  uint64_t off0, K, idb;
+  uint64_t off0, K, idb, key;
   uint32_t r, nops;
 };
 template <int DMAX>
@@ -1224,7 +1247,41 @@ __device__ __forceinline__ uint32_t incl_tile(const uint32_t (&x)[OPL][DMAX], co
   return ib;
 }
 
-template <int DMAX, int TYPE, bool EXACT>
+// incl_tile over the lag view: commit entries c (AM_PK_ESC: escaped), four u16 lags per DC in
+// lv, the key's lag bases lb; X[d] - K = c - (lb[d] + lag) is rebuilt where it is used (the lags
+// stay packed two per register: the rebuilt entries would hold 4 * DMAX registers)
+template <int DMAX, bool RANGE>
+__device__ __forceinline__ uint32_t incl_tile_lag(const uint32_t (&c)[4], const uint2 (&lv)[DMAX],
+                                                  const uint32_t (&lb)[DMAX], const PkRead<DMAX> &pk, uint64_t g,
+                                                  uint64_t off0, uint64_t off1, uint32_t (&mx)[DMAX], uint32_t &esc,
+                                                  uint32_t &cand) {
+  auto xd = [&](int k, int d) -> uint32_t {
+    const uint32_t w = k < 2 ? lv[d].x : lv[d].y;
+    return c[k] - (lb[d] + ((k & 1) ? w >> 16 : w & 0xFFFFu));
+  };
+  uint32_t ib = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool e = c[k] == AM_PK_ESC;
+    const bool inr = !RANGE || (g + k >= off0 && g + k < off1);
+    bool in = inr && !e;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) in = in && xd(k, d) <= pk.thr[d];
+    esc |= (uint32_t)(inr && e) << k;
+    cand |= (uint32_t)(inr && !e) << k;
+    if (in) {
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) mx[d] = max(mx[d], xd(k, d));
+    }
+    ib |= (uint32_t)in << k;
+  }
+  return ib;
+}
+
+// LAG: the read streams the lag view (am_op_log.lag_ct / lag / key_lag, 4 + 2 D bytes per op)
+// and rebuilds each packed entry X[d] - K = lag_ct - key_lag[d] - lag[d] in u32 (exact: the entry
+// fits u32 for every op the view holds); else the packed view (4 D bytes per op)
+template <int DMAX, int TYPE, bool EXACT, bool LAG>
 __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                        am_retry next, uint32_t short_opl, uint32_t *ibm) {
   constexpr int OPL = 4;
@@ -1262,6 +1319,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
         elig = true;
         ISlot &w = sl[lane];
         w.off0 = mm.off0, w.K = L.key_tbase[mm.key], w.idb = L.key_id_base ? L.key_id_base[mm.key] : 1;
+        w.key = mm.key;
         w.r = (uint32_t)mm.r, w.nops = (uint32_t)(mm.off1 - mm.off0);
       }
     }
@@ -1280,28 +1338,52 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
       const uint64_t off0 = uniform_u64(sl[j].off0), off1 = off0 + uniform_u32(sl[j].nops);
       PkRead<DMAX> pk;
       pk_setup(u, nd, uniform_u64(sl[j].K), pk);
-      uint32_t mx[DMAX];
+      uint32_t mx[DMAX], lb[DMAX];  // lb: the key's lag bases (LAG)
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) mx[d] = 0;
+      if (LAG) {
+        const uint64_t key = uniform_u64(sl[j].key);
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) lb[d] = uniform_u32(d < (int)nd ? (uint32_t)L.key_lag[key * nd + d] : 0u);
+      }
       uint32_t cnt = 0, minex = 0xFFFFFFFFu, anyc = 0, anyesc = 0;
+      uint64_t escm = 0;  // the lane's escaped ops: bit OPL * tile + k (the first 64 / OPL tiles)
       const uint64_t t0 = off0 & ~31ull;  // 32-op aligned: lane groups of LPW fill whole bitmap words
       for (uint64_t t = t0; t < off1; t += TILE) {
         const uint64_t g = t + (uint64_t)lane * OPL;
-        uint32_t x[OPL][DMAX];
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          uint32_t q[OPL] = {};
-          if (d < (int)nd && g < off1) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
-#pragma unroll
-          for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
-        }
         uint32_t esc = 0, cand = 0, ib;
-        if (t >= off0 && t + TILE <= off1) ib = incl_tile<DMAX, OPL, false>(x, pk, g, off0, off1, mx, esc, cand);
-        else ib = incl_tile<DMAX, OPL, true>(x, pk, g, off0, off1, mx, esc, cand);
+        const bool whole = t >= off0 && t + TILE <= off1;
+        if constexpr (LAG) {
+          static_assert(OPL == 4, "four u16 lags per 8-byte load");
+          uint32_t c[OPL] = {};
+          if (g < off1) ld_n32<OPL>(L.lag_ct + g, c);
+          uint2 lv[DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            lv[d] = uint2{0, 0};
+            if (d < (int)nd && g < off1) lv[d] = *(const uint2 *)(L.lag + (uint64_t)d * stride + g);
+          }
+          // (pad DCs d >= nd: c - lb[d] with lb = 0 lies under the always-passing pad threshold)
+          ib = whole ? incl_tile_lag<DMAX, false>(c, lv, lb, pk, g, off0, off1, mx, esc, cand)
+                     : incl_tile_lag<DMAX, true>(c, lv, lb, pk, g, off0, off1, mx, esc, cand);
+        } else {
+          uint32_t x[OPL][DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint32_t q[OPL] = {};
+            if (d < (int)nd && g < off1) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
+          }
+          ib = whole ? incl_tile<DMAX, OPL, false>(x, pk, g, off0, off1, mx, esc, cand)
+                     : incl_tile<DMAX, OPL, true>(x, pk, g, off0, off1, mx, esc, cand);
+        }
         if (pk.never) ib = 0;
         cnt += (uint32_t)__popc(ib);
         anyc |= cand;
         anyesc |= esc;
+        const uint64_t ti = (t - t0) / TILE;
+        if (esc) escm |= ti < 64 / OPL ? (uint64_t)esc << (OPL * ti) : ~0ull;  // ~0: walk the key
         const uint32_t ex = cand & ~ib;
         if (ex) minex = min(minex, (uint32_t)(g - t0) + (uint32_t)__builtin_ctz(ex));
         uint32_t word = ib << (OPL * (lane % LPW));
@@ -1349,7 +1431,19 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
         Acc<DMAX> a;
         a.reset();
         __builtin_amdgcn_s_waitcnt(0);
-        esc_pass_g<DMAX>(L, nd, u, off0, off1, stride, lane, ibm, a);
+        if (__ballot(escm == ~0ull)) {  // a long key's late tiles: the wave walks its escape marks
+          esc_pass_g<DMAX>(L, nd, u, off0, off1, stride, lane, ibm, a, LAG ? L.lag_ct : L.pk_vc);
+        } else {  // the lane's own escaped ops, marked by the tile loop: no second walk of the key
+          for (uint64_t m = escm; m; m &= m - 1) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            const uint64_t p = t0 + (uint64_t)(b / OPL) * TILE + (uint64_t)lane * OPL + b % OPL;
+            uint64_t sv[DMAX], ct;
+            uint32_t meta;
+            esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
+            if (eval_op<DMAX, false>(u, meta, ct, sv, u.allmask, false, p, a) && !(meta & AM_META_BAD))
+              atomicOr(&ibm[p >> 5], 1u << (p & 31));
+          }
+        }
         count += wave_sum_u32_v(a.count), flags |= wave_or_u32_v(a.flags), pres |= wave_or_u32_v(a.pres);
         min_excl = wave_min_u64_v(umin64(min_excl, a.min_excl));
 #pragma unroll
@@ -1636,13 +1730,12 @@ __global__ void __launch_bounds__(BLOCK) k_grp_row(am_op_log L, am_read_batch B,
       uint64_t incl = 0;
       // one op from the full columns (full view, or an op outside the packed view)
       auto eval_full = [&](uint64_t p) -> bool {
-        uint64_t svf[DMAX];
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) svf[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+        uint64_t svf[DMAX], ct;
+        uint32_t meta;
+        esc_load<DMAX>(L, nd, stride, p, svf, ct, meta);  // (the columns when the op has no row)
         const uint32_t sp = (GENERAL && L.snap_pres) ? L.snap_pres[p] : u.allmask;
         const bool txm = GENERAL && u.has_txid && L.op_txid[p] == u.txid;
-        const uint32_t meta = L.op_meta[p];
-        return eval_op<DMAX, GENERAL>(u, meta, L.commit_time[p], svf, sp, txm, p, a) && !(meta & AM_META_BAD);
+        return eval_op<DMAX, GENERAL>(u, meta, ct, svf, sp, txm, p, a) && !(meta & AM_META_BAD);
       };
 #pragma unroll
       for (uint32_t k = 0; k < ROW_OPS / RG; ++k) {
@@ -1724,9 +1817,12 @@ int launch_split(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_rea
   const uint64_t stride = L->snap_stride ? L->snap_stride : L->n_ops;
   void *ibm = nullptr;
   if (int rc = am_ctx_scratch(ctx, AM_SCR_INCL, (stride / 32 + 4) * 4, &ibm)) return rc;
+  // the lag view when the log has it: 4 + 2 D bytes of commit vector per op instead of 4 D
+  const bool lag = L->lag_ct && L->lag && L->key_lag;
   static int occ_i = 0, occ_w = 0;
   if (!occ_i) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_i, k_grp_incl<D, TYPE, EXACT>, BLOCK, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_i, k_grp_incl<D, TYPE, EXACT, true>, BLOCK, 0) !=
+            hipSuccess ||
         occ_i < 1)
       occ_i = 2;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, k_grp_recs<D, TYPE>, BLOCK, 0) != hipSuccess ||
@@ -1737,8 +1833,12 @@ int launch_split(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_rea
   const uint64_t bi = want_i < (uint64_t)ctx->n_cu * occ_i ? want_i : (uint64_t)ctx->n_cu * occ_i;
   const uint64_t bw = want_w < (uint64_t)ctx->n_cu * occ_w ? want_w : (uint64_t)ctx->n_cu * occ_w;
   if (bi == 0) return AM_OK;
-  hipLaunchKernelGGL((k_grp_incl<D, TYPE, EXACT>), dim3((unsigned)bi), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S,
-                     next, short_opl, (uint32_t *)ibm);
+  if (lag)
+    hipLaunchKernelGGL((k_grp_incl<D, TYPE, EXACT, true>), dim3((unsigned)bi), dim3(BLOCK), 0, ctx->stream, *L, *B, *R,
+                       S, next, short_opl, (uint32_t *)ibm);
+  else
+    hipLaunchKernelGGL((k_grp_incl<D, TYPE, EXACT, false>), dim3((unsigned)bi), dim3(BLOCK), 0, ctx->stream, *L, *B,
+                       *R, S, next, short_opl, (uint32_t *)ibm);
   hipLaunchKernelGGL((k_grp_recs<D, TYPE>), dim3((unsigned)bw), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S,
                      short_opl, (const uint32_t *)ibm);
   AM_HIP(hipGetLastError());

@@ -51,11 +51,11 @@ struct am_ctx {
   int64_t tee_shift = 0;
   uint8_t *tee_done = nullptr;
   // The mixed-batch planner's per-type streams (am_plan.hip): sub-contexts of the set types
-  // (and [3], [4]: the big-MV and big bounded-counter reads started beside the lane tier) on
-  // the same device, sharing the counters, each with its own stream, scratch slots and
-  // pinned buffer, so one type's tiers overlap another's.  ev_fork orders them after the
+  // (and [3]: the big-MV reads started beside the lane tier) on the same device, sharing the
+  // counters, each with its own stream, scratch slots and pinned buffer, so one type's tiers
+  // overlap another's.  ev_fork orders them after the
   // planner; their ev0 joins them back.
-  am_ctx *sub[5] = {};
+  am_ctx *sub[4] = {};
   bool is_sub = false;
   hipEvent_t ev_fork = nullptr;
   // the CRDT types present in a log's keys, by key_type array: {n_keys, 1 << type mask}
@@ -100,7 +100,7 @@ struct am_store {
 // summary slot (include/antidote_mat.h)
 constexpr uint32_t AM_ZONE_EXTRA_ROWS = 5;
 // bounded-counter reads of longer logs go to the chunked big-read tier (am_bcwave.hip: a wave
-// streaming 32768 ops alone was the tail of C5 at a 32768 limit; am_plan.hip plans them early)
+// streaming 32768 ops alone was the tail of C5 at a 32768 limit)
 constexpr uint64_t AM_BCWAVE_OPS = 4096;
 
 void am_set_error(const char *fmt, ...);

@@ -289,13 +289,12 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_g(am_op_log L, am_read_batch B,
     if (esc) {  // rare: ops outside the packed view, from the full columns
       for (uint64_t p = off0; p < off1; ++p) {
         if (L.pk_vc[p] != AM_PK_ESC) continue;
-        uint64_t sv[DMAX];
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-        const uint32_t meta = L.op_meta[p];
+        uint64_t sv[DMAX], ct;
+        uint32_t meta;
+        esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
         const uint32_t sp = L.snap_pres ? L.snap_pres[p] : u.allmask;
         const bool txm = u.has_txid && L.op_txid[p] == u.txid;
-        if (!eval_op<DMAX, true>(u, meta, L.commit_time[p], sv, sp, txm, p, a)) continue;
+        if (!eval_op<DMAX, true>(u, meta, ct, sv, sp, txm, p, a)) continue;
         if (scal) {
           if (t == AM_PN) pv.add(L.p0[p], 0);
           else lv.add(L.p0[p], L.p1[p]);
@@ -799,11 +798,10 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
       uint64_t ek = 0;  // included set ops among them: the records are redone with them
       for (uint64_t p = off0; p < off1; ++p) {
         if (L.pk_vc[p] != AM_PK_ESC) continue;
-        uint64_t sv[DMAX];
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
-        const uint32_t meta = L.op_meta[p];
-        if (!eval_op<DMAX, false>(u, meta, L.commit_time[p], sv, u.allmask, false, p, a)) continue;
+        uint64_t sv[DMAX], ct;
+        uint32_t meta;
+        esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
+        if (!eval_op<DMAX, false>(u, meta, ct, sv, u.allmask, false, p, a)) continue;
         if (scal) {
           if (t == AM_PN) pv.add(L.p0[p], 0);
           else lv.add(L.p0[p], L.p1[p]);

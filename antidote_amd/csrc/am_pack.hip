@@ -175,6 +175,128 @@ struct MaxOp {
 unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536); }
 
 // builds the record view of a packed store (no-op for logs without set payloads)
+// ---- escape rows (am_op_log.esc_rows): every escaped op's commit time, meta byte and
+//      snapshot entries in one row of 2 + n_dc words, its index + 1 in the op's DC-1 packed
+//      entry.  One wave per key, the key's escaped ops compacted by ballot, rows claimed with one
+//      atomic per 64 ops; rows == null counts only ----
+__global__ void k_esc_rows(am_op_log L, uint32_t *pk_vc, uint64_t *rows, unsigned long long *cnt, uint64_t cap) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t nd = L.n_dc, E = 2 + nd;
+  for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; k < L.n_keys; k += waves) {
+    const uint64_t o0 = L.key_off[k], o1 = am_kend(L, k);
+    for (uint64_t b = o0; b < o1; b += WAVE) {
+      const uint64_t p = b + lane;
+      const bool e = p < o1 && pk_vc[p] == AM_PK_ESC;
+      const uint64_t m = __ballot(e);
+      if (!m) continue;
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd(cnt, (unsigned long long)__popcll(m));
+      base = shfl_u64(base, 0);
+      if (!e || !rows) continue;
+      const uint64_t row = base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (row >= cap) continue;
+      uint64_t *w = rows + row * E;
+      w[0] = L.commit_time[p];
+      w[1] = L.op_meta[p];
+      for (uint32_t d = 0; d < nd; ++d) w[2 + d] = L.snap_vc[(uint64_t)d * stride + p];
+      pk_vc[stride + p] = (uint32_t)(row + 1);
+    }
+  }
+}
+
+int build_esc_rows(am_store *st) {
+  am_ctx *c = st->ctx;
+  am_op_log &d = st->dev;
+  d.esc_rows = nullptr;
+  if (!d.pk_vc || d.n_dc < 2 || !d.n_ops || !d.n_keys) return AM_OK;
+  void *cnt = nullptr;
+  if (int rc = am_ctx_scratch(c, AM_SCR_MISC, 256, &cnt)) return rc;
+  const uint64_t blocks = (d.n_keys + 3) / 4 < 65536 ? (d.n_keys + 3) / 4 : 65536;
+  AM_HIP(hipMemsetAsync(cnt, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_esc_rows, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, const_cast<uint32_t *>(d.pk_vc),
+                     (uint64_t *)nullptr, (unsigned long long *)cnt, (uint64_t)0);
+  AM_HIP(hipGetLastError());
+  uint64_t n_esc = 0;
+  if (int rc = am_ctx_fetch(c, cnt, 1, &n_esc)) return rc;
+  if (n_esc == 0) return AM_OK;
+  void *rows = nullptr;
+  if (int rc = am_dev_alloc(c, n_esc * (2 + d.n_dc) * 8, &rows)) return rc;
+  st->allocs.push_back(rows);
+  AM_HIP(hipMemsetAsync(cnt, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_esc_rows, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, const_cast<uint32_t *>(d.pk_vc),
+                     (uint64_t *)rows, (unsigned long long *)cnt, n_esc);
+  AM_HIP(hipGetLastError());
+  AM_HIP(hipStreamSynchronize(c->stream));
+  d.esc_rows = (const uint64_t *)rows;
+  return AM_OK;
+}
+
+// ---- the lag view (am_op_log.lag_ct / lag / key_lag) from the packed view: one wave per key.
+//      Pass 1: key_lag[k][d] = min over the key's packed ops of (ct - X[d]) = entry(dc) - entry(d);
+//      pass 2: each op's commit entry and lags, or AM_PK_ESC when a lag exceeds 16 bits ----
+constexpr uint32_t LAG_MAX_DC = 16;
+__global__ void k_lag(am_op_log L, uint32_t *lag_ct, uint16_t *lag, int32_t *key_lag) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  const uint64_t stride = L.snap_stride ? L.snap_stride : L.n_ops;
+  const uint32_t nd = L.n_dc;
+  for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; k < L.n_keys; k += waves) {
+    const uint64_t o0 = L.key_off[k], o1 = am_kend(L, k);
+    int64_t lb[LAG_MAX_DC];
+    bool fit = true;  // every lag base within int32
+    for (uint32_t d = 0; d < nd; ++d) {
+      uint64_t m = ~0ull;  // min of (ct - X[d]) + 2^32 (biased: the difference lies in (-2^32, 2^32))
+      for (uint64_t p = o0 + lane; p < o1; p += WAVE) {
+        if (L.pk_vc[p] == AM_PK_ESC) continue;
+        const uint32_t c = L.pk_vc[(uint64_t)AM_META_DC(L.op_meta[p]) * stride + p];
+        const uint64_t v = (uint64_t)c + (1ull << 32) - L.pk_vc[(uint64_t)d * stride + p];
+        m = v < m ? v : m;
+      }
+      m = wave_min_u64(m);
+      lb[d] = m == ~0ull ? 0 : (int64_t)m - (int64_t)(1ull << 32);
+      fit &= lb[d] >= INT32_MIN && lb[d] <= INT32_MAX;
+      if (lane == 0) key_lag[k * nd + d] = fit ? (int32_t)lb[d] : 0;
+    }
+    for (uint64_t p = o0 + lane; p < o1; p += WAVE) {
+      bool ok = fit && L.pk_vc[p] != AM_PK_ESC;
+      const uint32_t c = ok ? L.pk_vc[(uint64_t)AM_META_DC(L.op_meta[p]) * stride + p] : 0u;
+      for (uint32_t d = 0; d < nd; ++d) {
+        const int64_t l = ok ? (int64_t)c - (int64_t)L.pk_vc[(uint64_t)d * stride + p] - lb[d] : 0;
+        ok = ok && l >= 0 && l <= 0xFFFF;
+        lag[(uint64_t)d * stride + p] = (uint16_t)(ok ? l : 0);
+      }
+      lag_ct[p] = ok ? c : AM_PK_ESC;
+    }
+  }
+}
+
+int build_lag(am_store *st) {
+  am_ctx *c = st->ctx;
+  am_op_log &d = st->dev;
+  d.lag_ct = nullptr, d.lag = nullptr, d.key_lag = nullptr;
+  if (!d.pk_vc || d.n_dc > LAG_MAX_DC || !d.n_keys) return AM_OK;
+  const uint64_t stride = d.snap_stride ? d.snap_stride : d.n_ops;
+  void *ct = nullptr, *lg = nullptr, *kl = nullptr;
+  if (int rc = am_dev_alloc(c, stride * 4 + 16, &ct)) return rc;
+  st->allocs.push_back(ct);
+  if (int rc = am_dev_alloc(c, (size_t)d.n_dc * stride * 2 + 16, &lg)) return rc;
+  st->allocs.push_back(lg);
+  if (int rc = am_dev_alloc(c, d.n_keys * d.n_dc * 4 + 16, &kl)) return rc;
+  st->allocs.push_back(kl);
+  // free slots (room for appends, padding) stay escaped: 0xFF bytes
+  AM_HIP(hipMemsetAsync(ct, 0xFF, stride * 4 + 16, c->stream));
+  AM_HIP(hipMemsetAsync(lg, 0, (size_t)d.n_dc * stride * 2 + 16, c->stream));
+  const uint64_t blocks = (d.n_keys + 3) / 4 < 65536 ? (d.n_keys + 3) / 4 : 65536;
+  hipLaunchKernelGGL(k_lag, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, (uint32_t *)ct, (uint16_t *)lg,
+                     (int32_t *)kl);
+  AM_HIP(hipGetLastError());
+  AM_HIP(hipStreamSynchronize(c->stream));
+  d.lag_ct = (const uint32_t *)ct, d.lag = (const uint16_t *)lg, d.key_lag = (const int32_t *)kl;
+  return AM_OK;
+}
+
 int build_records(am_store *st) {
   am_ctx *c = st->ctx;
   am_op_log &d = st->dev;
@@ -449,6 +571,8 @@ int build_zones(am_store *st, int level) {
 // (am_gc.hip)
 int am_store_pack_records(am_store *st) {
   if (int rc = build_records(st)) return rc;
+  if (int rc = build_esc_rows(st)) return rc;
+  if (int rc = build_lag(st)) return rc;
   return build_zones(st, st->zone_level);
 }
 
@@ -503,5 +627,7 @@ int am_store_pack(am_store *st) {
   d.key_tbase = (const uint64_t *)tb;
   d.pk_vc = (const uint32_t *)pk;
   if (int rc = build_records(st)) return rc;
+  if (int rc = build_esc_rows(st)) return rc;  // after k_rec_count's escapes of invalid effects
+  if (int rc = build_lag(st)) return rc;
   return build_zones(st, st->zone_level);
 }

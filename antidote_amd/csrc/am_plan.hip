@@ -32,15 +32,12 @@ constexpr int PER = 4;               // reads per thread
 constexpr uint32_t PCHUNK = PB * PER;
 // classes: 1..5 = the type, 6 = done (status written), 0 = an MV read of a key in the chunked
 // big view when `mvbig` (the big-read tier takes it straight from the batch, beside the other
-// tiers; class 0 starts at 0, so its list is the plan's index array and its count range[1]),
-// 7 = a bounded-counter read of a key longer than the wave tier's limit when `bcbig` (the
-// big-read tier takes it straight from the batch too; its list is written to a second array
-// from 0 and its count is tot[7])
+// tiers; class 0 starts at 0, so its list is the plan's index array and its count range[1])
 constexpr int NCLS = 8;
-constexpr uint32_t CLS_MVBIG = 0, CLS_DONE = 6, CLS_BCBIG = 7;
+constexpr uint32_t CLS_MVBIG = 0, CLS_DONE = 6;
 
 __device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read_batch &B, am_read_result &R,
-                                               uint64_t r, bool write_status, bool mvbig, bool bcbig) {
+                                               uint64_t r, bool write_status, bool mvbig) {
   const uint32_t t = B.type[r];
   const uint64_t key = B.key[r];
   if (t < AM_PN || t > AM_BCOUNTER || key >= L.n_keys) {
@@ -48,8 +45,6 @@ __device__ __forceinline__ uint32_t read_class(const am_op_log &L, const am_read
     return CLS_DONE;
   }
   if (mvbig && t == AM_MVREG && L.key_type[key] == AM_MVREG && am_ngrp_big(L.key_ngrp[key])) return CLS_MVBIG;
-  if (bcbig && t == AM_BCOUNTER && L.key_type[key] == AM_BCOUNTER && am_kend(L, key) - L.key_off[key] > AM_BCWAVE_OPS)
-    return CLS_BCBIG;
   return t;
 }
 
@@ -62,15 +57,14 @@ __device__ __forceinline__ uint64_t in_read(am_sel in, uint64_t i) {
 }
 
 __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
-                                                   uint32_t *cnt, uint32_t *tot, bool write_status, bool mvbig,
-                                                   bool bcbig) {
+                                                   uint32_t *cnt, uint32_t *tot, bool write_status, bool mvbig) {
   __shared__ uint32_t c[NCLS];
   if (threadIdx.x < NCLS) c[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = base + (uint64_t)j * PB + threadIdx.x;
-    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), write_status, mvbig, bcbig)], 1u);
+    if (i < nin) atomicAdd(&c[read_class(L, B, R, in_read(in, i), write_status, mvbig)], 1u);
   }
   __syncthreads();
   if (threadIdx.x < NCLS) cnt[(uint64_t)blockIdx.x * NCLS + threadIdx.x] = atomicAdd(&tot[threadIdx.x], c[threadIdx.x]);
@@ -78,9 +72,8 @@ __global__ void __launch_bounds__(PB) k_plan_count(am_op_log L, am_read_batch B,
 
 __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch B, am_read_result R, am_sel in,
                                                      const uint32_t *off, const uint32_t *tot, uint32_t *range,
-                                                     uint32_t *idx, uint32_t *idx7, bool mvbig, bool bcbig) {
+                                                     uint32_t *idx, bool mvbig) {
   __shared__ uint32_t run[NCLS];
-  __shared__ uint32_t start7;
   __shared__ uint32_t wcnt[PB / WAVE][NCLS];
   const uint32_t tid = threadIdx.x, w = tid / WAVE, lane = tid % WAVE;
   if (tid < NCLS) {  // class start = the totals of the classes before it
@@ -88,13 +81,12 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
     for (uint32_t k = 0; k < tid; ++k) start += tot[k];
     run[tid] = start + off[(uint64_t)blockIdx.x * NCLS + tid];
     if (blockIdx.x == 0) range[2 * tid] = start, range[2 * tid + 1] = start + tot[tid];
-    if (tid == CLS_BCBIG) start7 = start;
   }
   const uint64_t base = (uint64_t)blockIdx.x * PCHUNK, nin = in_count(B, in);
   for (int j = 0; j < PER; ++j) {
     const uint64_t i = base + (uint64_t)j * PB + tid;
     const uint64_t r = i < nin ? in_read(in, i) : 0;
-    const uint32_t c = i < nin ? read_class(L, B, R, r, false, mvbig, bcbig) : NCLS;
+    const uint32_t c = i < nin ? read_class(L, B, R, r, false, mvbig) : NCLS;
     uint32_t rank = 0;
     for (uint32_t k = 0; k < NCLS; ++k) {
       const uint64_t m = __ballot(c == k);
@@ -105,8 +97,7 @@ __global__ void __launch_bounds__(PB) k_plan_scatter(am_op_log L, am_read_batch 
     if (c < NCLS) {
       uint32_t before = run[c];
       for (uint32_t v = 0; v < w; ++v) before += wcnt[v][c];
-      if (c == CLS_BCBIG) idx7[before + rank - start7] = (uint32_t)r;
-      else idx[before + rank] = (uint32_t)r;
+      idx[before + rank] = (uint32_t)r;
     }
     __syncthreads();
     if (tid < NCLS) {
@@ -341,13 +332,11 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   am_ctx *sub[3] = {};
   am_retry retry[3];
   am_ctx *ms = nullptr;  // the early big-MV tier's sub-context
-  am_ctx *bs = nullptr;  // the early big bounded-counter tier's sub-context
   int rc = AM_OK;
   auto join = [&]() {
     for (am_ctx *s : sub)
       if (s && hipEventRecord(s->ev0, s->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, s->ev0, 0);
-    for (am_ctx *s : {ms, bs})
-      if (s && hipEventRecord(s->ev0, s->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, s->ev0, 0);
+    if (ms && hipEventRecord(ms->ev0, ms->stream) == hipSuccess) (void)hipStreamWaitEvent(ctx->stream, ms->ev0, 0);
   };
   // type t's set chain over class range `range` of selection idx, on its sub-context
   auto start_chain = [&](uint32_t t, const uint32_t *idx, const uint32_t *range, bool forked) -> int {
@@ -371,23 +360,21 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     return e;
   };
   // the planner over selection `in` (n_in reads) on c's stream, scratch slot `slot`:
-  // [range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n][idx7: n when bcbig]
-  auto plan = [&](am_ctx *c, int slot, am_sel in, uint64_t n_in, bool write_status, bool mvbig, bool bcbig,
-                  uint32_t **range, uint32_t **idx) -> int {
+  // [range: 2*NCLS][tot: NCLS][cnt: n_blk*NCLS][idx: n]
+  auto plan = [&](am_ctx *c, int slot, am_sel in, uint64_t n_in, bool write_status, bool mvbig, uint32_t **range,
+                  uint32_t **idx) -> int {
     const uint64_t n_blk = (n_in + PCHUNK - 1) / PCHUNK;
     void *scr = nullptr;
-    const uint64_t words = 3 * NCLS + n_blk * NCLS + (bcbig ? 2 : 1) * (n + 64);
-    if (int e = am_ctx_scratch(c, slot, words * sizeof(uint32_t), &scr)) return e;
+    if (int e = am_ctx_scratch(c, slot, (3 * NCLS + n_blk * NCLS + n + 64) * sizeof(uint32_t), &scr)) return e;
     *range = (uint32_t *)scr;
     uint32_t *tot = *range + 2 * NCLS, *cnt = tot + NCLS;
     *idx = cnt + n_blk * NCLS;
-    uint32_t *idx7 = bcbig ? *idx + n + 64 : nullptr;
     AM_HIP(hipMemsetAsync(tot, 0, NCLS * sizeof(uint32_t), c->stream));
     hipLaunchKernelGGL(k_plan_count, dim3((unsigned)n_blk), dim3(PB), 0, c->stream, *L, *B, *R, in, cnt, tot,
-                       write_status, mvbig, bcbig);
+                       write_status, mvbig);
     AM_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_plan_scatter, dim3((unsigned)n_blk), dim3(PB), 0, c->stream, *L, *B, *R, in, cnt, tot,
-                       *range, *idx, idx7, mvbig, bcbig);
+                       *range, *idx, mvbig);
     AM_HIP(hipGetLastError());
     return AM_OK;
   };
@@ -396,10 +383,8 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
   uint32_t types = 0;
   if (lanes && (rc = log_types(ctx, L, &types))) return rc;
   // Reads whose tier is known from their key alone are planned from the whole batch and start
-  // beside the lane tier: the bounded-counter chain, and straight to the big-read tier the MV
-  // reads of keys in the chunked big view (the later planner leaves them out) and the
-  // bounded-counter reads of keys beyond the wave tier's limit (which the chain would reach
-  // only after its row, wave and LDS-sort tiers)
+  // beside the lane tier: the bounded-counter chain, and the MV reads of keys in the chunked
+  // big view (straight to the big-read tier; the later planner leaves them out)
   const bool bc_early = lanes && ((types >> AM_BCOUNTER) & 1u);
   // (the type mask is a per-log cache that may be stale: the log itself must hold the view)
   const bool mv_early = lanes && (types & TYPES_MVBIG) && L->key_ngrp && L->rec_g;
@@ -413,20 +398,17 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
       am_ctx *es = am_ctx_sub(ctx, bc_early ? (int)(AM_BCOUNTER - AM_AWSET) : 3);
       if (!es) return AM_ERR_HIP;
       AM_HIP(hipStreamWaitEvent(es->stream, ctx->ev_fork, 0));
-      rc = plan(es, AM_SCR_SPARE, all, n, false, mv_early, bc_early, &erange, &eidx);
-      if (!rc) AM_HIP(hipEventRecord(es->ev0, es->stream));  // the early plan, for the early big tiers
+      rc = plan(es, AM_SCR_SPARE, all, n, false, mv_early, &erange, &eidx);
       if (!rc && mv_early) {
         ms = am_ctx_sub(ctx, 3);
         if (!ms) return AM_ERR_HIP;
         ms->grp_hint_in = ctx->grp_hint_in;
         ms->tee_a = ctx->tee_a, ms->tee_b = ctx->tee_b, ms->tee_g = ctx->tee_g, ms->tee_shift = ctx->tee_shift;
         ms->tee_done = ctx->tee_done;
-        if (ms != es) AM_HIP(hipStreamWaitEvent(ms->stream, es->ev0, 0));
-      }
-      if (!rc && bc_early) {
-        bs = am_ctx_sub(ctx, 4);
-        if (!bs) return AM_ERR_HIP;
-        AM_HIP(hipStreamWaitEvent(bs->stream, es->ev0, 0));
+        if (ms != es) {
+          AM_HIP(hipEventRecord(es->ev0, es->stream));
+          AM_HIP(hipStreamWaitEvent(ms->stream, es->ev0, 0));
+        }
       }
       if (!rc && bc_early) rc = start_chain(AM_BCOUNTER, eidx, erange, true);
     }
@@ -442,12 +424,6 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
       big.list = eidx;
       rc = am_launch_big(ms, L, B, R, AM_MVREG, big);
     }
-    if (!rc && bc_early) {  // class 7 of the early plan: its own list, its count tot[7]
-      am_retry big;
-      big.count = erange + 3 * NCLS - 1;
-      big.list = eidx + n + 64;
-      rc = am_launch_big(bs, L, B, R, AM_BCOUNTER, big);
-    }
     // one counter readback: a batch of short reads (the common case) ends here instead of
     // launching the planner and every class's kernels over empty selections
     uint64_t hc = 0;
@@ -462,7 +438,7 @@ int am_launch_materialize(am_ctx *ctx, const am_op_log *L, const am_read_batch *
     in.range = lbuf;
   }
   uint32_t *range = nullptr, *idx = nullptr;
-  rc = plan(ctx, AM_SCR_PLAN, in, n_in, true, mv_early, false, &range, &idx);
+  rc = plan(ctx, AM_SCR_PLAN, in, n_in, true, mv_early, &range, &idx);
   if (!rc && hipEventRecord(ctx->ev_fork, ctx->stream) != hipSuccess) rc = AM_ERR_HIP;
   for (uint32_t t = AM_AWSET; t <= AM_BCOUNTER && !rc; ++t)
     if (t != AM_BCOUNTER || !bc_early) rc = start_chain(t, idx, range, false);

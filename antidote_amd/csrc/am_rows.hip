@@ -271,10 +271,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows(am_op_log L, am_read_batch B, am
           } else {
             uint64_t ct, sv[DMAX];
             if (PACKED) {  // rare: the op does not fit the packed view
-              meta = L.op_meta[p];
-              ct = L.commit_time[p];
-#pragma unroll
-              for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+              esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
             } else {
               ct = cur.w;
 #pragma unroll

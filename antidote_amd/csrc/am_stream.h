@@ -305,6 +305,8 @@ __global__ void __launch_bounds__(BLOCK) k_stream(am_op_log L, am_read_batch B, 
       const bool txm = GENERAL && u.has_txid && T.tx[k] == u.txid;
       if (PACKED) {
         if (T.x[k][0] == AM_PK_ESC) {  // rare: the op does not fit the packed view
+          // (from the columns: the escape row's lookup here cost the batch-clock LWW kernel its
+          // third wave per SIMD, 163 -> 169 VGPRs, and C2 1.55 -> 1.9 ms)
           uint64_t sv[DMAX];
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;

@@ -305,6 +305,29 @@ struct AccP {
     min_excl = NONE;
   }
 };
+// An escaped op's full-width inputs (is_op_in_snapshot/7): its escape row when the log has one
+// (am_op_log.esc_rows, index + 1 in the op's DC-1 packed entry; null otherwise -- and for an op
+// that is not escaped, whose DC-1 entry is a time: full-view callers may ask for any op)
+__device__ __forceinline__ const uint64_t *esc_row(const am_op_log &L, uint64_t stride, uint64_t p) {
+  if (!L.esc_rows || L.pk_vc[p] != AM_PK_ESC) return nullptr;
+  const uint32_t ri = L.pk_vc[stride + p];
+  return ri ? L.esc_rows + (uint64_t)(ri - 1) * (2 + L.n_dc) : nullptr;
+}
+// commit time, meta byte and snapshot entries of escaped op p: one row, or the op columns
+template <int DMAX>
+__device__ __forceinline__ void esc_load(const am_op_log &L, uint32_t nd, uint64_t stride, uint64_t p,
+                                         uint64_t (&sv)[DMAX], uint64_t &ct, uint32_t &meta) {
+  if (const uint64_t *w = esc_row(L, stride, p)) {
+    ct = w[0], meta = (uint32_t)w[1];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? w[2 + d] : 0;
+    return;
+  }
+  ct = L.commit_time[p], meta = L.op_meta[p];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+}
+
 // x[0] == AM_PK_ESC ops are the caller's (full columns)
 template <int DMAX, bool GENERAL>
 __device__ __forceinline__ bool pk_eval(const PkRead<DMAX> &t, const ReadU<DMAX> &u, const uint32_t (&x)[DMAX],
@@ -388,6 +411,66 @@ __device__ __forceinline__ uint32_t pk_tile(const ReadU<DMAX> &u, const PkRead<D
   return ib;
 }
 
+// a read over the lag view (am_op_log.lag_ct / lag / key_lag): its key's lag bases
+template <int DMAX>
+struct LagRead {
+  bool on;
+  uint32_t lb[DMAX];
+};
+template <int DMAX>
+__device__ __forceinline__ void lag_setup(const am_op_log &L, uint32_t nd, uint64_t key, bool on, LagRead<DMAX> &lr) {
+  lr.on = on;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) lr.lb[d] = on && d < (int)nd ? uniform_u32((uint32_t)L.key_lag[key * nd + d]) : 0u;
+}
+
+// pk_tile (am_wave.h) over the lag view: the OPL ops' commit entries c (AM_PK_ESC: escaped, or a
+// lag beyond 16 bits) and their u16 lags lw (two per word), the entries X[d] - K = c - (lb[d] +
+// lag) rebuilt where the compares and the max use them
+template <int DMAX, int OPL, bool GENERAL>
+__device__ __forceinline__ uint32_t pk_tile_lag(const ReadU<DMAX> &u, const PkRead<DMAX> &pk, const LagRead<DMAX> &lr,
+                                                const uint32_t (&c)[OPL], const uint32_t (&lw)[DMAX][(OPL + 1) / 2],
+                                                const uint64_t (&tx)[OPL], uint64_t g, uint64_t off0, uint64_t off1,
+                                                AccP<DMAX> &ap, bool &esc) {
+  auto xd = [&](int k, int d) -> uint32_t {
+    const uint32_t w = lw[d][k / 2];
+    return c[k] - (lr.lb[d] + ((k & 1) ? w >> 16 : w & 0xFFFFu));
+  };
+  uint32_t ib = 0, ev = 0;
+#pragma unroll
+  for (int k = 0; k < OPL; ++k) {
+    const uint64_t p = g + k;
+    const bool inr = p >= off0 && p < off1;
+    const bool e = c[k] == AM_PK_ESC;
+    esc |= inr && e;
+    uint32_t over = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(xd(k, d), pk.thr[d]);
+    bool cand = inr && !e;
+    if (GENERAL) {  // belongs_to_snapshot_op: not vectorclock:le(X, base)
+      uint32_t cov = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) cov |= __builtin_elementwise_sub_sat(xd(k, d), pk.cthr[d]);
+      const bool le = !pk.cnever && cov == 0;
+      cand = cand && (u.base_ignore || (u.has_txid && tx[k] == u.txid) || !le);
+    }
+    ib |= (uint32_t)(cand && !pk.never && over == 0) << k;
+    ev |= (uint32_t)cand << k;
+  }
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    uint32_t m = ap.mx[d];
+#pragma unroll
+    for (int k = 0; k < OPL; ++k) m = max(m, ((ib >> k) & 1u) ? xd(k, d) : 0u);
+    ap.mx[d] = m;
+  }
+  ap.count += (uint32_t)__popc(ib);
+  const uint32_t ex = ev & ~ib;
+  if (ex) ap.min_excl = umin64(ap.min_excl, g + (uint64_t)__builtin_ctz(ex));
+  if (ev) ap.flags |= pk.miss;
+  return ib;
+}
+
 // Inclusion of the 4 ops [g, g + 4) of one read inside [lo, hi) (is_op_in_snapshot/7 +
 // belongs_to_snapshot_op/3, every clock general): bit k = op g + k included.  Packed view
 // (PACKED): u32 entries through pk_tile, partials in ap, escaped ops from the full columns;
@@ -420,12 +503,11 @@ __device__ __forceinline__ uint32_t incl4(const am_op_log &L, uint32_t nd, uint6
     const uint64_t p = g + k;
     if (p < lo || p >= hi) continue;
     if (PACKED && L.pk_vc[p] != AM_PK_ESC) continue;
-    uint64_t sv[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) sv[d] = d < (int)nd ? L.snap_vc[(uint64_t)d * stride + p] : 0;
+    uint64_t sv[DMAX], ct;
+    uint32_t meta;
+    esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
     const uint32_t sp = L.snap_pres ? L.snap_pres[p] : u.allmask;
-    if (eval_op<DMAX, true>(u, L.op_meta[p], L.commit_time[p], sv, sp, u.has_txid && tx[k] == u.txid, p, a))
-      ib |= 1u << k;
+    if (eval_op<DMAX, true>(u, meta, ct, sv, sp, u.has_txid && tx[k] == u.txid, p, a)) ib |= 1u << k;
   }
   return ib;
 }

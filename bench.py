@@ -149,16 +149,28 @@ def set_view_bytes(mat, dlog, ko, kt):
     return float((off1 - off0)[quad].sum()) * GMASK_BYTES + float(nrec[~quad].sum()) * REC_BYTES
 
 
-def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None):
+def lag_split(cfg, dlog, base, index_level) -> bool:
+    """Whether the set reads of this step stream the lag view (am_op_log.lag_ct / lag / key_lag:
+    4 + 2 D bytes of commit vector per op, 4 D of lag bases per read): the split fresh read of a
+    single-type set batch (k_grp_incl) over a store without a zone index at D <= 8."""
+    return (base == "fresh" and index_level == abi.AM_INDEX_NONE and cfg["n_dc"] <= 8
+            and cfg["type"] in (abi.AM_AWSET, abi.AM_MVREG) and bool(dlog.lag_ct))
+
+
+def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None, lag=False):
     """Algorithmic bytes of one am_materialize over every key of the store (the layout model:
-    what the kernels must stream of this build's HBM layout)."""
+    what the kernels must stream of this build's HBM layout).  lag: the set reads
+    stream the lag view instead of the packed commit vectors (lag_split)."""
     lens = np.diff(ko.astype(np.int64))
     records = packed and bool(dlog.rec_key_off)
     total = set_view_bytes(mat, dlog, ko, kt) if records else float(dlog.n_var) * 8
     set_len = reads.set_len.cpu().numpy() if reads.set_len is not None else None
     for t in sorted(set(int(x) for x in np.unique(kt))):
         m = kt == t
-        total += float(lens[m].sum()) * bytes_per_op(t, cfg["n_dc"], packed)
+        if lag and t in (abi.AM_AWSET, abi.AM_MVREG):  # lag_ct 4 + lags 2 D per op, lag bases 4 D per read
+            total += float(lens[m].sum()) * (4 + 2 * cfg["n_dc"]) + float(m.sum()) * 4 * cfg["n_dc"]
+        else:
+            total += float(lens[m].sum()) * bytes_per_op(t, cfg["n_dc"], packed)
         sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER)) \
             else 0.0
         total += float(m.sum()) * (bytes_per_key(t, cfg["n_dc"], sl) + (8 if packed else 0))
@@ -495,7 +507,8 @@ def measure(st: Step, base: str, steps: int, warmup: int, barrier, pg, timed_wal
     kern_ms = float(np.mean(kern_ev))
     cfg = st.cfg
     packed = bool(st.dlog.pk_vc)
-    alg_bytes = workload_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, packed, mat)
+    alg_bytes = workload_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, packed, mat,
+                               lag=lag_split(cfg, st.dlog, base, st.index_level))
     if base == "cached":
         alg_bytes += cached_bytes(cfg, st.pre, st.reads)
     # the commit vectors of ops whose zone decided them are not streamed, nor the records whose
@@ -635,8 +648,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
-                              "packed commit vectors 4*D per op, payload, 4 B per token-group record or 8 B per "
-                              "group-mask op, per-read metadata and outputs; every op streamed (no zone index)"
+                              "commit vectors (packed: 4*D per op; lag view: 4 + 2*D per op and 4*D per read), "
+                              "payload, 4 B per token-group record or 8 B per group-mask op, per-read metadata and "
+                              "outputs; every op streamed (no zone index)"
                               if level == abi.AM_INDEX_NONE else
                               "layout bytes (DESIGN.md 4) minus the commit vectors / records the zone index stood in for",
                      "traffic": load_traffic(args.config if args.base == "fresh" else args.config + "_cached", workload,
@@ -653,8 +667,10 @@ def main():
                      "alg_bytes_per_launch": m["alg_bytes"],
                      "ops_skipped_per_launch": m["skipped"], "records_skipped_per_launch": m["rskip"],
                      "gsum_words_per_launch": m["gsw"],
-                     "layout": "packed (u32 commit vectors relative to a per-key time base); set effects as u32 token-group records"
-                     if m["packed"] else "full"},
+                     "layout": ("lag view (u32 commit time + u16 lag per DC, relative to per-key bases)"
+                                if lag_split(cfg, st.dlog, args.base, level) else
+                                "packed (u32 commit vectors relative to a per-key time base)")
+                               + "; set effects as u32 token-group records" if m["packed"] else "full"},
         "cpu_baseline": None,
     }
 

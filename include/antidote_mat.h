@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define AM_ABI_VERSION 10
+#define AM_ABI_VERSION 12
 #define AM_MAX_DC 32
 
 /* CRDT types (the reference's type atoms) */
@@ -241,6 +241,27 @@ typedef struct am_op_log {
    * have their births close together here, while in grp (output order) they lie a group run
    * apart: the record pass gathers a survivor's pair through its birth record. */
   const uint64_t *prec;        /* [n_rec][2] or NULL                                 */
+  /* Escape rows (device stores with the packed view and n_dc >= 2, or NULL): an op escaped from
+   * the packed view (pk_vc[0][p] == AM_PK_ESC) with pk_vc[1][p] = i > 0 has its full-width
+   * inputs of is_op_in_snapshot/7 in row i - 1 of 2 + n_dc words: commit time, op_meta, then
+   * snapshot_time entries by DC -- one contiguous row instead of n_dc + 2 column lines.  An
+   * escaped op with pk_vc[1][p] == 0 (written in place since the rows were built) reads the
+   * columns.  Escapes are ops with an entry outside the key's 2^32-us window (a DC whose entry
+   * lags, e.g. behind a partition) or an invalid effect. */
+  const uint64_t *esc_rows;    /* [n_esc][2 + n_dc] or NULL                           */
+  /* Lag view (device stores with the packed view, n_dc <= 16, or NULL): an op's commit vector
+   * as its commit time and one 16-bit lag per DC -- the snapshot entries of a transaction trail
+   * its commit by milliseconds -- so the inclusion test streams 4 + 2 * n_dc bytes per op instead
+   * of 4 * n_dc (20 B at D = 8, not 32):
+   *   lag_ct[p]     = commit_time - key_tbase[k]   (u32), or AM_PK_ESC when the op is escaped
+   *                   from the packed view or one of its lags does not fit
+   *   lag[d][p]     = (commit_time - X[d]) - key_lag[k][d]   in [0, 0xFFFF]   (X[dc] = ct: lag 0)
+   *   key_lag[k][d] = the smallest commit_time - X[d] over the key's fitting ops (int32)
+   * so X[d] - key_tbase[k] = lag_ct[p] - key_lag[k][d] - lag[d][p].  Maintained by every writer
+   * (am_store_apply rewrites a touched key's columns and its key_lag row). */
+  const uint32_t *lag_ct;      /* [snap_stride]                                       */
+  const uint16_t *lag;         /* [n_dc][snap_stride]                                 */
+  const int32_t *key_lag;      /* [n_keys][n_dc]                                      */
 } am_op_log;
 #define AM_ZONE_OPS 256u
 #define AM_GMASK_MAX_GRP 32u

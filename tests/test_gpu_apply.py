@@ -259,3 +259,55 @@ def test_gpu_vnode_load_hot_key_beside_short_keys(mat):
         compare_state(vn, st, {0: 0, 1: 1, 2: 2}, types, {d: d for d in range(n_dc)})
     finally:
         vn.close()
+
+
+@pytest.mark.parametrize("n_dc", [2, 5])
+def test_gpu_apply_escaped_ops(mat, n_dc):
+    """Ops escaped from the packed view (a snapshot entry 2^33 us behind: a lagging DC) in a
+    store with escape rows, then appended in place (an op written in place reads its escaped
+    inputs from the columns, am_op_log.esc_rows): reads match the oracle over the same ops and
+    a store built from them (rows for every escaped op)."""
+    from oracle import amo
+    from antidote_amd.oplog import HostBatch
+    rng = random.Random(9500 + n_dc)
+    t0 = 1 << 40
+    n_keys = 48
+    types = [randlog.TYPES[k % 5] for k in range(n_keys)]
+
+    def lag(ops):
+        for op in ops:
+            if rng.random() < 0.3:
+                d = rng.choice([d for d in range(n_dc) if d != op.commit_dc])
+                op.snap[d] = t0 - (1 << 33)
+        return ops
+
+    keys = [lag(randlog.rand_key_ops(rng, types[k], n_dc, rng.choice([0, 3, 20, 70]), t0=t0)) for k in range(n_keys)]
+    base = mat.store(HostLog(n_dc, keys, key_types=types))
+    inp = base.reserve()
+    try:
+        touched = sorted(rng.sample(range(n_keys), 20))
+        new_ops = []
+        for k in touched:
+            last = keys[k][-1].commit_time if keys[k] else t0
+            new_ops.append(lag(randlog.rand_key_ops(rng, types[k], n_dc, 1, t0=last)))  # fits the key's room
+        ok, _ = inp.apply(touched, new_log=HostLog(n_dc, new_ops, key_types=[types[k] for k in touched]))
+        assert ok
+        full = [list(ops) for ops in keys]
+        for k, ops in zip(touched, new_ops):
+            full[k] = full[k] + ops
+        flog = HostLog(n_dc, full, key_types=types)
+        fresh = mat.store(flog)
+        try:
+            for q in (0.3, 0.7, 1.0):
+                clock = {d: t0 + int(q * 400) for d in range(n_dc)}
+                reads = [Read(k, types[k], clock) for k in range(n_keys)]
+                ref = amo.materialize(flog, HostBatch(n_dc, reads))
+                for st in (inp, fresh):
+                    got = mat.read_batch(st, reads)
+                    for i in range(n_keys):
+                        assert got.result(i) == ref.result(i), (q, i, got.result(i), ref.result(i))
+        finally:
+            fresh.close()
+    finally:
+        inp.close()
+        base.close()
