@@ -100,6 +100,8 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
     if (GENERAL) bc_inputs<DMAX, true>(L, B, nd, r, u);
     PkRead<DMAX> pk;
     pk_setup(u, nd, uniform_u64(L.key_tbase[key]), pk);
+    LagRead<DMAX> lr;  // the batch clock at D > 8 reads the lag view where the store has one
+    lag_setup(L, nd, key, !GENERAL && DMAX > 8 && L.lag_ct != nullptr, lr);
     // slots start at the base value (orddict entries present in the base stay present)
     if (lane < DMAX) s.emx[lane] = 0;
     for (uint32_t k = lane; k < ns; k += WAVE) {
@@ -152,6 +154,16 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
       uint32_t ib;
       if constexpr (GENERAL) {
         ib = incl4<DMAX, true>(L, nd, stride, u, pk, g, off0, off1, ap, a);
+      } else if (DMAX > 8 && lr.on) {  // 4 + 2 D bytes per op
+        static_assert(GENERAL || DMAX <= 8 || OL == 2, "the lag loads below take 2 ops per lane");
+        typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t cv = *(const u32x2_t *)(L.lag_ct + g);
+        const uint32_t c[OL] = {cv.x, cv.y};
+        uint32_t lw[DMAX][(OL + 1) / 2];
+        uint64_t tx[OL] = {};
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) lw[d][0] = d < (int)nd ? *(const uint32_t *)(L.lag + (uint64_t)d * stride + g) : 0u;
+        ib = pk_tile_lag<DMAX, OL, false>(u, pk, lr, c, lw, tx, g, off0, off1, ap, esc);
       } else {
         uint32_t x[OL][DMAX];
         uint64_t tx[OL];
@@ -199,8 +211,9 @@ __global__ void __launch_bounds__(BLOCK) k_bc_wave(am_op_log L, am_read_batch B,
         uint64_t vS = 0;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) vS = (uint32_t)d == lane ? u.S[d] : vS;
+        const uint32_t *escv = lr.on ? L.lag_ct : L.pk_vc;  // the view the loop streamed
         for (uint64_t p = off0 + lane; p < off1; p += WAVE) {
-          if (L.pk_vc[p] != AM_PK_ESC) continue;
+          if (escv[p] != AM_PK_ESC) continue;
           const uint64_t *w = esc_row(L, stride, p);  // its escape row, or the columns
           const uint32_t meta = w ? (uint32_t)w[1] : L.op_meta[p], dc = meta & 31u;
           const uint64_t ct = w ? w[0] : L.commit_time[p];

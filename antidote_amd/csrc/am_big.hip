@@ -526,23 +526,38 @@ __device__ __forceinline__ void lean_clock(const am_read_batch &B, uint32_t nd, 
 // escaped ops' count / flags / min in a and their maxima in emx
 template <int DMAX>
 __device__ __forceinline__ uint32_t lean_incl4(const am_op_log &L, uint32_t nd, uint64_t stride, const ReadU<DMAX> &u,
-                                               const PkRead<DMAX> &pk, uint64_t vS, uint64_t g, uint64_t lo,
-                                               uint64_t hi, AccP<DMAX> &ap, Acc<DMAX> &a, unsigned long long *emx) {
-  uint32_t xs[4][DMAX];
-#pragma unroll
-  for (int d = 0; d < DMAX; ++d) {
-    u32x4 q = {0, 0, 0, 0};
-    if (d < (int)nd) q = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
-    xs[0][d] = q.x, xs[1][d] = q.y, xs[2][d] = q.z, xs[3][d] = q.w;
-  }
+                                               const PkRead<DMAX> &pk, const LagRead<DMAX> &lr, uint64_t vS,
+                                               uint64_t g, uint64_t lo, uint64_t hi, AccP<DMAX> &ap, Acc<DMAX> &a,
+                                               unsigned long long *emx) {
   const uint64_t tx[4] = {0, 0, 0, 0};
   bool esc = false;
-  uint32_t ib = pk_tile<DMAX, 4, false>(u, pk, xs, tx, g, lo, hi, ap, esc);
+  uint32_t ib;
+  if (lr.on) {  // the lag view: 4 + 2 D bytes per op
+    const u32x4 cq = *(const u32x4 *)(L.lag_ct + g);
+    const uint32_t c[4] = {cq.x, cq.y, cq.z, cq.w};
+    uint32_t lw[DMAX][2];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      const uint2 v = d < (int)nd ? *(const uint2 *)(L.lag + (uint64_t)d * stride + g) : uint2{0, 0};
+      lw[d][0] = v.x, lw[d][1] = v.y;
+    }
+    ib = pk_tile_lag<DMAX, 4, false>(u, pk, lr, c, lw, tx, g, lo, hi, ap, esc);
+  } else {
+    uint32_t xs[4][DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      u32x4 q = {0, 0, 0, 0};
+      if (d < (int)nd) q = *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + g);
+      xs[0][d] = q.x, xs[1][d] = q.y, xs[2][d] = q.z, xs[3][d] = q.w;
+    }
+    ib = pk_tile<DMAX, 4, false>(u, pk, xs, tx, g, lo, hi, ap, esc);
+  }
   if (!esc) return ib;
+  const uint32_t *escv = lr.on ? L.lag_ct : L.pk_vc;
 #pragma unroll 1
   for (int k = 0; k < 4; ++k) {  // rare
     const uint64_t p = g + k;
-    if (p < lo || p >= hi || L.pk_vc[p] != AM_PK_ESC) continue;
+    if (p < lo || p >= hi || escv[p] != AM_PK_ESC) continue;
     const uint64_t *w = esc_row(L, stride, p);  // its escape row, or the columns
     const uint32_t meta = w ? (uint32_t)w[1] : L.op_meta[p], dc = meta & 31u;
     const uint64_t ct = w ? w[0] : L.commit_time[p];
@@ -592,6 +607,9 @@ __device__ __forceinline__ void wave_partials(AccP<DMAX> &ap, const PkRead<DMAX>
 //      and reach the read's accumulators once per read and workgroup (k_big_chunk reduces and
 //      flushes every chunk).  LDS holds only what the type needs: MV the two hash sets, the
 //      bounded counter its slot sums (k_big_chunk's 64 KB allow two workgroups per CU). ----
+#ifndef AM_BIGRUN_LAG
+#define AM_BIGRUN_LAG 0  // the bounded-counter runs keep the packed view: the lag branch costs them
+#endif                   // an occupancy step (D = 16: 163 -> 173 VGPRs, 3 -> 2 waves)
 template <int DMAX, int TYPE, bool PACKED, bool LEAN = false>
 __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B, const uint32_t *nbig_p,
                                                    const BigRead *br, BigAcc *accs, uint32_t *bm, BigSlots SL,
@@ -622,6 +640,8 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
   Acc<DMAX> a;
   // the read's partials -> its accumulators (one LDS round over the waves)
   uint64_t vS = 0;  // LEAN: lane d holds the clock's entry d
+  LagRead<DMAX> lr;  // LEAN: the read's lag bases (the lag view, when the store has one)
+  lr.on = false;
   auto flush = [&]() {
     uint64_t mx[DMAX];
     wave_partials<DMAX, PACKED, LEAN>(ap, pk, u, nd, a, mx);
@@ -673,7 +693,9 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
       R0 = br[b];
       if (tid < DMAX) emx[tid] = 0;
       __syncthreads();
-      pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[R0.r])]), pk);
+      const uint64_t key = uniform_u64(B.key[R0.r]);
+      pk_setup(u, nd, uniform_u64(L.key_tbase[key]), pk);
+      lag_setup(L, nd, key, AM_BIGRUN_LAG && L.lag_ct != nullptr, lr);
       ap.reset();
       a.reset();
     } else if (b != cur) {
@@ -703,7 +725,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     if (TYPE == AM_BCOUNTER) {  // included ops -> LDS slot sums (orddict:update_counter)
       if (g < hi) {
         const uint32_t meta4 = *(const uint32_t *)(L.op_meta + g);
-        const uint32_t ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, vS, g, R0.off0, hi, ap, a, emx)
+        const uint32_t ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, lr, vS, g, R0.off0, hi, ap, a, emx)
                                  : incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
 #pragma unroll
         for (int k = 0; k < OPL; ++k) {
@@ -726,7 +748,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_run(am_op_log L, am_read_batch B,
     if (tid < CHUNK / 32) incl[tid] = 0;
     __syncthreads();
     if (g < hi) {
-      const uint32_t ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, vS, g, R0.off0, hi, ap, a, emx)
+      const uint32_t ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, lr, vS, g, R0.off0, hi, ap, a, emx)
                                : incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
       if (ib) atomicOr(&incl[(uint32_t)(g - lo) >> 5], ib << ((uint32_t)(g - lo) & 31u));
     }
@@ -767,6 +789,8 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
   AccP<DMAX> ap;
   Acc<DMAX> a;
   uint64_t vS = 0;  // LEAN: lane d holds the clock's entry d
+  LagRead<DMAX> lr;  // LEAN: the read's lag bases (the lag view, when the store has one)
+  lr.on = false;
   auto flush = [&]() {
     uint64_t mx[DMAX];
     wave_partials<DMAX, PACKED, LEAN>(ap, pk, u, nd, a, mx);
@@ -804,7 +828,9 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
       R0 = br[b];
       if (tid < DMAX) emx[tid] = 0;
       __syncthreads();
-      pk_setup(u, nd, uniform_u64(L.key_tbase[uniform_u64(B.key[R0.r])]), pk);
+      const uint64_t key = uniform_u64(B.key[R0.r]);
+      pk_setup(u, nd, uniform_u64(L.key_tbase[key]), pk);
+      lag_setup(L, nd, key, L.lag_ct != nullptr, lr);
       ap.reset();
       a.reset();
     } else if (b != cur) {
@@ -834,7 +860,7 @@ __global__ void __launch_bounds__(BLOCK) k_big_gincl(am_op_log L, am_read_batch 
     const uint64_t g = lo + (uint64_t)tid * OPL;
     uint32_t ib = 0;
     if (g < hi)
-      ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, vS, g, R0.off0, hi, ap, a, emx)
+      ib = LEAN ? lean_incl4<DMAX>(L, nd, stride, u, pk, lr, vS, g, R0.off0, hi, ap, a, emx)
                 : incl4<DMAX, PACKED>(L, nd, stride, u, pk, g, R0.off0, hi, ap, a);
     uint32_t word = ib << (OPL * (tid % 8));  // 8 lanes of 4 ops per 32-bit word
     word |= (uint32_t)__shfl_xor((int)word, 1);

@@ -446,8 +446,8 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
     // ---- 1. inclusion per op -> bitmap + scalar partials ----
     PkRead<DMAX> pk;
     if (PACKED) pk_setup(u, nd, uniform_u64(L.key_tbase[m.key]), pk);
-    LagRead<DMAX> lr;  // (the packed view)
-    lag_setup(L, nd, m.key, false, lr);
+    LagRead<DMAX> lr;
+    lag_setup(L, nd, m.key, PACKED && L.lag_ct != nullptr, lr);
     AccP<DMAX> ap;
     Acc<DMAX> a;
     ap.reset();
@@ -467,7 +467,8 @@ __global__ void __launch_bounds__(WBLOCK, 4) k_grp_wg(am_op_log L, am_read_batch
     }
     const bool full = !PACKED || __syncthreads_or(esc);
     if (PACKED && full)  // rare: ops outside the packed view, from the full columns
-      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, tid, WBLOCK, s.incl, a, L.pk_vc);
+      esc_pass<DMAX, GENERAL>(L, nd, u, m.off0, m.off1, t0, stride, tid, WBLOCK, s.incl, a,
+                              lr.on ? L.lag_ct : L.pk_vc);
     {  // wave partials of the scalar outputs (VGPR reductions: the scalar file is full)
       uint32_t cnt, fl, pr;
       uint64_t mn, mxl;

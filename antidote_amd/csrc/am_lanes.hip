@@ -392,6 +392,7 @@ struct QSlot {  // the read at a scan position, for the quad that scans it
   uint64_t off0, rk0;
   uint32_t nops, nrec, tk, ctl;  // ctl: AM_FLAG_MISSING_DC_LOGGED | never << 31
   uint32_t thr[DMAX];            // MinSnapshotTime - K per DC (pk_clamp)
+  uint32_t lb[DMAX];             // the lag view: the key's lag bases (key_lag; 0 past n_dc)
 };
 struct QOwn {  // the lane's own read of a block (registers, from q_publish)
   uint64_t off0, K, rk0, idb, ooff;
@@ -470,7 +471,7 @@ __device__ __forceinline__ QMeta q_meta(const am_op_log &L, const am_read_result
 // does not take go to `next` (one atomic per wave), the rest are placed by type (PN, LWW, AW, MV,
 // then the reads their own lanes finish, then the rest).  Returns the lane's position; *any
 // whether any read is taken.
-template <int DMAX>
+template <int DMAX, bool LAG>
 __device__ __forceinline__ QOwn q_publish(const am_op_log &L, const am_read_result &R, const ReadU<DMAX> &u,
                                           uint32_t nd, const QMeta &m, bool inb, uint32_t accept, am_retry next,
                                           QSlot<DMAX> *slot, uint32_t lane, bool &any) {
@@ -523,6 +524,10 @@ __device__ __forceinline__ QOwn q_publish(const am_op_log &L, const am_read_resu
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) w.thr[d] = pk.thr[d];
     w.ctl = pk.miss | (pk.never ? QC_NEVER : 0u);
+    if (LAG) {
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) w.lb[d] = d < (int)nd ? (uint32_t)L.key_lag[m.key * nd + d] : 0u;
+    }
   }
   any = __ballot(take) != 0;
   return o;
@@ -586,7 +591,10 @@ __device__ __forceinline__ void q_lww(uint32_t ib, u32x4 e0, u32x4 e1, u32x4 e2,
     lv.has |= in ? 1u : 0u;
   }
 }
-template <int DMAX, bool SEL>
+#ifndef AM_LANE_LAG
+#define AM_LANE_LAG 1
+#endif
+template <int DMAX, bool SEL, bool LAG>
 __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                    am_retry next, uint32_t accept) {
   constexpr int NPH = qph<DMAX>();
@@ -607,7 +615,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
   QSlot<DMAX> *const slot = sm.slot;
   QPre pn = q_pre<SEL>(B, S, sel0, nsel, first + step + lane);
   bool any = false;
-  QOwn own = q_publish<DMAX>(L, R, u, nd, q_meta(L, R, q_pre<SEL>(B, S, sel0, nsel, first + lane)),
+  QOwn own = q_publish<DMAX, LAG>(L, R, u, nd, q_meta(L, R, q_pre<SEL>(B, S, sel0, nsel, first + lane)),
                              first + lane < nsel, accept, next, slot, lane, any);
   wave_sync();
   PH_DECL();
@@ -617,7 +625,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
     if (!any) {
       m = q_meta(L, R, pn);
       pn = q_pre<SEL>(B, S, sel0, nsel, b0 + 2 * step + lane);
-      own = q_publish<DMAX>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
+      own = q_publish<DMAX, LAG>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
       wave_sync();
       PH(5);
       continue;
@@ -631,6 +639,8 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
 #pragma unroll
     for (int pg = 0; pg < 4; pg += NPH) {
       u32x4 xv[NPH][DMAX], wv[NPH][4];
+      u32x4 cv[NPH];         // LAG: the tile's lag_ct words
+      uint2 lv[NPH][DMAX];   // LAG: its u16 lags, 4 per DC
 #pragma unroll
       for (int h = 0; h < NPH; ++h) {
         const QSlot<DMAX> &sl = slot[16 * (pg + h) + qq];
@@ -639,9 +649,16 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
         const uint64_t o0 = sl.off0, o1 = o0 + sl.nops, g = (o0 & ~3ull) + 4 * qj;
         const bool lo = qt && g < o1;
         const uint64_t gg = lo ? g : 0;
+        if constexpr (LAG) {  // 4 + 2 D bytes per op
+          cv[h] = *(const u32x4 *)(L.lag_ct + gg);
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d)
-          xv[h][d] = d < (int)nd ? *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + gg) : u32x4{0, 0, 0, 0};
+          for (int d = 0; d < DMAX; ++d)
+            lv[h][d] = d < (int)nd ? *(const uint2 *)(L.lag + (uint64_t)d * stride + gg) : uint2{0, 0};
+        } else {
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d)
+            xv[h][d] = d < (int)nd ? *(const u32x4 *)(L.pk_vc + (uint64_t)d * stride + gg) : u32x4{0, 0, 0, 0};
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {  // PN p0 | LWW p0, p1 | a set read's group masks
           const bool v = lo && (e < 2 || ty == AM_LWW);
@@ -670,12 +687,22 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
         uint32_t mx[DMAX];
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) mx[d] = 0;
+        if constexpr (LAG) {  // the packed entries X[d] - K = lag_ct - (lb[d] + lag[d])
+          const u32x4 c = cv[h];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            const uint32_t b = sl.lb[d];
+            const uint2 v = lv[h][d];
+            xv[h][d] = u32x4{c.x - (b + (v.x & 0xFFFFu)), c.y - (b + (v.x >> 16)), c.z - (b + (v.y & 0xFFFFu)),
+                             c.w - (b + (v.y >> 16))};
+          }
+        }
         if (qt) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const uint32_t p = 4 * qj + (uint32_t)k;
             const bool inr = p - rel0 < n0;  // (unsigned: p < rel0 wraps)
-            const uint32_t x0 = xv[h][0][k];
+            const uint32_t x0 = LAG ? cv[h][k] : xv[h][0][k];  // AM_PK_ESC: escaped
             const bool e = x0 == AM_PK_ESC;
             uint32_t over = 0;
 #pragma unroll
@@ -743,7 +770,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
     // the next block's reads: statuses, hand-offs, positions (its metadata has arrived by now;
     // the slots are free once scanned)
     wave_sync();
-    own = q_publish<DMAX>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
+    own = q_publish<DMAX, LAG>(L, R, u, nd, m, b0 + step + lane < nsel, accept, next, slot, lane, any);
     wave_sync();
     PH(1);
 
@@ -796,8 +823,10 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
     }
     if (esc) {  // rare: ops outside the packed view, from the full columns
       uint64_t ek = 0;  // included set ops among them: the records are redone with them
+      // the view that flagged them: the quad scan's lag_ct (LAG) or the lane's packed entries
+      const uint32_t *escv = (LAG && (tk & QT_QUAD)) ? L.lag_ct : L.pk_vc;
       for (uint64_t p = off0; p < off1; ++p) {
-        if (L.pk_vc[p] != AM_PK_ESC) continue;
+        if (escv[p] != AM_PK_ESC) continue;
         uint64_t sv[DMAX], ct;
         uint32_t meta;
         esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
@@ -851,14 +880,14 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
   PH_END();
 }
 
-template <int D>
-int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
-             uint32_t accept, bool general) {
+template <int D, bool LAG>
+int launch_dl(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
+              uint32_t accept, bool general) {
   static int occ_g = 0, occ_q = 0;
   int &occ = general ? occ_g : occ_q;
   if (!occ) {
     const hipError_t e = general ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane_g<D>, LBLOCK, 0)
-                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane_q<D, false>, LBLOCK, 0);
+                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_lane_q<D, false, LAG>, LBLOCK, 0);
     if (e != hipSuccess || occ < 1) occ = 2;
   }
   uint64_t blocks = (B->n_reads + LBLOCK - 1) / LBLOCK, cap = (uint64_t)ctx->n_cu * occ;
@@ -867,13 +896,21 @@ int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_re
   if (general)
     hipLaunchKernelGGL((k_lane_g<D>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next, accept);
   else if (S.idx)
-    hipLaunchKernelGGL((k_lane_q<D, true>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next,
-                       accept);
+    hipLaunchKernelGGL((k_lane_q<D, true, LAG>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S,
+                       next, accept);
   else
-    hipLaunchKernelGGL((k_lane_q<D, false>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S, next,
-                       accept);
+    hipLaunchKernelGGL((k_lane_q<D, false, LAG>), dim3((unsigned)blocks), dim3(LBLOCK), 0, ctx->stream, *L, *B, *R, S,
+                       next, accept);
   AM_HIP(hipGetLastError());
   return AM_OK;
+}
+// the quad scan reads the lag view (4 + 2 D bytes per op instead of 4 D) where the store has one
+template <int D>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,
+             uint32_t accept, bool general) {
+  if constexpr (D <= 16 && AM_LANE_LAG)
+    if (!general && L->lag_ct && L->lag && L->key_lag) return launch_dl<D, true>(ctx, L, B, R, S, next, accept, general);
+  return launch_dl<D, false>(ctx, L, B, R, S, next, accept, general);
 }
 
 int launch_g(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next,

@@ -149,31 +149,35 @@ def set_view_bytes(mat, dlog, ko, kt):
     return float((off1 - off0)[quad].sum()) * GMASK_BYTES + float(nrec[~quad].sum()) * REC_BYTES
 
 
-def lag_split(cfg, dlog, base, index_level) -> bool:
-    """Whether the set reads of this step stream the lag view (am_op_log.lag_ct / lag / key_lag:
-    4 + 2 D bytes of commit vector per op, 4 D of lag bases per read): the split fresh read of a
-    single-type set batch (k_grp_incl) over a store without a zone index at D <= 8."""
-    return (base == "fresh" and index_level == abi.AM_INDEX_NONE and cfg["n_dc"] <= 8
-            and cfg["type"] in (abi.AM_AWSET, abi.AM_MVREG) and bool(dlog.lag_ct))
+def lag_split(cfg, dlog, base=None, index_level=None) -> bool:
+    """Whether this step's commit vectors are counted at the lag view's size (am_op_log.lag_ct /
+    lag / key_lag: 4 + 2 D bytes per op, 4 D of lag bases per read) instead of the packed view's
+    4 D per op.  The store has a lag view at D <= 16, and every tier that reads commit vectors
+    reads it (the split and wave set reads, the workgroup tier, the lane tier's quad scan, the
+    bounded-counter rows / wave at D > 8, the big-read inclusion pass) except the PN / LWW
+    stream and row tiers, the lanes' longer reads and the bounded-counter runs: a single-type
+    PN / LWW config keeps the packed size; a mixed config counts every op at the lag size, a
+    lower bound on what its packed-view tiers stream (frac conservative)."""
+    return bool(dlog.lag_ct) and cfg["n_dc"] <= 16 and cfg["type"] not in (abi.AM_PN, abi.AM_LWW)
 
 
 def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None, lag=False):
     """Algorithmic bytes of one am_materialize over every key of the store (the layout model:
-    what the kernels must stream of this build's HBM layout).  lag: the set reads
-    stream the lag view instead of the packed commit vectors (lag_split)."""
+    what the kernels must stream of this build's HBM layout).  lag: the commit
+    vectors are counted at the lag view's size (lag_split)."""
     lens = np.diff(ko.astype(np.int64))
     records = packed and bool(dlog.rec_key_off)
     total = set_view_bytes(mat, dlog, ko, kt) if records else float(dlog.n_var) * 8
     set_len = reads.set_len.cpu().numpy() if reads.set_len is not None else None
+    D = cfg["n_dc"]
     for t in sorted(set(int(x) for x in np.unique(kt))):
         m = kt == t
-        if lag and t in (abi.AM_AWSET, abi.AM_MVREG):  # lag_ct 4 + lags 2 D per op, lag bases 4 D per read
-            total += float(lens[m].sum()) * (4 + 2 * cfg["n_dc"]) + float(m.sum()) * 4 * cfg["n_dc"]
-        else:
-            total += float(lens[m].sum()) * bytes_per_op(t, cfg["n_dc"], packed)
+        total += float(lens[m].sum()) * bytes_per_op(t, D, packed)
+        if lag:  # lag_ct 4 + lags 2 D per op instead of 4 D, lag bases 4 D per read
+            total += float(lens[m].sum()) * (4 + 2 * D - 4 * D) + float(m.sum()) * 4 * D
         sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER)) \
             else 0.0
-        total += float(m.sum()) * (bytes_per_key(t, cfg["n_dc"], sl) + (8 if packed else 0))
+        total += float(m.sum()) * (bytes_per_key(t, D, sl) + (8 if packed else 0))
     return total
 
 
@@ -507,13 +511,13 @@ def measure(st: Step, base: str, steps: int, warmup: int, barrier, pg, timed_wal
     kern_ms = float(np.mean(kern_ev))
     cfg = st.cfg
     packed = bool(st.dlog.pk_vc)
-    alg_bytes = workload_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, packed, mat,
-                               lag=lag_split(cfg, st.dlog, base, st.index_level))
+    lag = packed and lag_split(cfg, st.dlog)
+    alg_bytes = workload_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, packed, mat, lag=lag)
     if base == "cached":
         alg_bytes += cached_bytes(cfg, st.pre, st.reads)
     # the commit vectors of ops whose zone decided them are not streamed, nor the records whose
     # zones' group summaries stood in for them (4 B per record out, 4 B per summary word in)
-    alg_bytes -= skipped * bytes_per_vc(cfg["n_dc"], packed)
+    alg_bytes -= skipped * ((4 + 2 * cfg["n_dc"]) if lag else bytes_per_vc(cfg["n_dc"], packed))
     alg_bytes += 4.0 * (gsw - rskip)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     logical = logical_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, cached=base == "cached")
@@ -648,7 +652,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
-                              "commit vectors (packed: 4*D per op; lag view: 4 + 2*D per op and 4*D per read), "
+                              "commit vectors (packed: 4*D per op; lag view, every set / mixed config at D <= 16: "
+                              "4 + 2*D per op and 4*D per read), "
                               "payload, 4 B per token-group record or 8 B per group-mask op, per-read metadata and "
                               "outputs; every op streamed (no zone index)"
                               if level == abi.AM_INDEX_NONE else
@@ -668,7 +673,7 @@ def main():
                      "ops_skipped_per_launch": m["skipped"], "records_skipped_per_launch": m["rskip"],
                      "gsum_words_per_launch": m["gsw"],
                      "layout": ("lag view (u32 commit time + u16 lag per DC, relative to per-key bases)"
-                                if lag_split(cfg, st.dlog, args.base, level) else
+                                if lag_split(cfg, st.dlog) else
                                 "packed (u32 commit vectors relative to a per-key time base)")
                                + "; set effects as u32 token-group records" if m["packed"] else "full"},
         "cpu_baseline": None,

@@ -65,13 +65,17 @@ def test_fullpop_config(mat, cfg_name, escape):
 
         if cfg_name == "c4" and not escape:
             # a planted one-op change: the oldest op of a PN key leaves the snapshot (its DC-0
-            # packed entry above every threshold); the comparator must flag that key alone
+            # packed entry, and its lag view commit entry where the store has one, above every
+            # threshold); the comparator must flag that key alone
             k = int(np.nonzero((kt == abi.AM_PN) & (dev["count"] > 0) & (lens > 0))[0][1000])
             pos = int(ko[k])
             stride = dlog.snap_stride or dlog.n_ops
             v = np.array([0xFFFFFFFE], np.uint32)
             abi.check(mat.L.am_memcpy_h2d(mat.ctx, ctypes.c_void_p(dlog.pk_vc + 4 * (0 * stride + pos)),
                                           v.ctypes.data, 4), "am_memcpy_h2d")
+            if dlog.lag_ct:
+                abi.check(mat.L.am_memcpy_h2d(mat.ctx, ctypes.c_void_p(dlog.lag_ct + 4 * pos), v.ctypes.data, 4),
+                          "am_memcpy_h2d")
             mat.sync()
             dev2 = _device_read(mat, dlog, p, kt, cfg, clock)
             k0 = max(0, k - 100)
