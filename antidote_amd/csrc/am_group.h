@@ -1282,8 +1282,11 @@ __device__ __forceinline__ uint32_t incl_tile_lag(const uint32_t (&c)[4], const 
 // LAG: the read streams the lag view (am_op_log.lag_ct / lag / key_lag, 4 + 2 D bytes per op)
 // and rebuilds each packed entry X[d] - K = lag_ct - key_lag[d] - lag[d] in u32 (exact: the entry
 // fits u32 for every op the view holds); else the packed view (4 D bytes per op)
+#ifndef AM_INCL_WAVES
+#define AM_INCL_WAVES 3  // waves per SIMD: the pipelined tile loop holds two tiles (168 VGPRs)
+#endif
 template <int DMAX, int TYPE, bool EXACT, bool LAG>
-__global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+__global__ void __launch_bounds__(BLOCK, AM_INCL_WAVES) k_grp_incl(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                        am_retry next, uint32_t short_opl, uint32_t *ibm) {
   constexpr int OPL = 4;
   constexpr uint64_t TILE = (uint64_t)WAVE * OPL;
@@ -1350,35 +1353,8 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
       uint32_t cnt = 0, minex = 0xFFFFFFFFu, anyc = 0, anyesc = 0;
       uint64_t escm = 0;  // the lane's escaped ops: bit OPL * tile + k (the first 64 / OPL tiles)
       const uint64_t t0 = off0 & ~31ull;  // 32-op aligned: lane groups of LPW fill whole bitmap words
-      for (uint64_t t = t0; t < off1; t += TILE) {
-        const uint64_t g = t + (uint64_t)lane * OPL;
-        uint32_t esc = 0, cand = 0, ib;
-        const bool whole = t >= off0 && t + TILE <= off1;
-        if constexpr (LAG) {
-          static_assert(OPL == 4, "four u16 lags per 8-byte load");
-          uint32_t c[OPL] = {};
-          if (g < off1) ld_n32<OPL>(L.lag_ct + g, c);
-          uint2 lv[DMAX];
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            lv[d] = uint2{0, 0};
-            if (d < (int)nd && g < off1) lv[d] = *(const uint2 *)(L.lag + (uint64_t)d * stride + g);
-          }
-          // (pad DCs d >= nd: c - lb[d] with lb = 0 lies under the always-passing pad threshold)
-          ib = whole ? incl_tile_lag<DMAX, false>(c, lv, lb, pk, g, off0, off1, mx, esc, cand)
-                     : incl_tile_lag<DMAX, true>(c, lv, lb, pk, g, off0, off1, mx, esc, cand);
-        } else {
-          uint32_t x[OPL][DMAX];
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d) {
-            uint32_t q[OPL] = {};
-            if (d < (int)nd && g < off1) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
-#pragma unroll
-            for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
-          }
-          ib = whole ? incl_tile<DMAX, OPL, false>(x, pk, g, off0, off1, mx, esc, cand)
-                     : incl_tile<DMAX, OPL, true>(x, pk, g, off0, off1, mx, esc, cand);
-        }
+      // one tile's inclusion bits -> partials, escape marks and the bitmap words
+      auto tile_out = [&](uint64_t t, uint64_t g, uint32_t ib, uint32_t esc, uint32_t cand) {
         if (pk.never) ib = 0;
         cnt += (uint32_t)__popc(ib);
         anyc |= cand;
@@ -1401,6 +1377,59 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_incl(am_op_log L, am_read_batc
             atomicAnd(ibm + (w0 >> 5), ~mask);
             atomicOr(ibm + (w0 >> 5), word & mask);
           }
+        }
+      };
+      if constexpr (LAG) {
+        static_assert(OPL == 4, "four u16 lags per 8-byte load");
+        // software-pipelined: tile t + 1's loads are issued before tile t is evaluated, into the
+        // other of two register sets (no copies between them: a copy would wait for the loads)
+        uint32_t cA[OPL], cB[OPL];
+        uint2 lA[DMAX], lB[DMAX];
+        auto load = [&](uint64_t t, uint32_t (&c)[OPL], uint2 (&lv)[DMAX]) {
+          const uint64_t g = t + (uint64_t)lane * OPL;
+#pragma unroll
+          for (int k = 0; k < OPL; ++k) c[k] = 0;
+          if (g < off1) ld_n32<OPL>(L.lag_ct + g, c);
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            lv[d] = uint2{0, 0};
+            if (d < (int)nd && g < off1) lv[d] = *(const uint2 *)(L.lag + (uint64_t)d * stride + g);
+          }
+        };
+        auto eval = [&](uint64_t t, const uint32_t (&c)[OPL], const uint2 (&lv)[DMAX]) {
+          const uint64_t g = t + (uint64_t)lane * OPL;
+          uint32_t esc = 0, cand = 0;
+          const bool whole = t >= off0 && t + TILE <= off1;
+          // (pad DCs d >= nd: c - lb[d] with lb = 0 lies under the always-passing pad threshold)
+          const uint32_t ib = whole ? incl_tile_lag<DMAX, false>(c, lv, lb, pk, g, off0, off1, mx, esc, cand)
+                                    : incl_tile_lag<DMAX, true>(c, lv, lb, pk, g, off0, off1, mx, esc, cand);
+          tile_out(t, g, ib, esc, cand);
+        };
+        load(t0, cA, lA);
+        for (uint64_t t = t0; t < off1; t += 2 * TILE) {
+          const uint64_t t1 = t + TILE;
+          if (t1 < off1) load(t1, cB, lB);
+          eval(t, cA, lA);
+          if (t1 >= off1) break;
+          if (t1 + TILE < off1) load(t1 + TILE, cA, lA);
+          eval(t1, cB, lB);
+        }
+      } else {
+        for (uint64_t t = t0; t < off1; t += TILE) {
+          const uint64_t g = t + (uint64_t)lane * OPL;
+          uint32_t esc = 0, cand = 0;
+          const bool whole = t >= off0 && t + TILE <= off1;
+          uint32_t x[OPL][DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            uint32_t q[OPL] = {};
+            if (d < (int)nd && g < off1) ld_n32<OPL>(L.pk_vc + (uint64_t)d * stride + g, q);
+#pragma unroll
+            for (int k = 0; k < OPL; ++k) x[k][d] = q[k];
+          }
+          const uint32_t ib = whole ? incl_tile<DMAX, OPL, false>(x, pk, g, off0, off1, mx, esc, cand)
+                                    : incl_tile<DMAX, OPL, true>(x, pk, g, off0, off1, mx, esc, cand);
+          tile_out(t, g, ib, esc, cand);
         }
       }
       // ---- the read's scalar outputs: LastOpCt maxima reduced through LDS (lane 8 d + c takes
