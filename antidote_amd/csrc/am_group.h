@@ -805,6 +805,12 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
 // BM (the split fresh read, after k_grp_incl): the inclusion bits come from the global bitmap
 // ibm (bit p = op slot p) and the scalar outputs are already written; this pass streams the
 // records and gathers the survivors only.
+#ifndef AM_WAVE_FRESH_LAG
+#define AM_WAVE_FRESH_LAG 0
+#endif
+#ifndef AM_WAVE_ZONE_LAG
+#define AM_WAVE_ZONE_LAG 0
+#endif
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT, bool BM = false>
 __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
                                                                   am_sel S, am_retry next, uint32_t short_opl,
@@ -904,8 +910,14 @@ __global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batc
       // ---- 1. inclusion per op -> the wave's bitmap + per-lane scalar partials ----
       PkRead<DMAX> pk;
       if (PACKED) pk_setup(u, nd, uniform_u64(s.slot[j].K), pk);
-      LagRead<DMAX> lr;  // the lag view: 4 + 2 D bytes per op instead of 4 D
-      lag_setup(L, nd, uniform_u64(s.slot[j].key), PACKED && L.lag_ct != nullptr, lr);
+      // the lag view (4 + 2 D bytes per op instead of 4 D): the cached (GENERAL) reads of a store
+      // without a zone index.  Not the fresh variant (128 VGPRs: its lag branch spilled 39, the
+      // indexed fresh C3 read 4.3 -> 6.4 ms) nor zone-indexed reads (their exact zones skip most
+      // commit vectors; the per-read lag bases are one more dependent load round)
+      LagRead<DMAX> lr;
+      lag_setup(L, nd, uniform_u64(s.slot[j].key),
+                PACKED && (GENERAL || AM_WAVE_FRESH_LAG) && L.lag_ct != nullptr && (AM_WAVE_ZONE_LAG || !L.zone_vc),
+                lr);
       AccP<DMAX> ap;
       Acc<DMAX> a;
       ap.reset();

@@ -149,16 +149,18 @@ def set_view_bytes(mat, dlog, ko, kt):
     return float((off1 - off0)[quad].sum()) * GMASK_BYTES + float(nrec[~quad].sum()) * REC_BYTES
 
 
-def lag_split(cfg, dlog, base=None, index_level=None) -> bool:
+def lag_split(cfg, dlog, index_level) -> bool:
     """Whether this step's commit vectors are counted at the lag view's size (am_op_log.lag_ct /
     lag / key_lag: 4 + 2 D bytes per op, 4 D of lag bases per read) instead of the packed view's
-    4 D per op.  The store has a lag view at D <= 16, and every tier that reads commit vectors
-    reads it (the split and wave set reads, the workgroup tier, the lane tier's quad scan, the
-    bounded-counter rows / wave at D > 8, the big-read inclusion pass) except the PN / LWW
-    stream and row tiers, the lanes' longer reads and the bounded-counter runs: a single-type
-    PN / LWW config keeps the packed size; a mixed config counts every op at the lag size, a
-    lower bound on what its packed-view tiers stream (frac conservative)."""
-    return bool(dlog.lag_ct) and cfg["n_dc"] <= 16 and cfg["type"] not in (abi.AM_PN, abi.AM_LWW)
+    4 D per op.  The store has a lag view at D <= 16.  It is read by the split fresh set read,
+    the cached (general) wave tier, the workgroup set tier, the lane tier's quad scan, the
+    big-read inclusion pass and the bounded-counter wave at D > 8; the PN / LWW stream and row
+    tiers, the fresh wave tier, the lanes' longer reads, the bounded-counter rows and runs and
+    every zone-indexed read keep the packed view.  So: a single-type PN / LWW config or a
+    zone-indexed store counts the packed size; a set or mixed config counts every op at the lag
+    size, a lower bound on what its packed-view tiers stream (frac conservative)."""
+    return (bool(dlog.lag_ct) and cfg["n_dc"] <= 16 and cfg["type"] not in (abi.AM_PN, abi.AM_LWW)
+            and index_level == abi.AM_INDEX_NONE)
 
 
 def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None, lag=False):
@@ -511,7 +513,7 @@ def measure(st: Step, base: str, steps: int, warmup: int, barrier, pg, timed_wal
     kern_ms = float(np.mean(kern_ev))
     cfg = st.cfg
     packed = bool(st.dlog.pk_vc)
-    lag = packed and lag_split(cfg, st.dlog)
+    lag = packed and lag_split(cfg, st.dlog, st.index_level)
     alg_bytes = workload_bytes(cfg, st.dlog, st.ko, st.kt, st.reads, packed, mat, lag=lag)
     if base == "cached":
         alg_bytes += cached_bytes(cfg, st.pre, st.reads)
@@ -652,7 +654,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
-                              "commit vectors (packed: 4*D per op; lag view, every set / mixed config at D <= 16: "
+                              "commit vectors (packed: 4*D per op; lag view, set / mixed configs at D <= 16 without a zone index: "
                               "4 + 2*D per op and 4*D per read), "
                               "payload, 4 B per token-group record or 8 B per group-mask op, per-read metadata and "
                               "outputs; every op streamed (no zone index)"
@@ -673,7 +675,7 @@ def main():
                      "ops_skipped_per_launch": m["skipped"], "records_skipped_per_launch": m["rskip"],
                      "gsum_words_per_launch": m["gsw"],
                      "layout": ("lag view (u32 commit time + u16 lag per DC, relative to per-key bases)"
-                                if lag_split(cfg, st.dlog) else
+                                if lag_split(cfg, st.dlog, level) else
                                 "packed (u32 commit vectors relative to a per-key time base)")
                                + "; set effects as u32 token-group records" if m["packed"] else "full"},
         "cpu_baseline": None,

@@ -2,7 +2,7 @@
 # One GPU iteration on one box: optional GPU tests of the in-tree library, then interleaved A/B
 # rounds of library variants (scripts/build_variant.sh -> scripts/ab/lib_<V>.so) per config.
 #   TESTS="tests/test_gpu_zones.py ..."   pytest targets first (empty: skip; "all": tests -m gpu)
-#   AB="c3:cur,new:2 c4:cur,new:1:--base cached"   CFG:VARIANTS:ROUNDS[:bench args] per entry
+#   AB="c3:cur,new:2 c4:cur,new:1:--base=cached,--index=summaries"   CFG:VARIANTS:ROUNDS[:bench args, comma-separated]
 #   PMC="c4:cur,new"                       optional SQ counter passes (scripts/pmc_sq.sh)
 # Every step is time-limited; a failing test run stops the iteration; the in-tree library is
 # restored at the end.  Results land in gpurun_out/ (steps.log, ab_*.json).
@@ -20,7 +20,7 @@ fi
 cp antidote_amd/libantidote_mat.so /tmp/intree.so
 for spec in ${AB:-}; do
   IFS=: read -r cfg vars rounds extra <<< "$spec"
-  VARS="${vars//,/ }" CFG=$cfg ROUNDS=${rounds:-2} BENCH_EXTRA="${extra:-}" bash scripts/ab_libs.sh || exit $?
+  VARS="${vars//,/ }" CFG=$cfg ROUNDS=${rounds:-2} BENCH_EXTRA="${extra//,/ }" bash scripts/ab_libs.sh || exit $?
 done
 for spec in ${PMC:-}; do
   IFS=: read -r cfg vars <<< "$spec"
