@@ -149,34 +149,60 @@ def set_view_bytes(mat, dlog, ko, kt):
     return float((off1 - off0)[quad].sum()) * GMASK_BYTES + float(nrec[~quad].sum()) * REC_BYTES
 
 
+GRP_MAX_REC = 2048          # include/antidote_mat.h AM_GRP_MAX_REC
+BIG_MIN_OPS = GRP_MAX_REC // 2  # AM_BIG_MIN_OPS: an MV key above it reads through the big-read tier
+ROWS_BC = 48                # am_plan.hip: bounded-counter reads up to 48 ops take the row tier
+BCWAVE_OPS = 4096           # am_internal.h AM_BCWAVE_OPS: the bounded-counter wave tier's limit
+
+
 def lag_split(cfg, dlog, index_level) -> bool:
-    """Whether this step's commit vectors are counted at the lag view's size (am_op_log.lag_ct /
-    lag / key_lag: 4 + 2 D bytes per op, 4 D of lag bases per read) instead of the packed view's
-    4 D per op.  The store has a lag view at D <= 16.  It is read by the split fresh set read,
-    the cached (general) wave tier, the workgroup set tier, the lane tier's quad scan, the
-    big-read inclusion pass and the bounded-counter wave at D > 8; the PN / LWW stream and row
-    tiers, the fresh wave tier, the lanes' longer reads, the bounded-counter rows and runs and
-    every zone-indexed read keep the packed view.  So: a single-type PN / LWW config or a
-    zone-indexed store counts the packed size; a set or mixed config counts every op at the lag
-    size, a lower bound on what its packed-view tiers stream (frac conservative)."""
+    """Whether this step streams the lag view (am_op_log.lag_ct / lag / key_lag: 4 + 2 D bytes
+    of commit vector per op, 4 D of lag bases per read) anywhere: the store has one (D <= 16),
+    no zone index (zone-indexed reads keep the packed view), and the config holds set or
+    bounded-counter keys (the PN / LWW stream and row tiers keep the packed view)."""
     return (bool(dlog.lag_ct) and cfg["n_dc"] <= 16 and cfg["type"] not in (abi.AM_PN, abi.AM_LWW)
             and index_level == abi.AM_INDEX_NONE)
 
 
+def lag_keys(cfg, dlog, ko, kt, mat):
+    """The keys whose reads stream the lag view, by the tier the planner gives them (am_plan.hip):
+    a single-type set config: every key (the split fresh read; the cached wave tier); a mixed
+    config: the lane tier's quad reads (at most 16 ops from the aligned start; sets at most 32
+    groups), MV keys in the big view (the big-read inclusion pass), bounded-counter reads of
+    the wave tier at D > 8 (49 .. 4096 ops).  The rest (the lanes' longer reads, the fresh
+    wave and workgroup set tiers' reads, the row tiers, the bounded-counter runs) are counted
+    at the packed size."""
+    n = len(kt)
+    if cfg["type"] in (abi.AM_AWSET, abi.AM_MVREG):
+        return np.ones(n, bool)
+    off0, off1 = ko[:-1].astype(np.int64), ko[1:].astype(np.int64)
+    lens = off1 - off0
+    sets = (kt == abi.AM_AWSET) | (kt == abi.AM_MVREG)
+    short = off1 <= (off0 & ~3) + 16
+    ng = np.zeros(n, np.uint32)
+    if dlog.key_ngrp:
+        abi.check(mat.L.am_memcpy_d2h(mat.ctx, ng.ctypes.data, dlog.key_ngrp, ng.nbytes), "d2h key_ngrp")
+    quad = short & (~sets | ((ng <= 32) & bool(dlog.gmask))) & (kt != abi.AM_BCOUNTER)
+    big_mv = (kt == abi.AM_MVREG) & (lens > BIG_MIN_OPS)
+    bc_wave = (kt == abi.AM_BCOUNTER) & (lens > ROWS_BC) & (lens <= BCWAVE_OPS) & (cfg["n_dc"] > 8)
+    return quad | big_mv | bc_wave
+
+
 def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None, lag=False):
     """Algorithmic bytes of one am_materialize over every key of the store (the layout model:
-    what the kernels must stream of this build's HBM layout).  lag: the commit
-    vectors are counted at the lag view's size (lag_split)."""
+    what the kernels must stream of this build's HBM layout).  lag: the keys of
+    lag_keys stream the lag view's commit vectors instead of the packed ones."""
     lens = np.diff(ko.astype(np.int64))
     records = packed and bool(dlog.rec_key_off)
     total = set_view_bytes(mat, dlog, ko, kt) if records else float(dlog.n_var) * 8
     set_len = reads.set_len.cpu().numpy() if reads.set_len is not None else None
     D = cfg["n_dc"]
+    lk = lag_keys(cfg, dlog, ko, kt, mat) if lag else np.zeros(len(kt), bool)
     for t in sorted(set(int(x) for x in np.unique(kt))):
         m = kt == t
         total += float(lens[m].sum()) * bytes_per_op(t, D, packed)
-        if lag:  # lag_ct 4 + lags 2 D per op instead of 4 D, lag bases 4 D per read
-            total += float(lens[m].sum()) * (4 + 2 * D - 4 * D) + float(m.sum()) * 4 * D
+        # lag view: lag_ct 4 + lags 2 D per op instead of 4 D, lag bases 4 D per read
+        total += float(lens[m & lk].sum()) * (4 + 2 * D - 4 * D) + float((m & lk).sum()) * 4 * D
         sl = float(set_len[m].mean()) if (set_len is not None and t in (abi.AM_AWSET, abi.AM_MVREG, abi.AM_BCOUNTER)) \
             else 0.0
         total += float(m.sum()) * (bytes_per_key(t, D, sl) + (8 if packed else 0))
@@ -654,8 +680,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "model": "layout bytes (DESIGN.md 4): what the kernels stream of this build's HBM layout -- "
-                              "commit vectors (packed: 4*D per op; lag view, set / mixed configs at D <= 16 without a zone index: "
-                              "4 + 2*D per op and 4*D per read), "
+                              "commit vectors (packed: 4*D per op; lag view, for the reads of the tiers that stream it "
+                              "(bench.lag_keys): 4 + 2*D per op and 4*D per read), "
                               "payload, 4 B per token-group record or 8 B per group-mask op, per-read metadata and "
                               "outputs; every op streamed (no zone index)"
                               if level == abi.AM_INDEX_NONE else

@@ -22,6 +22,7 @@ for s in $STEPS; do
     pmccached)
            timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmcf_c3_cached -o pmc --output-format csv -- python bench.py --base cached --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmcf_c3_cached.log 2>&1; ok $? pmcf_c3_cached
            timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw_c3_cached -o pmc --output-format csv -- python bench.py --base cached --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmcw_c3_cached.log 2>&1; ok $? pmcw_c3_cached ;;
+    escape) for spec in ${ESC_SPECS:-c3:0.01 c3:0.1 c2:0.1 c4:0.1 c5:0.1}; do c=${spec%%:*}; e=${spec#*:}; timeout -k 10 300 python bench.py --config $c --escape $e --no-secondary --no-cpu-baseline > $OUT/esc_${c}_$e.json 2> $OUT/esc_${c}_$e.err; ok $? esc_${c}_$e; done ;;
     ingest) timeout -k 10 400 python scripts/bench_ingest.py ${INGEST_ARGS:-} > $OUT/ingest.json 2> $OUT/ingest.err; ok $? ingest ;;
     prof) for c in ${PROF_CFGS:-c2 c3 c4 c5}; do timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline ${PROF_ARGS:-} > $OUT/prof_$c.json 2> $OUT/prof_$c.log; ok $? prof_$c; done ;;
     pmc) for c in ${PMC_CFGS:-c4 c5}; do
