@@ -716,6 +716,7 @@ def main():
         mc = measure(st, "cached", ksteps, 2, barrier, pg)
         sec["c3_cached"] = summary(st, mc, world, "c3 --base cached: read/6 through the device snapshot cache "
                                                   "(q = 0.5 bases), materialize/4, write-back")
+        sec["c3_cached"]["traffic"] = load_traffic("c3_cached", f"c3: {CONFIGS['c3']['desc']}", "none")
         # the zone index: its build cost, and what it buys a fresh and a cached read
         ims = st.reindex(abi.AM_INDEX_SUMMARIES)
         mi = measure(st, "fresh", ksteps, 2, barrier, pg)
