@@ -66,8 +66,14 @@ __device__ __forceinline__ uint32_t row_max_u32(uint32_t v) {
   return v;
 }
 
+#ifndef AM_BCR_PREFETCH
+#define AM_BCR_PREFETCH 1  // the next read's first window loaded while this read is evaluated
+#endif
+#ifndef AM_BCR_WAVES
+#define AM_BCR_WAVES 1     // waves per SIMD the kernel is compiled for (1: the compiler's choice)
+#endif
 template <int DMAX>
-__global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
+__global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                    am_retry next) {
   __shared__ BcrSmem smem[BLOCK / WAVE];
   BcrSmem &sm = smem[threadIdx.x / WAVE];
@@ -137,82 +143,95 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
     const uint64_t tm = __ballot(take);
     wave_sync();
 
-    // ---- row q reads the batch's reads q, q + 4, ... (every row in lockstep, full EXEC).  The
-    //      first 16 ops of the row's next read are loaded while this one is evaluated (most
-    //      reads have at most 16) ----
-    uint32_t nx[DMAX], nmeta = 0;
-    int64_t namt = 0;
-    uint64_t nft = 0;
-    auto load_op = [&](const BcrIn &w, uint32_t q, uint32_t(&x)[DMAX], uint32_t &meta, int64_t &amt, uint64_t &ft) {
-      const uint64_t p = (w.tk && q < w.nops) ? w.off0 + q : 0;  // (a row without a read loads op 0, unused)
+    // ---- row q reads the batch's reads q, q + 4, ... (every row in lockstep, full EXEC).  Lane
+    //      d of a row holds DC d: a step takes a 16-op window aligned to 4 (four 16-byte loads of
+    //      the DC's packed entries), the window's failures are one row OR of the lanes' fail
+    //      bits, and lane d's LastOpCt entry is its own running maximum.  Lane k applies op k of
+    //      the window.  The next read's first window is loaded while this read is evaluated ----
+    uint64_t vS = 0;  // lane d: the clock entry S[d]
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) x[d] = d < (int)nd ? L.pk_vc[(uint64_t)d * stride + p] : 0u;
-      meta = L.op_meta[p], amt = (int64_t)L.p0[p], ft = L.p1[p];
+    for (int d = 0; d < DMAX; ++d) vS = (uint32_t)d == sl ? u.S[d] : vS;
+    const bool dl = sl < nd;  // the lane holds a DC of the log
+    struct Win {
+      u32x4 e[4];  // DC sl's packed entries of the window's ops 0..15
+      uint32_t meta;
+      int64_t amt;
+      uint64_t ft;  // op sl of the window
     };
-    if (tm) load_op(sm.in[row], sl, nx, nmeta, namt, nft);
+    auto load_win = [&](const BcrIn &w, uint32_t t, Win &x) {
+      const uint64_t wb = (w.off0 & ~3ull) + (uint64_t)RG * t, end = w.off0 + w.nops;
+      const bool any = w.tk != 0 && wb < end;
+      // unpredicated: a quad the read does not need (or a pad lane's) is loaded from the
+      // column's first line and ignored
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint64_t a = (any && dl && wb + 4 * h < end) ? (uint64_t)sl * stride + wb + 4 * h : 0;
+        x.e[h] = *(const u32x4 *)(L.pk_vc + a);
+      }
+      const uint64_t p = wb + sl;
+      const uint64_t pp = (any && p >= w.off0 && p < end) ? p : 0;
+      x.meta = L.op_meta[pp], x.amt = (int64_t)L.p0[pp], x.ft = L.p1[pp];
+    };
+    constexpr uint32_t NST = BCR_OPS / RG + 1;  // windows of a read of <= 64 ops from off0 & ~3
+    Win nx;
+    if (AM_BCR_PREFETCH && tm) load_win(sm.in[row], 0, nx);
     for (uint32_t it = 0; it < WAVE / 4 && (tm >> (4 * it)); ++it) {
       const uint32_t j = 4 * it + row;
       const BcrIn in = sm.in[j];
-      uint32_t cx[DMAX];
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) cx[d] = nx[d];
-      const uint32_t cmeta = nmeta;
-      const int64_t camt = namt;
-      const uint64_t cft = nft;
-      if (it + 1 < WAVE / 4 && (tm >> (4 * (it + 1)))) load_op(sm.in[j + 4], sl, nx, nmeta, namt, nft);
+      const Win cx = nx;
+      if (AM_BCR_PREFETCH && it + 1 < WAVE / 4 && (tm >> (4 * (it + 1)))) load_win(sm.in[j + 4], 0, nx);
       const bool act = in.tk != 0;
-      PkRead<DMAX> pk;
-      pk_setup(u, nd, in.K, pk);
+      const uint64_t a0 = in.off0 & ~3ull, end = in.off0 + in.nops;
+      const uint32_t thr = dl ? pk_clamp(vS, in.K) : AM_PK_ESC;  // pad lanes pass
+      const bool never = miss != 0 || row_or_u32((dl && vS < in.K) ? 1u : 0u) != 0;
       if (sl < NSW + 1) rs.bm[sl] = 0;
       wave_sync();
-      uint32_t mx[DMAX];
+      uint32_t mxl = 0;  // lane d: max X[d] - K of the included ops (packed)
+      uint32_t cnt = 0, fl = 0, mex = 0xFFFFFFFFu, esc = 0;  // cnt, mex: row-uniform
+      uint32_t pslot[NST];
+      int64_t pamt[NST];
+      uint32_t pv = 0;  // pairs held (bit t: op sl of window t)
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) mx[d] = 0;
-      uint32_t cnt = 0, fl = 0, mex = 0xFFFFFFFFu, esc = 0;
-      uint32_t pslot[BCR_OPS / RG];
-      int64_t pamt[BCR_OPS / RG];
-      uint32_t pv = 0;  // pairs held
-#pragma unroll
-      for (uint32_t t = 0; t < BCR_OPS / RG; ++t) {
+      for (uint32_t t = 0; t < NST; ++t) {
         pslot[t] = 0, pamt[t] = 0;
-        if (!__ballot(act && RG * t < in.nops)) continue;
-        const uint32_t q = RG * t + sl;
-        const bool v = act && q < in.nops;
-        uint32_t x[DMAX], meta;
-        int64_t amt;
-        uint64_t ft;
-        if (t == 0) {  // prefetched
+        const uint64_t wb = a0 + (uint64_t)RG * t;
+        if (!__ballot(act && wb < end)) continue;
+        Win x;
+        if (AM_BCR_PREFETCH && t == 0) x = cx;  // prefetched
+        else load_win(in, t, x);
+        uint32_t ob = 0, eb = 0;  // the lane's fail bits; escape marks (lane 0: DC 0 == AM_PK_ESC)
 #pragma unroll
-          for (int d = 0; d < DMAX; ++d) x[d] = cx[d];
-          meta = cmeta, amt = camt, ft = cft;
-        } else {
-          load_op(in, q, x, meta, amt, ft);
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t e = x.e[k >> 2][k & 3];
+          ob |= (uint32_t)(e > thr) << k;
+          eb |= (uint32_t)(e == AM_PK_ESC) << k;
         }
-        if (!v) continue;
-        if (x[0] == AM_PK_ESC) {  // outside the packed view: the row evaluates it below
-          esc |= 1u << t;
-          continue;
+        const uint32_t fail = row_or_u32(ob);
+        const uint32_t em = shfl_u32(eb, row * RG);
+        uint32_t vm = 0;  // the window's ops inside [off0, off1)
+        if (act && wb < end) {
+          const uint32_t lo = in.off0 > wb ? (uint32_t)(in.off0 - wb) : 0u;
+          const uint32_t hi = end - wb < (uint64_t)RG ? (uint32_t)(end - wb) : RG;
+          vm = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
         }
-        uint32_t over = 0;
+        const uint32_t cand = vm & ~em, inc = never ? 0u : cand & ~fail;
+        if (cand) fl |= miss;
+        cnt += (uint32_t)__popc(inc);
+        const uint32_t ex = cand & ~inc;
+        if (ex) mex = min(mex, (uint32_t)(wb - in.off0) + (uint32_t)__builtin_ctz(ex));
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d) over |= __builtin_elementwise_sub_sat(x[d], pk.thr[d]);
-        fl |= pk.miss;
-        if (pk.never || over) {
-          mex = min(mex, q);
-          continue;
-        }
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) mx[d] = max(mx[d], x[d]);
-        ++cnt;
-        const uint32_t kind = AM_META_KIND(meta), from = (uint32_t)(ft & 0xFF), to = (uint32_t)((ft >> 8) & 0xFF);
+        for (int k = 0; k < 16; ++k) mxl = max(mxl, ((inc >> k) & 1u) ? x.e[k >> 2][k & 3] : 0u);
+        if (((vm & em) >> sl) & 1u) esc |= 1u << t;  // op sl escaped: the row evaluates it below
+        if (!((inc >> sl) & 1u)) continue;
+        const uint32_t kind = AM_META_KIND(x.meta), from = (uint32_t)(x.ft & 0xFF), to = (uint32_t)((x.ft >> 8) & 0xFF);
         if (kind > AM_BC_TRANSFER || from >= nd || to >= nd) {  // Type:update/2 would raise
           fl |= FLAG_BAD;
           continue;
         }
         const uint32_t slot = kind == AM_BC_DECREMENT ? np + from : from * nd + (kind == AM_BC_INCREMENT ? from : to);
-        if (amt >= (1ll << 56) || amt < -(1ll << 56)) rs.bm[NSW] = 1;  // exactness of the int64 sums: defer
+        if (x.amt >= (1ll << 56) || x.amt < -(1ll << 56)) rs.bm[NSW] = 1;  // exactness of the int64 sums: defer
         atomicOr(&rs.bm[slot >> 5], 1u << (slot & 31));
-        pslot[t] = slot, pamt[t] = amt, pv |= 1u << t;
+        pslot[t] = slot, pamt[t] = x.amt, pv |= 1u << t;
       }
       // ops outside the packed view, one at a time by the whole row (lane d: DC d)
       uint64_t emx = 0;   // lane d: the max X[d] of the included escaped ops
@@ -220,20 +239,18 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
       for (uint32_t lm = row_or_u32(esc ? 1u << sl : 0u); lm; lm &= lm - 1) {
         const uint32_t owner = (uint32_t)__builtin_ctz(lm);
         for (uint32_t tb = shfl_u32(esc, row * RG + owner); tb; tb &= tb - 1) {
-          const uint32_t t = (uint32_t)__builtin_ctz(tb), q = RG * t + owner;
-          const uint64_t p = in.off0 + q;
+          const uint32_t t = (uint32_t)__builtin_ctz(tb);
+          const uint64_t p = a0 + (uint64_t)RG * t + owner;
+          const uint32_t q = (uint32_t)(p - in.off0);
           const uint64_t *w = esc_row(L, stride, p);  // its escape row, or the columns
           const uint32_t meta = w ? (uint32_t)w[1] : L.op_meta[p], dc = meta & 31u;
-          uint64_t xd = 0, sd = 0;
+          uint64_t xd = 0;
           if (sl < nd) xd = sl == dc ? (w ? w[0] : L.commit_time[p]) : (w ? w[2 + sl] : L.snap_vc[(uint64_t)sl * stride + p]);
-#pragma unroll
-          for (int d = 0; d < DMAX; ++d)
-            if ((uint32_t)d == sl) sd = u.S[d];
-          const bool fail = sl < nd && (!((u.spres >> sl) & 1u) || xd > sd);
-          const bool included = row_or_u32(fail ? 1u : 0u) == 0;
+          const bool failx = sl < nd && (!((u.spres >> sl) & 1u) || xd > vS);
+          const bool included = row_or_u32(failx ? 1u : 0u) == 0;
           if (sl == 0) fl |= miss;
           if (!included) {
-            if (sl == 0) mex = min(mex, q);
+            mex = min(mex, q);
             continue;
           }
           emx = max(emx, xd);
@@ -254,7 +271,7 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
           if (amt >= (1ll << 56) || amt < -(1ll << 56)) rs.bm[NSW] = 1;
           atomicOr(&rs.bm[slot >> 5], 1u << (slot & 31));
 #pragma unroll
-          for (uint32_t tt = 0; tt < BCR_OPS / RG; ++tt)
+          for (uint32_t tt = 0; tt < NST; ++tt)
             if (tt == t) pslot[tt] = slot, pamt[tt] = amt;
           pv |= 1u << t;
         }
@@ -268,7 +285,7 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
       for (uint32_t e = sl; e < ns; e += RG) rs.sum[e] = 0;
       wave_sync();
 #pragma unroll
-      for (uint32_t t = 0; t < BCR_OPS / RG; ++t) {
+      for (uint32_t t = 0; t < NST; ++t) {
         if (!((pv >> t) & 1u)) continue;
         const uint32_t s = pslot[t], w = s >> 5;
         uint32_t rank = 0;
@@ -279,16 +296,10 @@ __global__ void __launch_bounds__(BLOCK) k_bc_rows(am_op_log L, am_read_batch B,
       }
       wave_sync();
       // ---- row reductions (full EXEC) ----
-      const uint32_t count = row_sum_u32(cnt) + ecnt;
+      const uint32_t count = cnt + ecnt;
       const uint32_t flags = row_or_u32(fl);
-      const uint32_t minq = row_min_u32(mex);
-      uint64_t myct = 0;  // lane d: LastOpCt entry d (max X[d] of the included ops)
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        if (d >= (int)nd) continue;
-        const uint32_t m = row_max_u32(mx[d]);
-        if ((uint32_t)d == sl) myct = (count - ecnt) ? in.K + m : 0;
-      }
+      const uint32_t minq = mex;
+      uint64_t myct = (dl && cnt) ? in.K + mxl : 0;  // lane d: LastOpCt entry d
       myct = max(myct, emx);
       int32_t status = (flags & FLAG_BAD) ? AM_ERR_UNEXPECTED_OPERATION : AM_OK;
       uint32_t nent = 0;

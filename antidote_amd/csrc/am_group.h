@@ -811,8 +811,11 @@ __device__ bool base_merge(const am_op_log &L, const am_read_batch &B, am_read_r
 #ifndef AM_WAVE_ZONE_LAG
 #define AM_WAVE_ZONE_LAG 0
 #endif
+#ifndef AM_WAVE_WAVES
+#define AM_WAVE_WAVES 4  // waves per SIMD the wave tier is compiled for
+#endif
 template <int DMAX, int TYPE, bool GENERAL, bool PACKED, bool EXACT, bool BM = false>
-__global__ void __launch_bounds__(BLOCK, 4) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
+__global__ void __launch_bounds__(BLOCK, AM_WAVE_WAVES) k_grp_wave(am_op_log L, am_read_batch B, am_read_result R,
                                                                   am_sel S, am_retry next, uint32_t short_opl,
                                                                   GrpHint H, const uint32_t *ibm = nullptr) {
   constexpr int OPL = vopl<DMAX, PACKED>();
