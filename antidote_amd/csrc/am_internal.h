@@ -102,6 +102,8 @@ constexpr uint32_t AM_ZONE_EXTRA_ROWS = 5;
 // bounded-counter reads of longer logs go to the chunked big-read tier (am_bcwave.hip: a wave
 // streaming 32768 ops alone was the tail of C5 at a 32768 limit)
 constexpr uint64_t AM_BCWAVE_OPS = 4096;
+// the LDS-sort tier (am_sets.hip) hands logs longer than this to the big-read tier whole
+constexpr uint64_t AM_SETS_BIG_OPS = 4096;
 
 void am_set_error(const char *fmt, ...);
 

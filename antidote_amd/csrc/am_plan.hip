@@ -207,8 +207,12 @@ int run_sets_front(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_r
       nx.list = grp_buf + 64;
       rc = am_launch_bcwave(ctx, L, B, R, cur, nx);
       if (rc) return rc;
-      cur.idx = nx.list;
-      cur.range = grp_buf;
+      // the wave tier hands on only logs above AM_BCWAVE_OPS, which the LDS-sort tier would pass
+      // to the big-read tier whole: its list is the big tier's retry list (C5: k_sets over that
+      // list held the bounded-counter chain ~0.25 ms)
+      static_assert(AM_SETS_BIG_OPS <= AM_BCWAVE_OPS, "k_sets would take some of the wave tier's hand-offs");
+      *retry_out = nx;
+      return AM_OK;
     }
   } else if (grp_buf && am_group_applies(L, R, type)) {
     // wave -> lane (or, off the packed view, row) -> workgroup kernels; each hands what it

@@ -40,7 +40,8 @@ constexpr int OPL = 4;
 constexpr uint64_t TILE = (uint64_t)BLOCK * OPL;
 constexpr uint32_t KCAP = 2048;
 constexpr uint32_t BCAP = 1024;
-constexpr uint64_t BIG_OPS = 4 * TILE;  // logs longer than this skip the LDS tier
+constexpr uint64_t BIG_OPS = AM_SETS_BIG_OPS;  // logs longer than this skip the LDS tier
+static_assert(BIG_OPS == 4 * TILE, "the LDS tier takes logs of up to four tiles");
 
 struct Smem {
   uint64_t *ka, *kb;  // kills: token, elem (MV: 0)
