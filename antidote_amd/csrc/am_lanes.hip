@@ -403,6 +403,7 @@ struct QRes {  // the quad's results for the read at position p
   uint64_t w0, w1;                 // PN 128-bit sum (hi, lo) | LWW (ts, value)
   uint32_t incl, born, killed;     // inclusion bits from off0 & ~3; groups born / killed
   uint32_t mex, count, flags;      // oldest excluded op (from off0 & ~3) or ~0; count; flags
+  uint32_t escb;                   // escaped ops (from off0 & ~3): the lane evaluates just these
   uint32_t mx[DMAX];
 };
 constexpr uint32_t QGL = 256;  // survivor-list entries per gather round
@@ -711,7 +712,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
             const bool in = cand && !(ctl & QC_NEVER) && over == 0;
             ib |= (uint32_t)in << k;
             ev |= (uint32_t)cand << k;
-            esc |= (uint32_t)(inr && e);
+            esc |= (uint32_t)(inr && e) << k;
 #pragma unroll
             for (int d = 0; d < DMAX; ++d) mx[d] = max(mx[d], in ? xv[h][d][k] : 0u);
           }
@@ -725,7 +726,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
         qlv.reset();
         if (tb && ty == AM_PN) q_pn(ib, wv[h][0], wv[h][1], qpv);
         if (tl && ty == AM_LWW) q_lww(ib, wv[h][0], wv[h][1], wv[h][2], wv[h][3], qlv);
-        const uint32_t qincl = quad_or_u32(ib << (4 * qj));
+        const uint32_t qincl = quad_or_u32(ib << (4 * qj)), qesc = quad_or_u32(esc << (4 * qj));
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) mx[d] = d < (int)nd ? quad_max_u32(mx[d]) : 0u;
         cnt = quad_sum_u32(cnt);
@@ -759,7 +760,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
           QRes<DMAX> &o = sm.res[i];
           o.w0 = ty == AM_LWW ? qlv.ts : (uint64_t)qpv.hi;
           o.w1 = ty == AM_LWW ? qlv.val : qpv.lo;
-          o.incl = qincl, o.born = born, o.killed = killed, o.mex = mex, o.count = cnt;
+          o.incl = qincl, o.born = born, o.killed = killed, o.mex = mex, o.count = cnt, o.escb = qesc;
           o.flags = fl | (qlv.has ? QF_HAS : 0u);
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) o.mx[d] = mx[d];
@@ -790,6 +791,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
     lv.reset();
     uint64_t incl = 0, born = 0, killed = 0;
     bool esc = false;
+    uint32_t escb = 0;  // a quad read's escaped ops (from a0)
     if (tk & QT_QUAD) {
       const QRes<DMAX> &o = sm.res[me.pos];
       incl = o.incl, born = o.born, killed = o.killed;
@@ -798,6 +800,7 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) ap.mx[d] = o.mx[d];
       esc = (o.flags & QF_ESC) != 0;
+      escb = o.escb;
       if (t == AM_PN) pv.hi = (int64_t)o.w0, pv.lo = o.w1;
       if (t == AM_LWW) lv.ts = o.w0, lv.val = o.w1, lv.has = (o.flags & QF_HAS) ? 1u : 0u;
     } else if (tk_take) {  // longer logs of the lane tier (up to 64 ops / 64 groups)
@@ -823,20 +826,23 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_q(am_op_log L, am_read_batch B,
     }
     if (esc) {  // rare: ops outside the packed view, from the full columns
       uint64_t ek = 0;  // included set ops among them: the records are redone with them
-      // the view that flagged them: the quad scan's lag_ct (LAG) or the lane's packed entries
-      const uint32_t *escv = (LAG && (tk & QT_QUAD)) ? L.lag_ct : L.pk_vc;
-      for (uint64_t p = off0; p < off1; ++p) {
-        if (escv[p] != AM_PK_ESC) continue;
+      auto esc_op = [&](uint64_t p) {
         uint64_t sv[DMAX], ct;
         uint32_t meta;
         esc_load<DMAX>(L, nd, stride, p, sv, ct, meta);
-        if (!eval_op<DMAX, false>(u, meta, ct, sv, u.allmask, false, p, a)) continue;
+        if (!eval_op<DMAX, false>(u, meta, ct, sv, u.allmask, false, p, a)) return;
         if (scal) {
           if (t == AM_PN) pv.add(L.p0[p], 0);
           else lv.add(L.p0[p], L.p1[p]);
         } else if (!(meta & AM_META_BAD)) {
           ek |= 1ull << (p - a0);
         }
+      };
+      if (tk & QT_QUAD) {  // the quad scan marked them
+        for (uint32_t m = escb; m; m &= m - 1) esc_op(a0 + (uint64_t)__builtin_ctz(m));
+      } else {  // the lane's own scan of a longer log: its packed entries flag them
+        for (uint64_t p = off0; p < off1; ++p)
+          if (L.pk_vc[p] == AM_PK_ESC) esc_op(p);
       }
       if (setr && ek) {
         incl |= ek;
