@@ -34,7 +34,7 @@ constexpr uint32_t BCR_OPS = 64;    // 4 steps of 16 ops
 constexpr uint32_t NSW = 9;         // bitmap words: 16 * 16 + 16 = 272 slots
 
 struct BcrIn {  // a taken read of the batch, for the row that reads it
-  uint64_t off0, K, idb, ooff;
+  uint64_t off0, K, idb, ooff, key;
   uint32_t nops, cap, r, tk;
 };
 struct BcrOut {  // its scalar outputs, for the read's lane
@@ -72,7 +72,7 @@ __device__ __forceinline__ uint32_t row_max_u32(uint32_t v) {
 #ifndef AM_BCR_WAVES
 #define AM_BCR_WAVES 1     // waves per SIMD the kernel is compiled for (1: the compiler's choice)
 #endif
-template <int DMAX>
+template <int DMAX, bool LAG>
 __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am_read_batch B, am_read_result R, am_sel S,
                                                    am_retry next) {
   __shared__ BcrSmem smem[BLOCK / WAVE];
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am
         w.ooff = R.value.set_off[r];
         const uint64_t cap = R.value.set_off[r + 1] - w.ooff;
         w.cap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
-        w.r = (uint32_t)r;
+        w.r = (uint32_t)r, w.key = key;
       }
       sm.out[lane].store = 0;
     }
@@ -153,7 +153,9 @@ __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am
     for (int d = 0; d < DMAX; ++d) vS = (uint32_t)d == sl ? u.S[d] : vS;
     const bool dl = sl < nd;  // the lane holds a DC of the log
     struct Win {
-      u32x4 e[4];  // DC sl's packed entries of the window's ops 0..15
+      u32x4 e[4];  // DC sl's packed entries of the window's ops 0..15 (LAG: the ops' lag_ct)
+      uint2 g[4];  // LAG: DC sl's u16 lags of the window's ops
+      uint32_t lb;  // LAG: the key's lag base of DC sl (the read's first window)
       uint32_t meta;
       int64_t amt;
       uint64_t ft;  // op sl of the window
@@ -165,9 +167,16 @@ __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am
       // column's first line and ignored
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        const uint64_t a = (any && dl && wb + 4 * h < end) ? (uint64_t)sl * stride + wb + 4 * h : 0;
-        x.e[h] = *(const u32x4 *)(L.pk_vc + a);
+        if constexpr (LAG) {  // 4 + 2 D bytes per op: the row shares the lag_ct lines
+          const bool in = any && wb + 4 * h < end;
+          x.e[h] = *(const u32x4 *)(L.lag_ct + (in ? wb + 4 * h : 0));
+          x.g[h] = *(const uint2 *)(L.lag + ((in && dl) ? (uint64_t)sl * stride + wb + 4 * h : 0));
+        } else {
+          const uint64_t a = (any && dl && wb + 4 * h < end) ? (uint64_t)sl * stride + wb + 4 * h : 0;
+          x.e[h] = *(const u32x4 *)(L.pk_vc + a);
+        }
       }
+      if (LAG && t == 0) x.lb = (w.tk != 0 && dl) ? (uint32_t)L.key_lag[w.key * nd + sl] : 0u;
       const uint64_t p = wb + sl;
       const uint64_t pp = (any && p >= w.off0 && p < end) ? p : 0;
       x.meta = L.op_meta[pp], x.amt = (int64_t)L.p0[pp], x.ft = L.p1[pp];
@@ -179,6 +188,7 @@ __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am
       const uint32_t j = 4 * it + row;
       const BcrIn in = sm.in[j];
       const Win cx = nx;
+      const uint32_t lb = LAG ? cx.lb : 0u;  // this read's lag base of DC sl
       if (AM_BCR_PREFETCH && it + 1 < WAVE / 4 && (tm >> (4 * (it + 1)))) load_win(sm.in[j + 4], 0, nx);
       const bool act = in.tk != 0;
       const uint64_t a0 = in.off0 & ~3ull, end = in.off0 + in.nops;
@@ -200,14 +210,25 @@ __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am
         if (AM_BCR_PREFETCH && t == 0) x = cx;  // prefetched
         else load_win(in, t, x);
         uint32_t ob = 0, eb = 0;  // the lane's fail bits; escape marks (lane 0: DC 0 == AM_PK_ESC)
+        if constexpr (LAG) {  // X[d] - K = lag_ct - (key_lag[d] + lag[d]); escapes: lag_ct == AM_PK_ESC
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const uint32_t e = x.e[k >> 2][k & 3];
-          ob |= (uint32_t)(e > thr) << k;
-          eb |= (uint32_t)(e == AM_PK_ESC) << k;
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t c = x.e[k >> 2][k & 3], gw = (k & 2) ? x.g[k >> 2].y : x.g[k >> 2].x;
+            const uint32_t e = c - (lb + ((k & 1) ? gw >> 16 : gw & 0xFFFFu));
+            x.e[k >> 2][k & 3] = e;
+            ob |= (uint32_t)(e > thr) << k;
+            eb |= (uint32_t)(c == AM_PK_ESC) << k;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t e = x.e[k >> 2][k & 3];
+            ob |= (uint32_t)(e > thr) << k;
+            eb |= (uint32_t)(e == AM_PK_ESC) << k;
+          }
         }
         const uint32_t fail = row_or_u32(ob);
-        const uint32_t em = shfl_u32(eb, row * RG);
+        const uint32_t em = LAG ? eb : shfl_u32(eb, row * RG);
         uint32_t vm = 0;  // the window's ops inside [off0, off1)
         if (act && wb < end) {
           const uint32_t lo = in.off0 > wb ? (uint32_t)(in.off0 - wb) : 0u;
@@ -350,18 +371,29 @@ __global__ void __launch_bounds__(BLOCK, AM_BCR_WAVES) k_bc_rows(am_op_log L, am
   }
 }
 
-template <int D>
-int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
+template <int D, bool LAG>
+int launch_dl(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
   static int occ = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bc_rows<D>, BLOCK, 0) != hipSuccess || occ < 1))
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_bc_rows<D, LAG>, BLOCK, 0) != hipSuccess || occ < 1))
     occ = 1;
   const uint64_t batches = (B->n_reads + WAVE - 1) / WAVE;
   uint64_t blocks = (batches + BLOCK / WAVE - 1) / (BLOCK / WAVE), cap = (uint64_t)ctx->n_cu * occ;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return AM_OK;
-  hipLaunchKernelGGL((k_bc_rows<D>), dim3((unsigned)blocks), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S, next);
+  hipLaunchKernelGGL((k_bc_rows<D, LAG>), dim3((unsigned)blocks), dim3(BLOCK), 0, ctx->stream, *L, *B, *R, S, next);
   AM_HIP(hipGetLastError());
   return AM_OK;
+}
+
+// the lag view at D > 8 where the store has one (#ifndef AM_BCR_LAG: on)
+#ifndef AM_BCR_LAG
+#define AM_BCR_LAG 1
+#endif
+template <int D>
+int launch_d(am_ctx *ctx, const am_op_log *L, const am_read_batch *B, am_read_result *R, am_sel S, am_retry next) {
+  if constexpr (D > 8 && AM_BCR_LAG)
+    if (L->lag_ct && L->lag && L->key_lag) return launch_dl<D, true>(ctx, L, B, R, S, next);
+  return launch_dl<D, false>(ctx, L, B, R, S, next);
 }
 
 }  // namespace

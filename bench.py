@@ -151,7 +151,6 @@ def set_view_bytes(mat, dlog, ko, kt):
 
 GRP_MAX_REC = 2048          # include/antidote_mat.h AM_GRP_MAX_REC
 BIG_MIN_OPS = GRP_MAX_REC // 2  # AM_BIG_MIN_OPS: an MV key above it reads through the big-read tier
-ROWS_BC = 48                # am_plan.hip: bounded-counter reads up to 48 ops take the row tier
 BCWAVE_OPS = 4096           # am_internal.h AM_BCWAVE_OPS: the bounded-counter wave tier's limit
 
 
@@ -169,9 +168,9 @@ def lag_keys(cfg, dlog, ko, kt, mat):
     a single-type set config: every key (the split fresh read; the cached wave tier); a mixed
     config: the lane tier's quad reads (at most 16 ops from the aligned start; sets at most 32
     groups), MV keys in the big view (the big-read inclusion pass), bounded-counter reads of
-    the wave tier at D > 8 (49 .. 4096 ops).  The rest (the lanes' longer reads, the fresh
-    wave and workgroup set tiers' reads, the row tiers, the bounded-counter runs) are counted
-    at the packed size."""
+    the row and wave tiers at D > 8 (up to 4096 ops).  The rest (the lanes' longer reads, the
+    fresh wave and workgroup set tiers' reads, the PN / LWW row tier, the bounded-counter runs)
+    are counted at the packed size."""
     n = len(kt)
     if cfg["type"] in (abi.AM_AWSET, abi.AM_MVREG):
         return np.ones(n, bool)
@@ -184,8 +183,8 @@ def lag_keys(cfg, dlog, ko, kt, mat):
         abi.check(mat.L.am_memcpy_d2h(mat.ctx, ng.ctypes.data, dlog.key_ngrp, ng.nbytes), "d2h key_ngrp")
     quad = short & (~sets | ((ng <= 32) & bool(dlog.gmask))) & (kt != abi.AM_BCOUNTER)
     big_mv = (kt == abi.AM_MVREG) & (lens > BIG_MIN_OPS)
-    bc_wave = (kt == abi.AM_BCOUNTER) & (lens > ROWS_BC) & (lens <= BCWAVE_OPS) & (cfg["n_dc"] > 8)
-    return quad | big_mv | bc_wave
+    bc_short = (kt == abi.AM_BCOUNTER) & (lens <= BCWAVE_OPS) & (cfg["n_dc"] > 8)
+    return quad | big_mv | bc_short
 
 
 def workload_bytes(cfg, dlog, ko, kt, reads, packed, mat=None, lag=False):
