@@ -1,27 +1,29 @@
 // am_bcrows.hip -- materialize/4 for SHORT bounded-counter reads (antidote_crdt_counter_b:
 // orddict:update_counter on P[{From,To}] and D[Id] is a keyed sum, folded by
 // clocksi_materializer:apply_operations/4, src/clocksi_materializer.erl:113-121), batch clock,
-// packed view, n_dc <= 16: one 16-lane row per read, four reads of a wave at a time.
+// packed or lag view, n_dc <= 16: one 16-lane row per read, four reads of a wave at a time.
 //
 // The general row tier (am_rows.hip) keeps a read's D*D + D slot sums in an LDS array: every
 // read clears all 272 slots (D = 16), adds each included amount with a 64-bit LDS atomic and
 // scans the array to emit -- for reads averaging a few dozen ops that touch a handful of slots --
 // and its full-width per-DC state holds it at one wave per SIMD.  Here a read's result is built
 // from the slots it touches only:
-//   * each lane evaluates up to 4 ops (16-op steps; is_op_in_snapshot/7 on the packed u32
-//     entries against thresholds computed once per read) and keeps its included ops' (slot,
-//     amount) pairs in registers;
-//   * the row marks the touched slots in a 272-bit LDS bitmap (one atomicOr per included op):
-//     the slot's rank among the touched ones is its place in the orddicts' key order (P
-//     {From,To} then D Id), so the result needs no sort;
+//   * lane d of the row holds DC d: a step takes a 16-op window aligned to 4 and loads DC d's
+//     entries of it (four 16-byte loads of the packed view; at D > 8 the lag view: DC d's u16
+//     lags, the commit words shared by the row), so is_op_in_snapshot/7 is one row OR of the
+//     lanes' fail bits per window and lane d's LastOpCt entry is its own running maximum (u32,
+//     relative to the key's time base, no reductions);
+//   * lane k applies op k of the window: the row marks the touched slots in a 272-bit LDS bitmap
+//     (one atomicOr per included op) and keeps its (slot, amount) pairs in registers; the slot's
+//     rank among the touched ones is its place in the orddicts' key order (P {From,To} then
+//     D Id), so the result needs no sort;
 //   * the amounts are summed at their rank in a compact LDS array (<= 64 entries, exact: every
 //     |amount| < 2^56, a larger one defers the read), and lane l emits entries l, l + 16, ...:
 //     its slot is the rank's set bit of the bitmap, its value the sum;
-//   * LastOpCt entries are u32 maxima relative to the key's time base (row DPP reductions),
-//     written by lane d of the row; the scalar outputs go through LDS to the read's lane and
-//     leave with one coalesced store per column.
-// Ops outside the packed view are evaluated from the full columns by the row, one DC per lane.
-// Reads it does not take (> BCR_OPS ops) go to `next`.
+//   * the scalar outputs go through LDS to the read's lane and leave with one coalesced store
+//     per column; the next read's first window is loaded while a read is evaluated.
+// Ops outside the views are evaluated from their escape rows or the full columns by the row,
+// one DC per lane.  Reads it does not take (> BCR_OPS ops) go to `next`.
 #include "am_block.h"
 
 using namespace amk;

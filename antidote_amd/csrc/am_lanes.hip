@@ -373,15 +373,18 @@ __global__ void __launch_bounds__(LBLOCK) k_lane_g(am_op_log L, am_read_batch B,
 //     positions) holds one or two types, and the payload (PN sum / LWW max) and record (sets)
 //     code of a type runs only in the phases that hold it (wave-uniform branches);
 //   * the scan is quad-shaped: the quad at position p scans that read's first 16-op tile, lane j
-//     ops [4j, 4j + 4) -- 64 contiguous bytes per packed column per quad -- with the ops'
-//     payload or records in the same loads; the loads of QPH phases are issued together;
+//     ops [4j, 4j + 4) -- 64 contiguous bytes per packed column per quad, or with the lag view
+//     (LAG) the ops' commit words and 8 bytes of u16 lags per DC, the key's lag bases published
+//     with the read -- with the ops' payload or records in the same loads; the loads of QPH
+//     phases are issued together;
 //   * positions, inclusion bits, groups and the oldest-excluded index are 32-bit in the scan
 //     (the quad takes reads of at most 16 ops and 32 groups; the thresholds S - K are computed
 //     once per read by its lane and published with it); a set read ORs its included ops'
 //     group masks (the gmask view: births | effective kills per op) instead of testing records;
-//   * a read the quad does not take (longer logs up to 64 ops / 64 groups, an escaped op) is
-//     finished by its own lane; results come back through LDS; survivors leave through one
-//     gather per wave; each lane writes its read's outputs (coalesced stores).
+//   * a read the quad does not take (longer logs up to 64 ops / 64 groups) is finished by its
+//     own lane, and so are a quad read's escaped ops, which the quad marks (the lane evaluates
+//     just those); results come back through LDS; survivors leave through one gather per wave;
+//     each lane writes its read's outputs (coalesced stores).
 // phases whose loads are in flight together (2 at D <= 4 measured within noise of 4)
 template <int DMAX>
 constexpr int qph() {
